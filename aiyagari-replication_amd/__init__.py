@@ -1,0 +1,14 @@
+"""MI355X-native (gfx950, fp64) solver for the hot path of kostastril/Aiyagari-Replication.
+
+The MATLAB scripts' inner loops (Bellman sweeps, EGM steps, the Monte-Carlo capital supply,
+the Krusell-Smith improvement/Howard steps) run as hand-written HIP kernels behind the C ABI
+in include/aiyagari_hip.h.  This package is the Python host mirror of that boundary.
+There is no CPU fallback: importing works without a GPU, calling a solver without the HIP
+library or a device raises.
+"""
+from . import calibration
+from ._capi import AiyError, LIB_PATH, declared_symbols, lib
+from .vfi import Workspace, vfi_solve, vfi_sweep
+
+__all__ = ["AiyError", "LIB_PATH", "Workspace", "calibration", "declared_symbols", "lib",
+           "vfi_solve", "vfi_sweep"]

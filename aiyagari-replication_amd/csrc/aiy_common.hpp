@@ -1,0 +1,71 @@
+// Shared host/device plumbing for the gfx950 solver: status + thread-local error text,
+// HIP error checking, small device helpers.  No compatibility layers: CDNA4 only.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include <cstdarg>
+#include <string>
+
+#include "../../include/aiyagari_hip.h"
+#include "aiy_math.h"
+
+namespace aiy {
+
+// ---------------------------------------------------------------- errors (host)
+void set_error(const char* fmt, ...);
+int fail(int code, const char* fmt, ...);
+
+#define AIY_HIP(call)                                                                  \
+    do {                                                                               \
+        hipError_t e_ = (call);                                                        \
+        if (e_ != hipSuccess)                                                          \
+            return ::aiy::fail(AIY_HIP_ERROR, "%s failed: %s (%s:%d)", #call,          \
+                               hipGetErrorString(e_), __FILE__, __LINE__);             \
+    } while (0)
+
+#define AIY_TRY(expr)                \
+    do {                             \
+        int rc_ = (expr);            \
+        if (rc_ != AIY_OK) return rc_; \
+    } while (0)
+
+// ---------------------------------------------------------------- device helpers
+__device__ __forceinline__ int readfirst(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// first k in [0, n) with a[k] >= x  (== count of a[k] < x), a non-decreasing.
+__device__ __forceinline__ int lower_bound_dev(const double* __restrict__ a, int n, double x) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (a[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+// largest i with x[i] <= q clamped to [0, n-2]  (interp1 segment; np_oracle / aiy_oracle
+// use the same rule)
+__device__ __forceinline__ int seg_of_dev(const double* __restrict__ x, int n, double q) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (x[mid] <= q) lo = mid + 1;
+        else hi = mid;
+    }
+    int i = lo - 1;
+    i = i < 0 ? 0 : i;
+    i = i > n - 2 ? n - 2 : i;
+    return i;
+}
+
+// IEEE-ordered key for a non-negative double: uint64 compare == double compare
+__device__ __forceinline__ unsigned long long nonneg_key(double x) {
+    return (unsigned long long)aiy_dbits(x);
+}
+
+inline int is_int_ge(double x, double lo) {
+    return x >= lo && x < 64 && (double)(int64_t)x == x;
+}
+
+}  // namespace aiy

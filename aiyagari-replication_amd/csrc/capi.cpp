@@ -1,0 +1,309 @@
+// C ABI (include/aiyagari_hip.h): workspace management, the device tier (*_dev) and the
+// MATLAB-layout host tier.  Host code only; kernels live in *_kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "aiy_common.hpp"
+#include "ws.hpp"
+
+namespace aiy {
+
+static thread_local std::string g_err;
+
+void set_error(const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+
+int fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+// ---------------------------------------------------------------------------- workspace
+template <class T>
+static int dalloc(T** p, size_t n) {
+    if (*p) return AIY_OK;
+    hipError_t e = hipMalloc((void**)p, std::max<size_t>(n, 1) * sizeof(T));
+    if (e != hipSuccess)
+        return fail(AIY_NO_MEMORY, "hipMalloc(%zu bytes) failed: %s", n * sizeof(T),
+                    hipGetErrorString(e));
+    return AIY_OK;
+}
+template <class T>
+static void dfree(T*& p) {
+    if (p) (void)hipFree((void*)p);
+    p = nullptr;
+}
+
+int ws_ensure_vfi(aiy_ws* ws) {
+    size_t n = (size_t)ws->N * ws->Na;
+    AIY_TRY(dalloc(&ws->EV, n));
+    AIY_TRY(dalloc(&ws->T, n));
+    AIY_TRY(dalloc(&ws->coh, n));
+    AIY_TRY(dalloc(&ws->best0, n));
+    AIY_TRY(dalloc(&ws->kf, n));
+    AIY_TRY(dalloc(&ws->idx0, n));
+    int nchunk = (int)((ws->Na + ws->CK - 1) / ws->CK);
+    size_t need = (size_t)nchunk * n;
+    if (ws->partial && ws->partial_cap < need) dfree(ws->partial);
+    if (!ws->partial) {
+        AIY_TRY(dalloc(&ws->partial, need));
+        ws->partial_cap = need;
+    }
+    AIY_TRY(dalloc(&ws->diff, 2));
+    AIY_TRY(dalloc(&ws->hitcount, 1));
+    if (!ws->hdiff) AIY_HIP(hipHostMalloc((void**)&ws->hdiff, 4 * sizeof(unsigned long long)));
+    return AIY_OK;
+}
+
+int ws_timing_begin(aiy_ws* ws, hipStream_t st) {
+    if (!ws->timing) return AIY_OK;
+    if (ws->ev_used == (int)ws->ev_start.size()) AIY_TRY(ws_timing_drain(ws));
+    AIY_HIP(hipEventRecord(ws->ev_start[ws->ev_used], st));
+    return AIY_OK;
+}
+int ws_timing_end(aiy_ws* ws, hipStream_t st) {
+    if (!ws->timing) return AIY_OK;
+    AIY_HIP(hipEventRecord(ws->ev_stop[ws->ev_used], st));
+    ws->ev_used++;
+    return AIY_OK;
+}
+int ws_timing_drain(aiy_ws* ws) {
+    for (int q = 0; q < ws->ev_used; ++q) {
+        AIY_HIP(hipEventSynchronize(ws->ev_stop[q]));
+        float ms = 0.f;
+        AIY_HIP(hipEventElapsedTime(&ms, ws->ev_start[q], ws->ev_stop[q]));
+        ws->tot_ms += ms;
+        ws->launches++;
+    }
+    ws->ev_used = 0;
+    return AIY_OK;
+}
+
+// ---------------------------------------------------------------------------- VFI sweep
+int vfi_sweep_dev(aiy_ws* ws, const double* v_old, const double* a, const double* s,
+                  const double* P, double r, double w, double beta, double sigma,
+                  const int* hint, int coarse_first, int mode, double* v_new, int* idx,
+                  double* pk, double* pc, double* diff_out, hipStream_t st) {
+    if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
+    if (!v_old || !a || !s || !P || !v_new || !idx)
+        return fail(AIY_BAD_ARG, "NULL device pointer");
+    if (!(beta == beta) || !(r == r) || !(w == w) || !(sigma == sigma))
+        return fail(AIY_NON_FINITE, "non-finite scalar argument");
+    AIY_TRY(ws_ensure_vfi(ws));
+    VfiArgs A{};
+    A.N = (int)ws->N;
+    A.Na = (int)ws->Na;
+    A.np = is_int_ge(sigma, 2.0) && sigma <= 9.0 ? (int)sigma - 1 : 0;
+    if (mode == 2) A.np = is_int_ge(sigma, 2.0) && sigma <= 9.0 ? (int)sigma - 1 : 0;
+    if (mode == 1 && A.np == 0)
+        return fail(AIY_BAD_ARG, "screened sweep (mode 1) needs integer sigma in [2, 9]");
+    bool screened = (mode != 2) && A.np > 0;
+    A.coarse = (hint && !coarse_first) ? 0 : ws->coarse;
+    A.CK = ws->CK;
+    A.r = r;
+    A.w = w;
+    A.beta = beta;
+    A.sigma = sigma;
+    A.v_old = v_old;
+    A.a = a;
+    A.s = s;
+    A.P = P;
+    A.hint = hint;
+    A.EV = ws->EV;
+    A.T = ws->T;
+    A.coh = ws->coh;
+    A.kf = ws->kf;
+    A.best0 = ws->best0;
+    A.idx0 = ws->idx0;
+    A.partial = ws->partial;
+    A.hitcount = ws->count_hits ? ws->hitcount : nullptr;
+    A.v_new = v_new;
+    A.idx = idx;
+    A.pk = pk;
+    A.pc = pc;
+    A.diff = ws->diff;
+    AIY_HIP(hipMemsetAsync(ws->diff, 0, 2 * sizeof(unsigned long long), st));
+    AIY_TRY(launch_vfi_table(A, st));
+    if (!screened) A.coarse = 0, A.hint = nullptr;
+    AIY_TRY(launch_vfi_init(A, st));
+    AIY_TRY(ws_timing_begin(ws, st));
+    if (screened) AIY_TRY(launch_vfi_screen(A, st));
+    else AIY_TRY(launch_vfi_plain(A, st));
+    AIY_TRY(ws_timing_end(ws, st));
+    AIY_TRY(launch_vfi_merge(A, screened ? 1 : 0, st));
+    if (diff_out)
+        AIY_HIP(hipMemcpyAsync(diff_out, ws->diff, 2 * sizeof(unsigned long long),
+                               hipMemcpyDeviceToDevice, st));
+    return AIY_OK;
+}
+
+// read {max|Δ| bits, any} from the workspace diff word (synchronises the stream)
+int ws_read_diff(aiy_ws* ws, hipStream_t st, double* d) {
+    AIY_HIP(hipMemcpyAsync(ws->hdiff, ws->diff, 2 * sizeof(unsigned long long),
+                           hipMemcpyDeviceToHost, st));
+    AIY_HIP(hipStreamSynchronize(st));
+    if (ws->hdiff[1] == 0) *d = NAN;
+    else memcpy(d, &ws->hdiff[0], sizeof(double));
+    return AIY_OK;
+}
+
+int vfi_solve_dev(aiy_ws* ws, double* v_a, double* v_b, const double* a, const double* s,
+                  const double* P, double r, double w, double beta, double sigma, double tol,
+                  int64_t max_iter, int mode, int* idx, double* pk, double* pc,
+                  const int* first_hint, int64_t* iters, int* out_new, hipStream_t st) {
+    if (max_iter < 1) return fail(AIY_BAD_ARG, "max_iter must be >= 1");
+    double* cur = v_a;
+    double* nxt = v_b;
+    int64_t it;
+    for (it = 1; it <= max_iter; ++it) {
+        const int* hint = (it == 1) ? first_hint : idx;
+        AIY_TRY(vfi_sweep_dev(ws, cur, a, s, P, r, w, beta, sigma, hint, it == 1, mode, nxt,
+                              idx, pk, pc, nullptr, st));
+        double d;
+        AIY_TRY(ws_read_diff(ws, st, &d));
+        if (d < tol) break;  // :85-86  (v_old keeps the previous iterate)
+        std::swap(cur, nxt); // :88
+    }
+    if (it > max_iter) {  // loop exhausted: v_old = v_new after the last sweep
+        it = max_iter;
+        // after the final swap `cur` holds v_new; make the other buffer equal to it
+        AIY_HIP(hipMemcpyAsync(nxt, cur, sizeof(double) * ws->N * ws->Na,
+                               hipMemcpyDeviceToDevice, st));
+        std::swap(cur, nxt);
+    }
+    *iters = it;
+    *out_new = (nxt == v_a) ? 0 : 1;
+    return AIY_OK;
+}
+
+}  // namespace aiy
+
+using namespace aiy;
+
+// ============================================================================ C ABI
+extern "C" {
+
+const char* aiy_last_error(void) { return g_err.c_str(); }
+int aiy_version(void) { return 100; }
+int aiy_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int aiy_ws_create(int64_t N, int64_t Na, int64_t Nl, aiy_ws** out) {
+    if (!out) return fail(AIY_BAD_ARG, "NULL out pointer");
+    if (N < 1 || Na < 2 || N > (1 << 16) || Na > (1 << 28) || N * Na > (1ll << 31) - 1)
+        return fail(AIY_BAD_SHAPE, "unsupported shape N=%lld Na=%lld", (long long)N,
+                    (long long)Na);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1)
+        return fail(AIY_NO_DEVICE, "no HIP device visible");
+    aiy_ws* ws = new aiy_ws();
+    ws->N = N;
+    ws->Na = Na;
+    ws->Nl = Nl < 1 ? 1 : Nl;
+    (void)hipGetDevice(&ws->dev);
+    ws->ev_start.resize(64);
+    ws->ev_stop.resize(64);
+    for (int q = 0; q < 64; ++q) {
+        if (hipEventCreate(&ws->ev_start[q]) != hipSuccess ||
+            hipEventCreate(&ws->ev_stop[q]) != hipSuccess) {
+            aiy_ws_destroy(ws);
+            return fail(AIY_HIP_ERROR, "hipEventCreate failed");
+        }
+    }
+    *out = ws;
+    return AIY_OK;
+}
+
+int aiy_ws_destroy(aiy_ws* ws) {
+    if (!ws) return AIY_OK;
+    ws->free_all();
+    for (auto& e : ws->ev_start)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& e : ws->ev_stop)
+        if (e) (void)hipEventDestroy(e);
+    delete ws;
+    return AIY_OK;
+}
+
+int aiy_ws_set_timing(aiy_ws* ws, int enable) {
+    if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
+    AIY_TRY(ws_timing_drain(ws));
+    ws->timing = enable != 0;
+    ws->count_hits = enable != 0;
+    ws->tot_ms = 0;
+    ws->launches = 0;
+    if (ws->hitcount) AIY_HIP(hipMemset(ws->hitcount, 0, sizeof(unsigned long long)));
+    return AIY_OK;
+}
+
+int aiy_ws_timing(aiy_ws* ws, double* total_ms, int64_t* launches, int64_t* hits) {
+    if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
+    AIY_TRY(ws_timing_drain(ws));
+    if (total_ms) *total_ms = ws->tot_ms;
+    if (launches) *launches = ws->launches;
+    if (hits) {
+        unsigned long long h = 0;
+        if (ws->hitcount)
+            AIY_HIP(hipMemcpy(&h, ws->hitcount, sizeof h, hipMemcpyDeviceToHost));
+        *hits = (int64_t)h;
+    }
+    return AIY_OK;
+}
+
+int aiy_ws_set_search(aiy_ws* ws, int coarse_stride, int k_chunk) {
+    if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
+    if (coarse_stride < 0 || k_chunk < 64 || k_chunk % 8)
+        return fail(AIY_BAD_ARG, "coarse_stride >= 0, k_chunk >= 64 and a multiple of 8");
+    if (coarse_stride) ws->coarse = coarse_stride;
+    if (k_chunk != ws->CK) {
+        ws->CK = k_chunk;
+        if (ws->partial) {
+            (void)hipFree(ws->partial);
+            ws->partial = nullptr;
+            ws->partial_cap = 0;
+        }
+    }
+    return AIY_OK;
+}
+
+int aiy_vfi_sweep_dev(aiy_ws* ws, const double* v_old, const double* a_grid, const double* s,
+                      const double* P, double r, double w, double beta, double sigma,
+                      const int32_t* hint, int mode, double* v_new, int32_t* idx,
+                      double* policy_k, double* policy_c, double* diff, void* stream) {
+    return vfi_sweep_dev(ws, v_old, a_grid, s, P, r, w, beta, sigma, hint, hint == nullptr,
+                         mode, v_new, idx, policy_k, policy_c, diff, (hipStream_t)stream);
+}
+
+int aiy_vfi_solve_dev(aiy_ws* ws, double* v_a, double* v_b, const double* a_grid,
+                      const double* s, const double* P, double r, double w, double beta,
+                      double sigma, double tol, int64_t max_iter, int mode, int32_t* idx,
+                      double* policy_k, double* policy_c, int64_t* iters, int* out_new,
+                      void* stream) {
+    if (!iters || !out_new) return fail(AIY_BAD_ARG, "NULL iters/out_new");
+    return vfi_solve_dev(ws, v_a, v_b, a_grid, s, P, r, w, beta, sigma, tol, max_iter, mode,
+                         idx, policy_k, policy_c, nullptr, iters, out_new,
+                         (hipStream_t)stream);
+}
+
+}  // extern "C"

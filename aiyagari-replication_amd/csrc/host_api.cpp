@@ -1,0 +1,182 @@
+// Host tier of the C ABI: MATLAB column-major arrays in and out, synchronous.  Each call
+// stages its inputs into library-owned device buffers (cached per shape), runs the device
+// tier and copies the outputs back in the layout of the variables the call replaces.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
+#include "aiy_common.hpp"
+#include "host_ctx.hpp"
+#include "ws.hpp"
+
+namespace aiy {
+
+static std::mutex g_mu;
+static std::map<std::tuple<int, int64_t, int64_t, int64_t>, std::unique_ptr<HostCtx>> g_ctx;
+
+HostCtx::~HostCtx() {
+    for (auto& kv : bufs) (void)hipFree(kv.second.first);
+    if (ws) aiy_ws_destroy(ws);
+    if (st) (void)hipStreamDestroy(st);
+}
+
+int HostCtx::buf(const char* name, size_t bytes, void** out) {
+    auto it = bufs.find(name);
+    if (it != bufs.end() && it->second.second >= bytes) {
+        *out = it->second.first;
+        return AIY_OK;
+    }
+    if (it != bufs.end()) {
+        (void)hipFree(it->second.first);
+        bufs.erase(it);
+    }
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes ? bytes : 8);
+    if (e != hipSuccess) return fail(AIY_NO_MEMORY, "hipMalloc(%zu) failed", bytes);
+    bufs[name] = {p, bytes};
+    *out = p;
+    return AIY_OK;
+}
+
+int get_ctx(int64_t N, int64_t Na, int64_t Nl, HostCtx** out) {
+    int dev = 0;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1)
+        return fail(AIY_NO_DEVICE, "no HIP device visible");
+    (void)hipGetDevice(&dev);
+    auto key = std::make_tuple(dev, N, Na, Nl);
+    auto it = g_ctx.find(key);
+    if (it != g_ctx.end()) {
+        *out = it->second.get();
+        return AIY_OK;
+    }
+    auto ctx = std::make_unique<HostCtx>();
+    AIY_TRY(aiy_ws_create(N, Na, Nl, &ctx->ws));
+    AIY_HIP(hipStreamCreateWithFlags(&ctx->st, hipStreamNonBlocking));
+    *out = ctx.get();
+    g_ctx[key] = std::move(ctx);
+    return AIY_OK;
+}
+
+std::mutex& host_mutex() { return g_mu; }
+
+// MATLAB N x Na column-major -> [N][Na] row-major
+void cm_to_rows(const double* cm, int64_t N, int64_t Na, double* rows) {
+    for (int64_t j = 0; j < Na; ++j)
+        for (int64_t i = 0; i < N; ++i) rows[i * Na + j] = cm[i + j * N];
+}
+void rows_to_cm(const double* rows, int64_t N, int64_t Na, double* cm) {
+    for (int64_t j = 0; j < Na; ++j)
+        for (int64_t i = 0; i < N; ++i) cm[i + j * N] = rows[i * Na + j];
+}
+
+int check_grid(const double* a, int64_t Na) {
+    if (!a) return fail(AIY_BAD_ARG, "a_grid is NULL");
+    for (int64_t k = 0; k < Na; ++k)
+        if (!std::isfinite(a[k])) return fail(AIY_NON_FINITE, "a_grid(%lld) is not finite", (long long)k + 1);
+    for (int64_t k = 1; k < Na; ++k)
+        if (a[k] < a[k - 1])
+            return fail(AIY_BAD_ARG, "a_grid must be non-decreasing (a_grid(%lld) < a_grid(%lld))",
+                        (long long)k + 1, (long long)k);
+    return AIY_OK;
+}
+
+// stage the common Aiyagari inputs (a_grid, s, P) on the device; P transposed to row-major
+int stage_common(HostCtx* c, const double* a, const double* s, const double* P, int64_t N,
+                 int64_t Na, double** da, double** ds, double** dP) {
+    AIY_TRY(c->buf("a", sizeof(double) * Na, (void**)da));
+    AIY_TRY(c->buf("s", sizeof(double) * N, (void**)ds));
+    AIY_TRY(c->buf("P", sizeof(double) * N * N, (void**)dP));
+    std::vector<double> Pr(N * N);
+    for (int64_t i = 0; i < N; ++i)
+        for (int64_t m = 0; m < N; ++m) Pr[i * N + m] = P[i + m * N];
+    AIY_HIP(hipMemcpyAsync(*da, a, sizeof(double) * Na, hipMemcpyHostToDevice, c->st));
+    AIY_HIP(hipMemcpyAsync(*ds, s, sizeof(double) * N, hipMemcpyHostToDevice, c->st));
+    AIY_HIP(hipMemcpyAsync(*dP, Pr.data(), sizeof(double) * N * N, hipMemcpyHostToDevice, c->st));
+    AIY_HIP(hipStreamSynchronize(c->st));
+    return AIY_OK;
+}
+
+static int vfi_host(const double* v_old_cm, const double* a, const double* s, const double* P,
+                    int64_t N, int64_t Na, double r, double w, double beta, double sigma,
+                    bool solve, double tol, int64_t max_iter, double* v_old_out_cm,
+                    double* v_new_cm, double* pk_cm, double* pc_cm, int32_t* idx_cm,
+                    int64_t* iters) {
+    if (!v_old_cm || !s || !P || !v_new_cm || !pk_cm || !pc_cm)
+        return fail(AIY_BAD_ARG, "NULL argument");
+    if (N < 1 || Na < 2) return fail(AIY_BAD_SHAPE, "need N >= 1 and Na >= 2");
+    AIY_TRY(check_grid(a, Na));
+    std::lock_guard<std::mutex> lk(g_mu);
+    HostCtx* c;
+    AIY_TRY(get_ctx(N, Na, 1, &c));
+    double *da, *ds, *dP, *dva, *dvb, *dpk, *dpc;
+    int* didx;
+    AIY_TRY(stage_common(c, a, s, P, N, Na, &da, &ds, &dP));
+    size_t nb = sizeof(double) * N * Na;
+    AIY_TRY(c->buf("va", nb, (void**)&dva));
+    AIY_TRY(c->buf("vb", nb, (void**)&dvb));
+    AIY_TRY(c->buf("pk", nb, (void**)&dpk));
+    AIY_TRY(c->buf("pc", nb, (void**)&dpc));
+    AIY_TRY(c->buf("idx", sizeof(int) * N * Na, (void**)&didx));
+    std::vector<double> rows(N * Na), tmp(N * Na);
+    cm_to_rows(v_old_cm, N, Na, rows.data());
+    AIY_HIP(hipMemcpyAsync(dva, rows.data(), nb, hipMemcpyHostToDevice, c->st));
+    int out_new = 1;
+    if (solve) {
+        AIY_TRY(vfi_solve_dev(c->ws, dva, dvb, da, ds, dP, r, w, beta, sigma, tol, max_iter, 0,
+                              didx, dpk, dpc, nullptr, iters, &out_new, c->st));
+    } else {
+        AIY_TRY(vfi_sweep_dev(c->ws, dva, da, ds, dP, r, w, beta, sigma, nullptr, 1, 0, dvb,
+                              didx, dpk, dpc, nullptr, c->st));
+    }
+    double* dnew = out_new ? dvb : dva;
+    double* dold = out_new ? dva : dvb;
+    auto back = [&](const double* d, double* cm) -> int {
+        AIY_HIP(hipMemcpyAsync(tmp.data(), d, nb, hipMemcpyDeviceToHost, c->st));
+        AIY_HIP(hipStreamSynchronize(c->st));
+        rows_to_cm(tmp.data(), N, Na, cm);
+        return AIY_OK;
+    };
+    AIY_TRY(back(dnew, v_new_cm));
+    AIY_TRY(back(dpk, pk_cm));
+    AIY_TRY(back(dpc, pc_cm));
+    if (solve && v_old_out_cm) AIY_TRY(back(dold, v_old_out_cm));
+    if (idx_cm) {
+        std::vector<int> ib(N * Na);
+        AIY_HIP(hipMemcpyAsync(ib.data(), didx, sizeof(int) * N * Na, hipMemcpyDeviceToHost, c->st));
+        AIY_HIP(hipStreamSynchronize(c->st));
+        for (int64_t j = 0; j < Na; ++j)
+            for (int64_t i = 0; i < N; ++i) idx_cm[i + j * N] = ib[i * Na + j] + 1;
+    }
+    return AIY_OK;
+}
+
+}  // namespace aiy
+
+using namespace aiy;
+
+extern "C" {
+
+int aiy_vfi_sweep(const double* v_old, const double* a_grid, const double* s, const double* P,
+                  int64_t N, int64_t Na, double r, double w, double beta, double sigma,
+                  double* v_new, double* policy_k, double* policy_c, int32_t* policy_idx) {
+    return vfi_host(v_old, a_grid, s, P, N, Na, r, w, beta, sigma, false, 0, 1, nullptr, v_new,
+                    policy_k, policy_c, policy_idx, nullptr);
+}
+
+int aiy_vfi_solve(double* v_old, const double* a_grid, const double* s, const double* P,
+                  int64_t N, int64_t Na, double r, double w, double beta, double sigma,
+                  double tol, int64_t max_iter, double* v_new, double* policy_k,
+                  double* policy_c, int32_t* policy_idx, int64_t* iters) {
+    if (!iters) return fail(AIY_BAD_ARG, "NULL iters");
+    return vfi_host(v_old, a_grid, s, P, N, Na, r, w, beta, sigma, true, tol, max_iter, v_old,
+                    v_new, policy_k, policy_c, policy_idx, iters);
+}
+
+}  // extern "C"

@@ -1,0 +1,102 @@
+"""A1/A2 — Aiyagari VFI through the C ABI.
+
+Host-tier wrappers mirror the MATLAB loop they replace (same inputs/outputs, MATLAB layout
+semantics: arrays are (N, Na) with v[i, j] == v_old(i+1, j+1); indices returned 1-based like
+`idx` in Aiyagari_VFI.m:79).  The device tier (`Workspace`) keeps everything in HBM.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._capi import check, d, i64, ip, lib, ptr, stream_handle, vp
+
+
+def _f(a):
+    """MATLAB column-major view of an (N, Na) array (Fortran order, float64)."""
+    return np.asfortranarray(a, dtype=np.float64)
+
+
+def vfi_sweep(v_old, a_grid, s, P, r, w, beta, sigma):
+    """Replaces Aiyagari_VFI.m:68-83: one Bellman sweep.
+    Returns (v_new, policy_k, policy_c, idx) with idx 1-based."""
+    v_old = _f(v_old)
+    N, Na = v_old.shape
+    a_grid, s = np.ascontiguousarray(a_grid, np.float64), np.ascontiguousarray(s, np.float64)
+    P = _f(P)
+    v_new = np.empty((N, Na), order="F"); pk = np.empty((N, Na), order="F")
+    pc = np.empty((N, Na), order="F"); idx = np.empty((N, Na), np.int32, order="F")
+    check(lib().aiy_vfi_sweep(ptr(v_old), ptr(a_grid), ptr(s), ptr(P), i64(N), i64(Na), d(r),
+                              d(w), d(beta), d(sigma), ptr(v_new), ptr(pk), ptr(pc), ptr(idx)))
+    return v_new, pk, pc, idx
+
+
+def vfi_solve(v_old, a_grid, s, P, r, w, beta, sigma, tol=1e-5, max_iter=1000):
+    """Replaces Aiyagari_VFI.m:65-90 (break before v_old = v_new: both are returned)."""
+    v_old = np.array(v_old, dtype=np.float64, order="F", copy=True)
+    N, Na = v_old.shape
+    a_grid, s = np.ascontiguousarray(a_grid, np.float64), np.ascontiguousarray(s, np.float64)
+    P = _f(P)
+    v_new = np.empty((N, Na), order="F"); pk = np.empty((N, Na), order="F")
+    pc = np.empty((N, Na), order="F"); idx = np.empty((N, Na), np.int32, order="F")
+    it = C.c_int64(0)
+    check(lib().aiy_vfi_solve(ptr(v_old), ptr(a_grid), ptr(s), ptr(P), i64(N), i64(Na), d(r),
+                              d(w), d(beta), d(sigma), d(tol), i64(max_iter), ptr(v_new),
+                              ptr(pk), ptr(pc), ptr(idx), C.byref(it)))
+    return dict(v_new=v_new, v_old=v_old, policy_k=pk, policy_c=pc, idx=idx, iters=it.value)
+
+
+class Workspace:
+    """Device-tier handle (aiy_ws): per-shape scratch reused across sweeps.  Arrays are torch
+    tensors on the current device, layout [N][Na] (z-major)."""
+
+    def __init__(self, N: int, Na: int, Nl: int = 1):
+        self.N, self.Na, self.Nl = N, Na, Nl
+        h = vp()
+        check(lib().aiy_ws_create(i64(N), i64(Na), i64(Nl), C.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().aiy_ws_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_timing(self, on: bool):
+        check(lib().aiy_ws_set_timing(self._h, ip(1 if on else 0)))
+
+    def timing(self):
+        ms, n, hits = C.c_double(0), C.c_int64(0), C.c_int64(0)
+        check(lib().aiy_ws_timing(self._h, C.byref(ms), C.byref(n), C.byref(hits)))
+        return ms.value, n.value, hits.value
+
+    def set_search(self, coarse_stride=0, k_chunk=1024):
+        check(lib().aiy_ws_set_search(self._h, ip(coarse_stride), ip(k_chunk)))
+
+    def vfi_sweep(self, v_old, a_grid, s, P, r, w, beta, sigma, v_new, idx, policy_k=None,
+                  policy_c=None, hint=None, mode=0, diff=None, stream=None):
+        """A1 on device (asynchronous on the current torch stream)."""
+        check(lib().aiy_vfi_sweep_dev(self._h, ptr(v_old), ptr(a_grid), ptr(s), ptr(P), d(r),
+                                      d(w), d(beta), d(sigma), ptr(hint), ip(mode), ptr(v_new),
+                                      ptr(idx), ptr(policy_k), ptr(policy_c), ptr(diff),
+                                      stream_handle(stream)))
+
+    def vfi_solve(self, v_a, v_b, a_grid, s, P, r, w, beta, sigma, tol, max_iter, idx,
+                  policy_k=None, policy_c=None, mode=0, stream=None):
+        """A2 on device; returns (iters, which) with which = 0 if v_a holds v_new else 1."""
+        it, which = C.c_int64(0), C.c_int(0)
+        check(lib().aiy_vfi_solve_dev(self._h, ptr(v_a), ptr(v_b), ptr(a_grid), ptr(s), ptr(P),
+                                      d(r), d(w), d(beta), d(sigma), d(tol), i64(max_iter),
+                                      ip(mode), ptr(idx), ptr(policy_k), ptr(policy_c),
+                                      C.byref(it), C.byref(which), stream_handle(stream)))
+        return it.value, which.value

@@ -1,0 +1,189 @@
+"""Headline benchmark: Bellman evals/s (Na·Na'·Nz per sweep, fp64) for BASELINE config 2 —
+Aiyagari VFI, Na = 20,000, Nz = 7 Rouwenhorst, one exhaustive Bellman sweep per step
+(Aiyagari_VFI.m:70-83) on the MI355X, inputs resident in HBM.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Multi-GPU: the general-equilibrium loop's candidate interest rates are independent units
+(SURVEY §8(e) E2), so each rank solves its own r (weak scaling, no collective on the data
+path); the timing is max over ranks.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib.util
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+PEAK_FP64_TFLOPS = 78.6   # MI355X fp64 vector (= fp64 matrix) peak, datasheet
+FLOPS_PER_CANDIDATE = 8  # sub, mul, mul, div, sub, mul, add, max
+
+
+def load_pkg():
+    name = "aiyagari_replication_amd"
+    if name in sys.modules:
+        return sys.modules[name]
+    root = ROOT / "aiyagari-replication_amd"
+    spec = importlib.util.spec_from_file_location(name, root / "__init__.py",
+                                                  submodule_search_locations=[str(root)])
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def feasible_candidates(a, s, r, w):
+    """Σ_{i,j} #{k : a_k < coh_ij}: the candidates that carry arithmetic (c <= 0 is NaN in
+    the reference, Aiyagari_VFI.m:73)."""
+    tot = 0
+    for si in s:
+        coh = (1 + r) * a + w * si
+        tot += int(np.searchsorted(a, coh, side="left").sum())
+    return tot
+
+
+def cpu_baseline(cal, r, w, sweeps, threads):
+    """The C restatement (oracle/liborc.so, exhaustive, reference op order) timed on the
+    host: `sweeps` sweeps from v = 0 at the full workload size."""
+    from oracle import corc
+    n = corc.num_threads(threads)
+    N, Na = cal["N"], cal["Na"]
+    v = np.zeros((N, Na))
+    t0 = time.perf_counter()
+    for _ in range(sweeps):
+        v, _, _, _ = corc.vfi_sweep(v, cal["a_grid"], cal["s"], cal["P"], r, w, cal["beta"],
+                                    cal["sigma"])
+    dt = time.perf_counter() - t0
+    return dict(value=sweeps * N * Na * Na / dt, unit="evals/s", cores=n, kind="port",
+                sample=f"{sweeps} exhaustive sweeps from v=0 at Na={Na}, Nz={N} "
+                       f"(C restatement oracle/aiy_oracle.c, OpenMP over states), {dt:.2f} s")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--na", type=int, default=20000)
+    ap.add_argument("--mode", type=int, default=1, help="1 screened exhaustive, 2 plain")
+    ap.add_argument("--k-chunk", type=int, default=1024)
+    ap.add_argument("--cpu-sweeps", type=int, default=4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    pkg = load_pkg()
+    cal = pkg.calibration.aiyagari(Na=args.na, shocks="rouwenhorst")
+    N, Na = cal["N"], cal["Na"]
+    # candidate interest rates of the GE bracket [-0.05, 1/beta-1]: one per rank
+    r_lo, r_hi = -0.05, 1 / cal["beta"] - 1
+    r = r_lo + (r_hi - r_lo) * (rank + 1) / (world + 1) if world > 1 else 0.04
+    w = pkg.calibration.wage(r, cal["alpha"], cal["delta"])
+
+    t = lambda x: torch.as_tensor(np.ascontiguousarray(x), device=dev)
+    a_t, s_t, P_t = t(cal["a_grid"]), t(cal["s"]), t(cal["P"])
+    v = [torch.zeros((N, Na), dtype=torch.float64, device=dev) for _ in range(2)]
+    idx = torch.zeros((N, Na), dtype=torch.int32, device=dev)
+    pk = torch.empty((N, Na), dtype=torch.float64, device=dev)
+    pc = torch.empty((N, Na), dtype=torch.float64, device=dev)
+    ws = pkg.Workspace(N, Na)
+    ws.set_search(0, args.k_chunk)
+
+    cur = 0
+
+    def step(first=False):
+        nonlocal cur
+        ws.vfi_sweep(v[cur], a_t, s_t, P_t, r, w, cal["beta"], cal["sigma"], v[1 - cur], idx,
+                     pk, pc, hint=None if first else idx, mode=args.mode)
+        cur = 1 - cur
+
+    for q in range(max(args.warmup, 1)):
+        step(first=(q == 0))
+    torch.cuda.synchronize()
+    ws.set_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    kern_ms, launches, hits = ws.timing()
+    ws.set_timing(False)
+    if world > 1:
+        tt = torch.tensor([dt, kern_ms / max(launches, 1)], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt, kern_avg_ms = float(tt[0]), float(tt[1])
+    else:
+        kern_avg_ms = kern_ms / max(launches, 1)
+
+    if rank == 0:
+        evals_per_sweep = N * Na * Na
+        value = world * evals_per_sweep * args.steps / dt
+        feas = feasible_candidates(cal["a_grid"], cal["s"], r, w)
+        achieved = FLOPS_PER_CANDIDATE * feas / (kern_avg_ms * 1e-3) / 1e12
+        traffic = None
+        tf = ROOT / "profiles" / "traffic_vfi_screen.json"
+        if tf.exists():
+            traffic = json.loads(tf.read_text()).get("bytes_per_launch")
+        out = {
+            "metric": "Bellman evals/sec (Na·Na'·Nz, fp64)",
+            "value": value,
+            "unit": "evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (reference calibration: Rouwenhorst Nz=7, quadratic grid)",
+            "config": {"workload": "aiyagari_vfi_sweep Na=20000 Nz=7 rouwenhorst (BASELINE configs[1])",
+                       "Na": Na, "Nz": N, "sigma": cal["sigma"], "beta": cal["beta"],
+                       "search": "exhaustive over a' (screened, exact)" if args.mode == 1
+                                 else "exhaustive over a' (plain)",
+                       "parallelism": f"replicas: one GE candidate r per rank ({world})",
+                       "feasible_fraction": feas / evals_per_sweep,
+                       "screen_hits_per_sweep": hits / max(launches, 1)},
+            "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_FP64_TFLOPS,
+                         "unit": "TFLOP/s", "frac": achieved / PEAK_FP64_TFLOPS,
+                         "traffic": traffic,
+                         "kernel": "vfi_screen_kernel<4,2,8>",
+                         "kernel_avg_ms": kern_avg_ms,
+                         "basis": f"{FLOPS_PER_CANDIDATE} algorithmic flops x {feas} feasible "
+                                  f"candidates per launch; peak = fp64 vector (= fp64 matrix) "
+                                  f"78.6 TF/s"},
+        }
+        if not args.no_cpu_baseline:
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count())
+            out["cpu_baseline"] = cpu_baseline(cal, r, w, args.cpu_sweeps, threads)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

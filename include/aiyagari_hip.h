@@ -1,0 +1,96 @@
+/* aiyagari_hip.h — C ABI of the MI355X (gfx950) solver for the hot path of
+ * kostastril/Aiyagari-Replication (six MATLAB scripts).
+ *
+ * The reference has no plugin/operator/FFI interface: its hot path is inline script code.
+ * Each entry point below replaces exactly one cited loop body, takes the same inputs and
+ * returns the same outputs.  A MEX/mkoctfile gateway
+ * (aiyagari-replication_amd/mex/) binds them one-to-one; INTEGRATION.md shows the binding.
+ *
+ * Two tiers:
+ *   1. Host-pointer functions (aiy_*, ks_*): MATLAB column-major arrays exactly as the
+ *      replaced variables are laid out, synchronous (return after the outputs are copied
+ *      back).  Device buffers are library-owned and cached per shape across calls.
+ *   2. Device-pointer functions (*_dev): arrays already resident in HBM, state-major layout
+ *      ([N][Na] row-major == MATLAB Na x N column-major), asynchronous on `stream`
+ *      (a hipStream_t; NULL = default stream).  Used by the python host mirror and bench.
+ *
+ * Conventions: all arrays fp64 unless typed otherwise; index outputs are 0-based in the
+ * device tier and 1-based (MATLAB) in the host tier; every function returns an aiy_status
+ * and leaves a message retrievable with aiy_last_error().
+ */
+#ifndef AIYAGARI_HIP_H
+#define AIYAGARI_HIP_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    AIY_OK = 0,
+    AIY_BAD_SHAPE = 1,   /* inconsistent or unsupported sizes */
+    AIY_NON_FINITE = 2,  /* an input that must be finite is not */
+    AIY_HIP_ERROR = 3,   /* HIP runtime failure (message has hipGetErrorString) */
+    AIY_RCCL_ERROR = 4,  /* reserved: collective failure (multi-device entry points) */
+    AIY_NO_DEVICE = 5,   /* no gfx950 device visible */
+    AIY_BAD_ARG = 6,     /* invalid scalar / unsorted grid / NULL pointer */
+    AIY_FIND_EMPTY = 7,  /* find(rand < cumsum(P(z,:)),1) empty: the reference would error */
+    AIY_NO_MEMORY = 8
+} aiy_status;
+
+const char* aiy_last_error(void); /* thread-local message of the last failing call */
+int aiy_version(void);            /* 100*major + minor */
+int aiy_device_count(void);
+
+/* ======================================================================================
+ * Host tier (MATLAB layouts).  VFI arrays N x Na; EGM arrays Na x N; KS k x K x S.
+ * ====================================================================================== */
+
+/* A1 — replaces Aiyagari_VFI.m:68-83 (one Bellman sweep).
+ * in : v_old N x Na, a_grid Na (non-decreasing), s N, P N x N, r, w, beta, sigma
+ * out: v_new, policy_k, policy_c (N x Na); policy_idx (N x Na, 1-based, may be NULL) */
+int aiy_vfi_sweep(const double* v_old, const double* a_grid, const double* s, const double* P,
+                  int64_t N, int64_t Na, double r, double w, double beta, double sigma,
+                  double* v_new, double* policy_k, double* policy_c, int32_t* policy_idx);
+
+/* A2 — replaces Aiyagari_VFI.m:65-90 (the sweep loop).  Break semantics of :85-88: on
+ * return v_new is the converged iterate and v_old (in/out) the previous one; when max_iter
+ * is exhausted v_old == v_new.  iters = the reference's `iter` at exit. */
+int aiy_vfi_solve(double* v_old, const double* a_grid, const double* s, const double* P,
+                  int64_t N, int64_t Na, double r, double w, double beta, double sigma,
+                  double tol, int64_t max_iter, double* v_new, double* policy_k,
+                  double* policy_c, int32_t* policy_idx, int64_t* iters);
+
+/* ======================================================================================
+ * Device tier: [N][Na] (z-major) arrays in HBM, async on `stream` (hipStream_t).
+ * A workspace holds the per-shape scratch (EV/D tables, init/partial buffers, events).
+ * ====================================================================================== */
+typedef struct aiy_ws aiy_ws;
+int aiy_ws_create(int64_t N, int64_t Na, int64_t Nl, aiy_ws** ws);
+int aiy_ws_destroy(aiy_ws* ws);
+/* kernel timing: when enabled, HIP events bracket the dominant kernel of every call on its
+ * stream; aiy_ws_timing reads the accumulated milliseconds and launch count. */
+int aiy_ws_set_timing(aiy_ws* ws, int enable);
+int aiy_ws_timing(aiy_ws* ws, double* total_ms, int64_t* launches, int64_t* hits);
+/* search knobs (defaults tuned for gfx950): coarse stride for cold starts, k-chunk. */
+int aiy_ws_set_search(aiy_ws* ws, int coarse_stride, int k_chunk);
+
+/* A1 on device.  hint (nullable, [N][Na] int32 0-based) = previous sweep's argmax; the result
+ * does not depend on it, only the run time.  diff (nullable, device double[2]) receives
+ * {max|v_new-v_old| ignoring NaN, 1 if any non-NaN}.  mode: 0 = auto, 1 = screened
+ * exhaustive (integer sigma>=2), 2 = plain exhaustive (any sigma). */
+int aiy_vfi_sweep_dev(aiy_ws* ws, const double* v_old, const double* a_grid, const double* s,
+                      const double* P, double r, double w, double beta, double sigma,
+                      const int32_t* hint, int mode, double* v_new, int32_t* idx,
+                      double* policy_k, double* policy_c, double* diff, void* stream);
+/* A2 on device: v_a (in: v_old) and v_b are ping-pong buffers; on return *out_new points
+ * (0 = v_a, 1 = v_b) to the buffer holding v_new, the other holds v_old (break semantics).
+ * idx doubles as the hint between sweeps. */
+int aiy_vfi_solve_dev(aiy_ws* ws, double* v_a, double* v_b, const double* a_grid,
+                      const double* s, const double* P, double r, double w, double beta,
+                      double sigma, double tol, int64_t max_iter, int mode, int32_t* idx,
+                      double* policy_k, double* policy_c, int64_t* iters, int* out_new,
+                      void* stream);
+#ifdef __cplusplus
+}
+#endif
+#endif
