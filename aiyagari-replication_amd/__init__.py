@@ -8,7 +8,7 @@ library or a device raises.
 """
 from . import calibration
 from ._capi import AiyError, LIB_PATH, declared_symbols, lib
-from .vfi import Workspace, vfi_solve, vfi_sweep
+from .vfi import Workspace, labor_vfi_solve, labor_vfi_sweep, vfi_solve, vfi_sweep
 
 __all__ = ["AiyError", "LIB_PATH", "Workspace", "calibration", "declared_symbols", "lib",
-           "vfi_solve", "vfi_sweep"]
+           "labor_vfi_solve", "labor_vfi_sweep", "vfi_solve", "vfi_sweep"]

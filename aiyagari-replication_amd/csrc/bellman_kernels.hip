@@ -1,0 +1,483 @@
+// A1/A2 and A3 — exhaustive Bellman sweeps on gfx950.
+//   A1: Aiyagari_VFI.m:70-83 (GE copy :152-165)           max over a'          (Nl = 1)
+//   A3: Aiyagari_Endogenous_Labor_VFI.m:69-112 (GE :176-219) max over (l, a') column-major
+// A1 is the Nl = 1 case of A3 with L = 1 and no disutility term: the cash-on-hand and value
+// expressions then coincide operation for operation, so one kernel family serves both.
+//
+// Four launches per sweep on the caller's stream:
+//   1. table   EV(i,k) = Σ_m (β·P(i,m))·V(m,k), m ascending (:79 / Labor :69), and the
+//              screening key D(i,k) = n·EV + 1 + τ(|n·EV| + 1), stored as (a_k, D) pairs.
+//   2. init    per state: an exact starting candidate — the hint (last sweep's argmax), a
+//              coarse scan of every feasible prefix (stride S) and a bracket refinement
+//              (steps S/2, S/4, ..., 1) around the best point of each labour level.  For a
+//              unimodal objective this IS the maximiser; it only sets the screening bar.
+//   3. screen  every feasible candidate.  Work item = one wave × (64·R states × LB labour
+//              levels) × CK candidates a', so all waves carry equal work.  Per candidate 6
+//              fp64 VALU ops: c = coh − a_k, q = c^n, t = (D_k − B)·q, test t ≥ 1 − 2^-48
+//              where B = n·(best + dis_l) − slack.  The test is TRUE for every candidate whose
+//              exact value reaches the running best (DESIGN.md §A1 bounds the rounding), so
+//              evaluating exactly only the candidates that pass, and merging with the
+//              (max value, first column-major index) rule, reproduces the plain exhaustive
+//              scan bit for bit.
+//   4. merge   per state: init ⊕ every chunk's improvement → v_new, index, policy_k = a(k),
+//              policy_l = L(l), policy_c = c(l,k), and max|v_new − v_old| ignoring NaN via an
+//              order-independent atomicMax on IEEE bits.
+// Non-integer σ (or σ > 9) runs a plain exhaustive kernel (device pow/log).
+#include <type_traits>
+
+#include "aiy_common.hpp"
+#include "bellman.hpp"
+
+namespace aiy {
+
+constexpr double kTau = 9.094947017729282e-13;  // 2^-40
+constexpr double kThr = 0.99999999999999644729;  // 1 - 2^-48
+
+// exact value of candidate (c, l, k) in the literal MATLAB order
+template <int NP, bool LAB>
+__device__ __forceinline__ double bell_val(double c, double ev, double sigma, double dis) {
+    double u;
+    if constexpr (NP > 0) {
+        double p = 1.0 / aiy_ipow(c, NP);  // c.^(1-sigma), sigma = NP + 1
+        u = (p - 1) / (1 - sigma);
+    } else {
+        if (!LAB && sigma == 1.0) u = log(c);  // Aiyagari_VFI.m:74-75 (labour script has no branch)
+        else u = (pow(c, 1.0 - sigma) - 1) / (1 - sigma);
+    }
+    if constexpr (LAB) return (u - dis) + ev;  // Labor_VFI.m:95-99
+    else return u + ev;                        // Aiyagari_VFI.m:79
+}
+
+// (max value, first index) merge; NaN never enters (MATLAB max omits NaN)
+__device__ __forceinline__ bool lexi_take(double val, int q, double& best, int& idx) {
+    if (val != val) return false;
+    if (idx < 0 || val > best || (val == best && q < idx)) {
+        best = val;
+        idx = q;
+        return true;
+    }
+    return false;
+}
+
+// screening bar of (best, dis_l):  n·(best + dis) − τ·n·(|best| + |dis|)
+__device__ __forceinline__ double screen_B(double best, int idx, double dis, int np) {
+    if (idx < 0) return -__builtin_inf();
+    double nd = (double)np;
+    return nd * (best + dis) - kTau * nd * (fabs(best) + fabs(dis));
+}
+
+template <bool LAB>
+__device__ __forceinline__ double cash(double x, double y, double Ll) {
+    if constexpr (LAB) return x + y * Ll;  // (1+r)a_j + (w s_i) L_l   (Labor_VFI.m:81)
+    else return x + y;                     // (1+r)a_j + w s_i          (Aiyagari_VFI.m:72)
+}
+
+// ------------------------------------------------------------------------------ 1. table
+__global__ void bell_table_kernel(int N, int Na, const double* __restrict__ P,
+                                  const double* __restrict__ V, double beta, int np,
+                                  const double* __restrict__ a, double* __restrict__ EV,
+                                  double2* __restrict__ T) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= N * Na) return;
+    int i = t / Na, k = t - i * Na;
+    double acc = 0.0;
+    for (int m = 0; m < N; ++m) acc = acc + (beta * P[i * N + m]) * V[m * Na + k];
+    EV[t] = acc;
+    if (T) {
+        double ne = (double)np * acc;
+        T[t] = make_double2(a[k], (ne + 1.0) + kTau * (fabs(ne) + 1.0));
+    }
+}
+
+// ------------------------------------------------------------------------------ 2. init
+template <int NP, bool LAB>
+__global__ void bell_init_kernel(BellArgs A) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= A.N * A.Na) return;
+    const int Na = A.Na, Nl = A.Nl;
+    int i = t / Na, j = t - i * Na;
+    const double* __restrict__ a = A.a;
+    const double* __restrict__ ev = A.EV + (size_t)i * Na;
+    double x = (1 + A.r) * a[j];
+    double y = A.w * A.s[i];
+    double best = __builtin_nan("");
+    int idx = -1;
+    bool anyfeas = false;
+    auto eval = [&](int l, int k, double coh) {
+        double dis = LAB ? A.dis[l] : 0.0;
+        return bell_val<NP, LAB>(coh - a[k], ev[k], A.sigma, dis);
+    };
+    if (A.hint) {
+        int h = A.hint[t];
+        int l = h % Nl, k = h / Nl;
+        if (h >= 0 && l >= 0 && l < Nl) {
+            double coh = cash<LAB>(x, y, LAB ? A.L[l] : 1.0);
+            int kf = lower_bound_dev(a, Na, coh);
+            if (kf > 0) {
+                k = k >= kf ? kf - 1 : k;
+                lexi_take(eval(l, k, coh), l + Nl * k, best, idx);
+            }
+        }
+    }
+    const int S = A.coarse;
+    for (int l = 0; l < Nl; ++l) {
+        double coh = cash<LAB>(x, y, LAB ? A.L[l] : 1.0);
+        int kf = lower_bound_dev(a, Na, coh);
+        if (kf == 0) continue;
+        anyfeas = true;
+        if (S <= 0) {
+            if (!A.hint) lexi_take(eval(l, 0, coh), l, best, idx);
+            continue;
+        }
+        // coarse scan of this labour level, then bracket refinement around its best point
+        double lb = __builtin_nan("");
+        int lk = -1;
+        for (int k = 0; k < kf; k += S) lexi_take(eval(l, k, coh), k, lb, lk);
+        lexi_take(eval(l, kf - 1, coh), kf - 1, lb, lk);
+        if (lk >= 0) {
+            for (int step = S >> 1; step >= 1; step >>= 1) {
+                int c0 = lk;
+                if (c0 - step >= 0) lexi_take(eval(l, c0 - step, coh), c0 - step, lb, lk);
+                if (c0 + step < kf) lexi_take(eval(l, c0 + step, coh), c0 + step, lb, lk);
+            }
+            lexi_take(lb, l + Nl * lk, best, idx);
+        }
+    }
+    A.best0[t] = best;
+    A.idx0[t] = anyfeas ? idx : -2;  // -2: no feasible choice at all
+}
+
+// ------------------------------------------------------------------------------ 3. screen
+template <int NP, bool LAB, int R, int LB, int KB>
+__global__ __launch_bounds__(256) void bell_screen_kernel(BellArgs A, int ntile, int nlb,
+                                                          int nchunk) {
+    const int wave = readfirst(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int item = readfirst(blockIdx.x * 4 + wave);
+    const int chunk = item % nchunk;
+    int rest = item / nchunk;
+    const int lbk = rest % nlb;
+    rest /= nlb;
+    const int tile = rest % ntile;
+    const int i = rest / ntile;
+    const int N = A.N, Na = A.Na, Nl = A.Nl, CK = A.CK;
+    if (i >= N) return;
+    const double* __restrict__ a = A.a;
+    const int jbase = tile * (64 * R);
+    const int jlast = min(jbase + 64 * R, Na) - 1;
+    const int l0 = lbk * LB;
+    const int l1 = min(l0 + LB, Nl);
+    const double y = A.w * A.s[i];
+    // wave-uniform feasible range: smallest / largest cash on hand in this item
+    double cmin = __builtin_inf(), cmax = -__builtin_inf();
+    {
+        double xb = (1 + A.r) * a[jbase], xl = (1 + A.r) * a[jlast];
+        for (int l = l0; l < l1; ++l) {
+            double Ll = LAB ? A.L[l] : 1.0;
+            cmin = fmin(cmin, cash<LAB>(xb, y, Ll));
+            cmax = fmax(cmax, cash<LAB>(xl, y, Ll));
+        }
+    }
+    const int kmax = readfirst(lower_bound_dev(a, Na, cmax));
+    const int k_lo = chunk * CK;
+    if (k_lo >= kmax) return;
+    const int kmin = readfirst(lower_bound_dev(a, Na, cmin));
+    const int k_hi = min(k_lo + CK, kmax);
+
+    double coh[R][LB], B[R][LB], best[R], dis[LB];
+    int idx[R], imp[R];
+#pragma unroll
+    for (int q = 0; q < LB; ++q) dis[q] = (LAB && l0 + q < l1) ? A.dis[l0 + q] : 0.0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        int j = jbase + r * 64 + lane;
+        imp[r] = -1;
+        bool ok = j < Na;
+        size_t ij = (size_t)i * Na + (ok ? j : 0);
+        best[r] = ok ? A.best0[ij] : 0.0;
+        idx[r] = ok ? A.idx0[ij] : 0x7fffffff;
+        if (idx[r] == -2) idx[r] = -1;
+        double x = ok ? (1 + A.r) * a[j] : 0.0;
+#pragma unroll
+        for (int q = 0; q < LB; ++q) {
+            bool okq = ok && (l0 + q < l1);
+            // invalid sub-states get a NaN bar: every screen test on them is false
+            coh[r][q] = okq ? cash<LAB>(x, y, LAB ? A.L[l0 + q] : 1.0) : 0.0;
+            B[r][q] = okq ? screen_B(best[r], idx[r], dis[q], NP) : __builtin_nan("");
+        }
+    }
+    const double2* __restrict__ Trow = A.T + (size_t)i * Na;
+    const double* __restrict__ ev = A.EV + (size_t)i * Na;
+    unsigned nhits = 0;
+
+    auto exact_block = [&](int k0, int kend) {
+        for (int k = k0; k < kend; ++k) {
+            const double2 tk = Trow[k];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+#pragma unroll
+                for (int q = 0; q < LB; ++q) {
+                    double c = coh[r][q] - tk.x;
+                    if (c > 0 && (tk.y - B[r][q]) * aiy_ipow(c, NP) >= kThr) {
+                        ++nhits;
+                        double val = bell_val<NP, LAB>(c, ev[k], A.sigma, dis[q]);
+                        int lin = (l0 + q) + Nl * k;
+                        if (lexi_take(val, lin, best[r], idx[r])) {
+                            imp[r] = lin;
+#pragma unroll
+                            for (int q2 = 0; q2 < LB; ++q2)
+                                if (B[r][q2] == B[r][q2])
+                                    B[r][q2] = screen_B(best[r], idx[r], dis[q2], NP);
+                        }
+                    }
+                }
+            }
+        }
+    };
+
+    // region 1: every sub-state feasible (k < kmin); region 2: c clamped at 0 so that
+    // infeasible candidates (NaN / -Inf in the reference) never pass the screen
+    auto run = [&](auto guard, int kb, int ke) {
+        int k = kb;
+        for (; k + KB <= ke; k += KB) {
+            bool hit = false;
+#pragma unroll
+            for (int kk = 0; kk < KB; ++kk) {
+                const double2 tk = Trow[k + kk];  // wave-uniform address → scalar loads
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+#pragma unroll
+                    for (int q = 0; q < LB; ++q) {
+                        double c = coh[r][q] - tk.x;
+                        if constexpr (decltype(guard)::value) c = fmax(c, 0.0);
+                        hit |= ((tk.y - B[r][q]) * aiy_ipow(c, NP) >= kThr);
+                    }
+                }
+            }
+            if (__any(hit)) exact_block(k, k + KB);
+        }
+        if (k < ke) {
+            bool hit = false;
+            for (int kk = k; kk < ke; ++kk) {
+                const double2 tk = Trow[kk];
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int q = 0; q < LB; ++q)
+                        hit |= ((tk.y - B[r][q]) * aiy_ipow(fmax(coh[r][q] - tk.x, 0.0), NP) >= kThr);
+            }
+            if (__any(hit)) exact_block(k, ke);
+        }
+    };
+    const int r1_end = min(k_hi, max(k_lo, kmin));
+    run(std::false_type{}, k_lo, r1_end);
+    run(std::true_type{}, r1_end, k_hi);
+
+    const size_t slab = ((size_t)lbk * nchunk + chunk) * N + i;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        int j = jbase + r * 64 + lane;
+        if (j < Na) A.partial[slab * Na + j] = imp[r];
+    }
+    if (A.hitcount && nhits) atomicAdd(A.hitcount, (unsigned long long)nhits);
+}
+
+// ------------------------------------------------------------------------------ 4. merge
+template <int NP, bool LAB, int LB>
+__global__ void bell_merge_kernel(BellArgs A, int use_partial, int nlb, int nchunk) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    bool ok = false;
+    double d = 0.0;
+    const int N = A.N, Na = A.Na, Nl = A.Nl;
+    if (t < N * Na) {
+        int i = t / Na, j = t - i * Na;
+        const double* __restrict__ a = A.a;
+        double x = (1 + A.r) * a[j];
+        double y = A.w * A.s[i];
+        double best = A.best0[t];
+        int idx = A.idx0[t];
+        if (use_partial && idx != -2) {
+            const double* __restrict__ ev = A.EV + (size_t)i * Na;
+            for (int lbk = 0; lbk < nlb; ++lbk) {
+                double cm = -__builtin_inf();
+                for (int l = lbk * LB; l < min(lbk * LB + LB, Nl); ++l)
+                    cm = fmax(cm, cash<LAB>(x, y, LAB ? A.L[l] : 1.0));
+                int nch = (lower_bound_dev(a, Na, cm) + A.CK - 1) / A.CK;
+                for (int c = 0; c < nch; ++c) {
+                    int q = A.partial[(((size_t)lbk * nchunk + c) * N + i) * Na + j];
+                    if (q >= 0) {
+                        int l = q % Nl, k = q / Nl;
+                        double coh = cash<LAB>(x, y, LAB ? A.L[l] : 1.0);
+                        lexi_take(bell_val<NP, LAB>(coh - a[k], ev[k], A.sigma,
+                                                    LAB ? A.dis[l] : 0.0),
+                                  q, best, idx);
+                    }
+                }
+            }
+        }
+        double vo = A.v_old[t];
+        if (idx == -2 && LAB) {
+            // Labor_VFI.m:85: no feasible choice → v_new keeps its value: the incoming v_new
+            // on a first sweep, == v_old on later sweeps of a solve (:120 v_old = v_new)
+            best = A.keep_incoming ? A.v_new[t] : vo;
+        } else {
+            if (idx < 0) {  // all candidates NaN: max returns NaN at index 1
+                idx = 0;
+                best = __builtin_nan("");
+            }
+            int l = idx % Nl, k = idx / Nl;
+            double kp = a[k];
+            double coh = cash<LAB>(x, y, LAB ? A.L[l] : 1.0);
+            A.idx[t] = idx;
+            if (A.pk) A.pk[t] = kp;
+            if (A.pc) A.pc[t] = coh - kp;
+            if (LAB && A.pl) A.pl[t] = A.L[l];
+        }
+        A.v_new[t] = best;
+        d = fabs(best - vo);
+        ok = (d == d);
+    }
+    if (A.diff) {
+        unsigned long long key = ok ? nonneg_key(d) : 0ull;
+        unsigned long long anyok = __ballot(ok);
+        for (int off = 32; off > 0; off >>= 1) {
+            unsigned long long o = __shfl_xor(key, off);
+            key = o > key ? o : key;
+        }
+        if ((threadIdx.x & 63) == 0 && anyok) {
+            atomicMax(A.diff, key);
+            atomicOr(A.diff + 1, 1ull);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------ plain
+template <int NP, bool LAB>
+__global__ void bell_plain_kernel(BellArgs A) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= A.N * A.Na) return;
+    if (A.idx0[t] == -2) return;
+    const int Na = A.Na, Nl = A.Nl;
+    int i = t / Na, j = t - i * Na;
+    const double* __restrict__ a = A.a;
+    const double* __restrict__ ev = A.EV + (size_t)i * Na;
+    double x = (1 + A.r) * a[j], y = A.w * A.s[i];
+    double best = __builtin_nan("");
+    int idx = -1;
+    for (int l = 0; l < Nl; ++l) {
+        double coh = cash<LAB>(x, y, LAB ? A.L[l] : 1.0);
+        double dis = LAB ? A.dis[l] : 0.0;
+        int kf = lower_bound_dev(a, Na, coh);
+        for (int k = 0; k < kf; ++k)
+            lexi_take(bell_val<NP, LAB>(coh - a[k], ev[k], A.sigma, dis), l + Nl * k, best, idx);
+    }
+    A.best0[t] = best;
+    A.idx0[t] = idx;
+}
+
+// ------------------------------------------------------------------------------ launchers
+static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+int launch_bell_table(const BellArgs& A, hipStream_t st) {
+    int n = A.N * A.Na;
+    bell_table_kernel<<<cdiv(n, 256), 256, 0, st>>>(A.N, A.Na, A.P, A.v_old, A.beta, A.np, A.a,
+                                                    A.EV, A.np > 0 ? A.T : nullptr);
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
+}
+
+template <int NP, bool LAB>
+struct Geo {
+    static constexpr int R = LAB ? 1 : 2;
+    static constexpr int LB = LAB ? 5 : 1;
+};
+
+template <int NP, bool LAB>
+static void run_init(const BellArgs& A, hipStream_t st) {
+    bell_init_kernel<NP, LAB><<<cdiv(A.N * A.Na, 128), 128, 0, st>>>(A);
+}
+template <int NP, bool LAB>
+static void run_screen(const BellArgs& A, hipStream_t st) {
+    if constexpr (NP > 0) {
+        constexpr int R = Geo<NP, LAB>::R, LB = Geo<NP, LAB>::LB;
+        int ntile = cdiv(A.Na, 64 * R), nlb = cdiv(A.Nl, LB), nchunk = cdiv(A.Na, A.CK);
+        long long items = (long long)A.N * ntile * nlb * nchunk;
+        bell_screen_kernel<NP, LAB, R, LB, 8><<<cdiv(items, 4), 256, 0, st>>>(A, ntile, nlb, nchunk);
+    }
+}
+template <int NP, bool LAB>
+static void run_plain(const BellArgs& A, hipStream_t st) {
+    bell_plain_kernel<NP, LAB><<<cdiv(A.N * A.Na, 128), 128, 0, st>>>(A);
+}
+template <int NP, bool LAB>
+static void run_merge(const BellArgs& A, int use_partial, hipStream_t st) {
+    constexpr int LB = Geo<NP, LAB>::LB;
+    bell_merge_kernel<NP, LAB, LB><<<cdiv(A.N * A.Na, 256), 256, 0, st>>>(
+        A, use_partial, cdiv(A.Nl, LB), cdiv(A.Na, A.CK));
+}
+
+template <template <int, bool> class F, class... Args>
+static int dispatch(int np, bool lab, Args&&... args) {
+#define AIY_CASE(n)                                              \
+    case n:                                                      \
+        if (lab) F<n, true>::go(args...);                        \
+        else F<n, false>::go(args...);                           \
+        break;
+    switch (np) {
+        AIY_CASE(1) AIY_CASE(2) AIY_CASE(3) AIY_CASE(4) AIY_CASE(5) AIY_CASE(6) AIY_CASE(7)
+        AIY_CASE(8)
+        default:
+            if (lab) F<0, true>::go(args...);
+            else F<0, false>::go(args...);
+    }
+#undef AIY_CASE
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
+}
+template <int NP, bool LAB>
+struct InitF { static void go(const BellArgs& A, hipStream_t st) { run_init<NP, LAB>(A, st); } };
+template <int NP, bool LAB>
+struct ScreenF { static void go(const BellArgs& A, hipStream_t st) { run_screen<NP, LAB>(A, st); } };
+template <int NP, bool LAB>
+struct PlainF { static void go(const BellArgs& A, hipStream_t st) { run_plain<NP, LAB>(A, st); } };
+template <int NP, bool LAB>
+struct MergeF {
+    static void go(const BellArgs& A, int u, hipStream_t st) { run_merge<NP, LAB>(A, u, st); }
+};
+
+int launch_bell_init(const BellArgs& A, hipStream_t st) { return dispatch<InitF>(A.np, A.labor, A, st); }
+int launch_bell_screen(const BellArgs& A, hipStream_t st) {
+    if (A.np < 1 || A.np > 8) return fail(AIY_BAD_ARG, "screened sweep needs integer sigma in [2, 9]");
+    return dispatch<ScreenF>(A.np, A.labor, A, st);
+}
+int launch_bell_plain(const BellArgs& A, hipStream_t st) { return dispatch<PlainF>(A.np, A.labor, A, st); }
+int launch_bell_merge(const BellArgs& A, int use_partial, hipStream_t st) {
+    return dispatch<MergeF>(A.np, A.labor, A, use_partial, st);
+}
+
+size_t bell_partial_slots(const BellArgs& A) {
+    int LB = A.labor ? 5 : 1;
+    return (size_t)cdiv(A.Nl, LB) * cdiv(A.Na, A.CK) * A.N * A.Na;
+}
+
+}  // namespace aiy
+
+namespace aiy {
+// dis_l = psi * L_l^(1+eta) / (1+eta)   (Aiyagari_Endogenous_Labor_VFI.m:96)
+__global__ void disutility_kernel(const double* __restrict__ L, int Nl, double psi, double eta,
+                                  double* __restrict__ dis) {
+    int l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= Nl) return;
+    double e1 = 1 + eta;
+    double Lp;
+    if (e1 >= 1 && e1 < 64 && (double)(int)e1 == e1) Lp = aiy_ipow(L[l], (int)e1);
+    else Lp = pow(L[l], e1);
+    dis[l] = psi * Lp / (1 + eta);
+}
+int launch_disutility(const double* L, int Nl, double psi, double eta, double* dis,
+                      hipStream_t st) {
+    disutility_kernel<<<(Nl + 63) / 64, 64, 0, st>>>(L, Nl, psi, eta, dis);
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
+}
+}  // namespace aiy

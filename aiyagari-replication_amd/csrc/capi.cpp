@@ -52,23 +52,20 @@ static void dfree(T*& p) {
     p = nullptr;
 }
 
-int ws_ensure_vfi(aiy_ws* ws) {
+int ws_ensure_bell(aiy_ws* ws, size_t partial_slots) {
     size_t n = (size_t)ws->N * ws->Na;
     AIY_TRY(dalloc(&ws->EV, n));
     AIY_TRY(dalloc(&ws->T, n));
-    AIY_TRY(dalloc(&ws->coh, n));
     AIY_TRY(dalloc(&ws->best0, n));
-    AIY_TRY(dalloc(&ws->kf, n));
     AIY_TRY(dalloc(&ws->idx0, n));
-    int nchunk = (int)((ws->Na + ws->CK - 1) / ws->CK);
-    size_t need = (size_t)nchunk * n;
-    if (ws->partial && ws->partial_cap < need) dfree(ws->partial);
+    if (ws->partial && ws->partial_cap < partial_slots) dfree(ws->partial);
     if (!ws->partial) {
-        AIY_TRY(dalloc(&ws->partial, need));
-        ws->partial_cap = need;
+        AIY_TRY(dalloc(&ws->partial, partial_slots));
+        ws->partial_cap = partial_slots;
     }
     AIY_TRY(dalloc(&ws->diff, 2));
     AIY_TRY(dalloc(&ws->hitcount, 1));
+    AIY_TRY(dalloc(&ws->dis, (size_t)std::max<int64_t>(ws->Nl, 1)));
     if (!ws->hdiff) AIY_HIP(hipHostMalloc((void**)&ws->hdiff, 4 * sizeof(unsigned long long)));
     return AIY_OK;
 }
@@ -97,60 +94,63 @@ int ws_timing_drain(aiy_ws* ws) {
     return AIY_OK;
 }
 
-// ---------------------------------------------------------------------------- VFI sweep
-int vfi_sweep_dev(aiy_ws* ws, const double* v_old, const double* a, const double* s,
-                  const double* P, double r, double w, double beta, double sigma,
-                  const int* hint, int coarse_first, int mode, double* v_new, int* idx,
-                  double* pk, double* pc, double* diff_out, hipStream_t st) {
+// ---------------------------------------------------------------------------- Bellman sweep
+int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
-    if (!v_old || !a || !s || !P || !v_new || !idx)
+    if (!c.v_old || !c.a || !c.s || !c.P || !c.v_new || !c.idx)
         return fail(AIY_BAD_ARG, "NULL device pointer");
-    if (!(beta == beta) || !(r == r) || !(w == w) || !(sigma == sigma))
+    if (c.labor && (!c.L || c.Nl < 1 || c.Nl > ws->Nl))
+        return fail(AIY_BAD_ARG, "labour sweep needs labor_choice and 1 <= Nl <= workspace Nl");
+    if (!(c.beta == c.beta) || !(c.r == c.r) || !(c.w == c.w) || !(c.sigma == c.sigma))
         return fail(AIY_NON_FINITE, "non-finite scalar argument");
-    AIY_TRY(ws_ensure_vfi(ws));
-    VfiArgs A{};
+    BellArgs A{};
     A.N = (int)ws->N;
     A.Na = (int)ws->Na;
-    A.np = is_int_ge(sigma, 2.0) && sigma <= 9.0 ? (int)sigma - 1 : 0;
-    if (mode == 2) A.np = is_int_ge(sigma, 2.0) && sigma <= 9.0 ? (int)sigma - 1 : 0;
-    if (mode == 1 && A.np == 0)
+    A.Nl = c.labor ? (int)c.Nl : 1;
+    A.labor = c.labor;
+    A.keep_incoming = c.keep_incoming;
+    A.np = is_int_ge(c.sigma, 2.0) && c.sigma <= 9.0 ? (int)c.sigma - 1 : 0;
+    if (c.mode == 1 && A.np == 0)
         return fail(AIY_BAD_ARG, "screened sweep (mode 1) needs integer sigma in [2, 9]");
-    bool screened = (mode != 2) && A.np > 0;
-    A.coarse = (hint && !coarse_first) ? 0 : ws->coarse;
+    bool screened = (c.mode != 2) && A.np > 0;
+    A.coarse = ws->coarse;
     A.CK = ws->CK;
-    A.r = r;
-    A.w = w;
-    A.beta = beta;
-    A.sigma = sigma;
-    A.v_old = v_old;
-    A.a = a;
-    A.s = s;
-    A.P = P;
-    A.hint = hint;
+    A.r = c.r;
+    A.w = c.w;
+    A.beta = c.beta;
+    A.sigma = c.sigma;
+    A.v_old = c.v_old;
+    A.a = c.a;
+    A.s = c.s;
+    A.P = c.P;
+    A.L = c.labor ? c.L : nullptr;
+    A.hint = c.hint;
+    AIY_TRY(ws_ensure_bell(ws, bell_partial_slots(A)));
+    A.dis = c.labor ? ws->dis : nullptr;
     A.EV = ws->EV;
     A.T = ws->T;
-    A.coh = ws->coh;
-    A.kf = ws->kf;
     A.best0 = ws->best0;
     A.idx0 = ws->idx0;
     A.partial = ws->partial;
     A.hitcount = ws->count_hits ? ws->hitcount : nullptr;
-    A.v_new = v_new;
-    A.idx = idx;
-    A.pk = pk;
-    A.pc = pc;
+    A.v_new = c.v_new;
+    A.idx = c.idx;
+    A.pk = c.pk;
+    A.pl = c.pl;
+    A.pc = c.pc;
     A.diff = ws->diff;
+    if (c.labor) AIY_TRY(launch_disutility(c.L, (int)c.Nl, c.psi, c.eta, ws->dis, st));
     AIY_HIP(hipMemsetAsync(ws->diff, 0, 2 * sizeof(unsigned long long), st));
-    AIY_TRY(launch_vfi_table(A, st));
+    AIY_TRY(launch_bell_table(A, st));
     if (!screened) A.coarse = 0, A.hint = nullptr;
-    AIY_TRY(launch_vfi_init(A, st));
+    AIY_TRY(launch_bell_init(A, st));
     AIY_TRY(ws_timing_begin(ws, st));
-    if (screened) AIY_TRY(launch_vfi_screen(A, st));
-    else AIY_TRY(launch_vfi_plain(A, st));
+    if (screened) AIY_TRY(launch_bell_screen(A, st));
+    else AIY_TRY(launch_bell_plain(A, st));
     AIY_TRY(ws_timing_end(ws, st));
-    AIY_TRY(launch_vfi_merge(A, screened ? 1 : 0, st));
-    if (diff_out)
-        AIY_HIP(hipMemcpyAsync(diff_out, ws->diff, 2 * sizeof(unsigned long long),
+    AIY_TRY(launch_bell_merge(A, screened ? 1 : 0, st));
+    if (c.diff_out)
+        AIY_HIP(hipMemcpyAsync(c.diff_out, ws->diff, 2 * sizeof(unsigned long long),
                                hipMemcpyDeviceToDevice, st));
     return AIY_OK;
 }
@@ -165,26 +165,26 @@ int ws_read_diff(aiy_ws* ws, hipStream_t st, double* d) {
     return AIY_OK;
 }
 
-int vfi_solve_dev(aiy_ws* ws, double* v_a, double* v_b, const double* a, const double* s,
-                  const double* P, double r, double w, double beta, double sigma, double tol,
-                  int64_t max_iter, int mode, int* idx, double* pk, double* pc,
-                  const int* first_hint, int64_t* iters, int* out_new, hipStream_t st) {
+int bell_solve_dev(aiy_ws* ws, BellCall c, double* v_a, double* v_b, double tol,
+                   int64_t max_iter, int64_t* iters, int* out_new, hipStream_t st) {
     if (max_iter < 1) return fail(AIY_BAD_ARG, "max_iter must be >= 1");
     double* cur = v_a;
     double* nxt = v_b;
+    const int* first_hint = c.hint;
     int64_t it;
     for (it = 1; it <= max_iter; ++it) {
-        const int* hint = (it == 1) ? first_hint : idx;
-        AIY_TRY(vfi_sweep_dev(ws, cur, a, s, P, r, w, beta, sigma, hint, it == 1, mode, nxt,
-                              idx, pk, pc, nullptr, st));
+        c.hint = (it == 1) ? first_hint : c.idx;
+        c.keep_incoming = (it == 1);
+        c.v_old = cur;
+        c.v_new = nxt;
+        AIY_TRY(bell_sweep_dev(ws, c, st));
         double d;
         AIY_TRY(ws_read_diff(ws, st, &d));
-        if (d < tol) break;  // :85-86  (v_old keeps the previous iterate)
+        if (d < tol) break;  // Aiyagari_VFI.m:85-86 (v_old keeps the previous iterate)
         std::swap(cur, nxt); // :88
     }
     if (it > max_iter) {  // loop exhausted: v_old = v_new after the last sweep
         it = max_iter;
-        // after the final swap `cur` holds v_new; make the other buffer equal to it
         AIY_HIP(hipMemcpyAsync(nxt, cur, sizeof(double) * ws->N * ws->Na,
                                hipMemcpyDeviceToDevice, st));
         std::swap(cur, nxt);
@@ -291,8 +291,11 @@ int aiy_vfi_sweep_dev(aiy_ws* ws, const double* v_old, const double* a_grid, con
                       const double* P, double r, double w, double beta, double sigma,
                       const int32_t* hint, int mode, double* v_new, int32_t* idx,
                       double* policy_k, double* policy_c, double* diff, void* stream) {
-    return vfi_sweep_dev(ws, v_old, a_grid, s, P, r, w, beta, sigma, hint, hint == nullptr,
-                         mode, v_new, idx, policy_k, policy_c, diff, (hipStream_t)stream);
+    BellCall c{};
+    c.v_old = v_old; c.a = a_grid; c.s = s; c.P = P; c.r = r; c.w = w; c.beta = beta;
+    c.sigma = sigma; c.hint = hint; c.mode = mode; c.v_new = v_new; c.idx = idx;
+    c.pk = policy_k; c.pc = policy_c; c.diff_out = diff;
+    return bell_sweep_dev(ws, c, (hipStream_t)stream);
 }
 
 int aiy_vfi_solve_dev(aiy_ws* ws, double* v_a, double* v_b, const double* a_grid,
@@ -301,9 +304,24 @@ int aiy_vfi_solve_dev(aiy_ws* ws, double* v_a, double* v_b, const double* a_grid
                       double* policy_k, double* policy_c, int64_t* iters, int* out_new,
                       void* stream) {
     if (!iters || !out_new) return fail(AIY_BAD_ARG, "NULL iters/out_new");
-    return vfi_solve_dev(ws, v_a, v_b, a_grid, s, P, r, w, beta, sigma, tol, max_iter, mode,
-                         idx, policy_k, policy_c, nullptr, iters, out_new,
-                         (hipStream_t)stream);
+    BellCall c{};
+    c.a = a_grid; c.s = s; c.P = P; c.r = r; c.w = w; c.beta = beta; c.sigma = sigma;
+    c.mode = mode; c.idx = idx; c.pk = policy_k; c.pc = policy_c;
+    return bell_solve_dev(ws, c, v_a, v_b, tol, max_iter, iters, out_new, (hipStream_t)stream);
+}
+
+int aiy_labor_vfi_sweep_dev(aiy_ws* ws, const double* v_old, const double* a_grid,
+                            const double* s, const double* P, const double* labor_choice,
+                            double r, double w, double beta, double sigma, double psi,
+                            double eta, const int32_t* hint, double* v_new, int32_t* lin,
+                            double* policy_k, double* policy_l, double* policy_c, double* diff,
+                            void* stream) {
+    BellCall c{};
+    c.labor = true; c.Nl = ws ? ws->Nl : 0; c.L = labor_choice; c.psi = psi; c.eta = eta;
+    c.v_old = v_old; c.a = a_grid; c.s = s; c.P = P; c.r = r; c.w = w; c.beta = beta;
+    c.sigma = sigma; c.hint = hint; c.v_new = v_new; c.idx = lin; c.pk = policy_k;
+    c.pl = policy_l; c.pc = policy_c; c.diff_out = diff;
+    return bell_sweep_dev(ws, c, (hipStream_t)stream);
 }
 
 }  // extern "C"

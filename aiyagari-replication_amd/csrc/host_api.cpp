@@ -128,12 +128,15 @@ static int vfi_host(const double* v_old_cm, const double* a, const double* s, co
     cm_to_rows(v_old_cm, N, Na, rows.data());
     AIY_HIP(hipMemcpyAsync(dva, rows.data(), nb, hipMemcpyHostToDevice, c->st));
     int out_new = 1;
+    BellCall bc{};
+    bc.a = da; bc.s = ds; bc.P = dP; bc.r = r; bc.w = w; bc.beta = beta; bc.sigma = sigma;
+    bc.idx = didx; bc.pk = dpk; bc.pc = dpc;
     if (solve) {
-        AIY_TRY(vfi_solve_dev(c->ws, dva, dvb, da, ds, dP, r, w, beta, sigma, tol, max_iter, 0,
-                              didx, dpk, dpc, nullptr, iters, &out_new, c->st));
+        AIY_TRY(bell_solve_dev(c->ws, bc, dva, dvb, tol, max_iter, iters, &out_new, c->st));
     } else {
-        AIY_TRY(vfi_sweep_dev(c->ws, dva, da, ds, dP, r, w, beta, sigma, nullptr, 1, 0, dvb,
-                              didx, dpk, dpc, nullptr, c->st));
+        bc.v_old = dva;
+        bc.v_new = dvb;
+        AIY_TRY(bell_sweep_dev(c->ws, bc, c->st));
     }
     double* dnew = out_new ? dvb : dva;
     double* dold = out_new ? dva : dvb;
@@ -153,6 +156,83 @@ static int vfi_host(const double* v_old_cm, const double* a, const double* s, co
         AIY_HIP(hipStreamSynchronize(c->st));
         for (int64_t j = 0; j < Na; ++j)
             for (int64_t i = 0; i < N; ++i) idx_cm[i + j * N] = ib[i * Na + j] + 1;
+    }
+    return AIY_OK;
+}
+
+// A3 host tier: VFI arrays N x Na column-major; v_new and policies in/out.
+static int labor_host(const double* v_old_cm, const double* a, const double* s, const double* P,
+                      const double* L, int64_t N, int64_t Na, int64_t Nl, double r, double w,
+                      double beta, double sigma, double psi, double eta, bool solve, double tol,
+                      int64_t max_iter, double* v_old_out_cm, double* v_new_cm, double* pk_cm,
+                      double* pl_cm, double* pc_cm, int32_t* lin_cm, int64_t* iters) {
+    if (!v_old_cm || !s || !P || !L || !v_new_cm || !pk_cm || !pl_cm || !pc_cm)
+        return fail(AIY_BAD_ARG, "NULL argument");
+    if (N < 1 || Na < 2 || Nl < 1) return fail(AIY_BAD_SHAPE, "need N >= 1, Na >= 2, Nl >= 1");
+    AIY_TRY(check_grid(a, Na));
+    std::lock_guard<std::mutex> lk(g_mu);
+    HostCtx* c;
+    AIY_TRY(get_ctx(N, Na, Nl, &c));
+    double *da, *ds, *dP, *dva, *dvb, *dpk, *dpc, *dpl, *dL;
+    int* dlin;
+    AIY_TRY(stage_common(c, a, s, P, N, Na, &da, &ds, &dP));
+    size_t nb = sizeof(double) * N * Na;
+    AIY_TRY(c->buf("va", nb, (void**)&dva));
+    AIY_TRY(c->buf("vb", nb, (void**)&dvb));
+    AIY_TRY(c->buf("pk", nb, (void**)&dpk));
+    AIY_TRY(c->buf("pc", nb, (void**)&dpc));
+    AIY_TRY(c->buf("pl", nb, (void**)&dpl));
+    AIY_TRY(c->buf("L", sizeof(double) * Nl, (void**)&dL));
+    AIY_TRY(c->buf("idx", sizeof(int) * N * Na, (void**)&dlin));
+    std::vector<double> rows(N * Na), tmp(N * Na);
+    std::vector<int> ib(N * Na);
+    auto up = [&](const double* cm, double* d) -> int {
+        cm_to_rows(cm, N, Na, rows.data());
+        AIY_HIP(hipMemcpyAsync(d, rows.data(), nb, hipMemcpyHostToDevice, c->st));
+        AIY_HIP(hipStreamSynchronize(c->st));
+        return AIY_OK;
+    };
+    AIY_TRY(up(v_old_cm, dva));
+    AIY_TRY(up(v_new_cm, dvb));  // in/out: states without a feasible choice keep these
+    AIY_TRY(up(pk_cm, dpk));
+    AIY_TRY(up(pl_cm, dpl));
+    AIY_TRY(up(pc_cm, dpc));
+    for (int64_t j = 0; j < Na; ++j)
+        for (int64_t i = 0; i < N; ++i) ib[i * Na + j] = lin_cm ? lin_cm[i + j * N] - 1 : 0;
+    AIY_HIP(hipMemcpyAsync(dlin, ib.data(), sizeof(int) * N * Na, hipMemcpyHostToDevice, c->st));
+    AIY_HIP(hipMemcpyAsync(dL, L, sizeof(double) * Nl, hipMemcpyHostToDevice, c->st));
+    int out_new = 1;
+    BellCall bc{};
+    bc.labor = true; bc.Nl = Nl; bc.L = dL; bc.psi = psi; bc.eta = eta;
+    bc.a = da; bc.s = ds; bc.P = dP; bc.r = r; bc.w = w; bc.beta = beta; bc.sigma = sigma;
+    bc.idx = dlin; bc.pk = dpk; bc.pl = dpl; bc.pc = dpc;
+    if (solve) {
+        // the MATLAB loop keeps v_new across sweeps; at sweep 1 the ping-pong partner of
+        // v_old must hold the incoming v_new, which merge copies from v_old where needed
+        AIY_TRY(bell_solve_dev(c->ws, bc, dva, dvb, tol, max_iter, iters, &out_new, c->st));
+    } else {
+        bc.v_old = dva;
+        bc.v_new = dvb;
+        AIY_TRY(bell_sweep_dev(c->ws, bc, c->st));
+    }
+    double* dnew = out_new ? dvb : dva;
+    double* dold = out_new ? dva : dvb;
+    auto back = [&](const double* d, double* cm) -> int {
+        AIY_HIP(hipMemcpyAsync(tmp.data(), d, nb, hipMemcpyDeviceToHost, c->st));
+        AIY_HIP(hipStreamSynchronize(c->st));
+        rows_to_cm(tmp.data(), N, Na, cm);
+        return AIY_OK;
+    };
+    AIY_TRY(back(dnew, v_new_cm));
+    AIY_TRY(back(dpk, pk_cm));
+    AIY_TRY(back(dpl, pl_cm));
+    AIY_TRY(back(dpc, pc_cm));
+    if (solve && v_old_out_cm) AIY_TRY(back(dold, v_old_out_cm));
+    if (lin_cm) {
+        AIY_HIP(hipMemcpyAsync(ib.data(), dlin, sizeof(int) * N * Na, hipMemcpyDeviceToHost, c->st));
+        AIY_HIP(hipStreamSynchronize(c->st));
+        for (int64_t j = 0; j < Na; ++j)
+            for (int64_t i = 0; i < N; ++i) lin_cm[i + j * N] = ib[i * Na + j] + 1;
     }
     return AIY_OK;
 }
@@ -177,6 +257,27 @@ int aiy_vfi_solve(double* v_old, const double* a_grid, const double* s, const do
     if (!iters) return fail(AIY_BAD_ARG, "NULL iters");
     return vfi_host(v_old, a_grid, s, P, N, Na, r, w, beta, sigma, true, tol, max_iter, v_old,
                     v_new, policy_k, policy_c, policy_idx, iters);
+}
+
+int aiy_labor_vfi_sweep(const double* v_old, const double* a_grid, const double* s,
+                        const double* P, const double* labor_choice, int64_t N, int64_t Na,
+                        int64_t Nl, double r, double w, double beta, double sigma, double psi,
+                        double eta, double* v_new, double* policy_k, double* policy_l,
+                        double* policy_c, int32_t* policy_lin) {
+    return labor_host(v_old, a_grid, s, P, labor_choice, N, Na, Nl, r, w, beta, sigma, psi, eta,
+                      false, 0, 1, nullptr, v_new, policy_k, policy_l, policy_c, policy_lin,
+                      nullptr);
+}
+
+int aiy_labor_vfi_solve(double* v_old, const double* a_grid, const double* s, const double* P,
+                        const double* labor_choice, int64_t N, int64_t Na, int64_t Nl, double r,
+                        double w, double beta, double sigma, double psi, double eta, double tol,
+                        int64_t max_iter, double* v_new, double* policy_k, double* policy_l,
+                        double* policy_c, int32_t* policy_lin, int64_t* iters) {
+    if (!iters) return fail(AIY_BAD_ARG, "NULL iters");
+    return labor_host(v_old, a_grid, s, P, labor_choice, N, Na, Nl, r, w, beta, sigma, psi, eta,
+                      true, tol, max_iter, v_old, v_new, policy_k, policy_l, policy_c,
+                      policy_lin, iters);
 }
 
 }  // extern "C"

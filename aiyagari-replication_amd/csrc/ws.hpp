@@ -5,21 +5,20 @@
 #include <vector>
 
 #include "../../include/aiyagari_hip.h"
-#include "vfi_kernels.hpp"
+#include "bellman.hpp"
 
 struct aiy_ws {
     int64_t N = 0, Na = 0, Nl = 1;
     int dev = 0;
     // search knobs (aiy_ws_set_search)
-    int coarse = 64;
+    int coarse = 128;
     int CK = 1024;
     // VFI scratch
     double* EV = nullptr;
     double2* T = nullptr;
-    double* coh = nullptr;
     double* best0 = nullptr;
-    int* kf = nullptr;
     int* idx0 = nullptr;
+    double* dis = nullptr;
     int* partial = nullptr;
     size_t partial_cap = 0;
     unsigned long long* diff = nullptr;      // device [2]
@@ -38,11 +37,11 @@ struct aiy_ws {
     int64_t launches = 0;
 
     void free_all() {
-        void* ps[] = {EV, T, coh, best0, kf, idx0, partial, diff, hitcount, g0, g1, g2, gi};
+        void* ps[] = {EV, T, best0, idx0, dis, partial, diff, hitcount, g0, g1, g2, gi};
         for (void* p : ps)
             if (p) (void)hipFree(p);
         if (hdiff) (void)hipHostFree(hdiff);
-        EV = nullptr; T = nullptr; coh = nullptr; best0 = nullptr; kf = nullptr;
+        EV = nullptr; T = nullptr; best0 = nullptr; dis = nullptr;
         idx0 = nullptr; partial = nullptr; diff = nullptr; hitcount = nullptr; hdiff = nullptr;
         g0 = g1 = g2 = nullptr; gi = nullptr;
         partial_cap = 0;
@@ -50,17 +49,34 @@ struct aiy_ws {
 };
 
 namespace aiy {
-int ws_ensure_vfi(aiy_ws* ws);
+struct BellCall {
+    bool labor = false;
+    int64_t Nl = 1;
+    const double* L = nullptr;
+    double psi = 0, eta = 0;
+    const double* v_old = nullptr;
+    const double* a = nullptr;
+    const double* s = nullptr;
+    const double* P = nullptr;
+    double r = 0, w = 0, beta = 0, sigma = 0;
+    const int* hint = nullptr;
+    int mode = 0;
+    bool keep_incoming = true;
+    double* v_new = nullptr;
+    int* idx = nullptr;
+    double* pk = nullptr;
+    double* pl = nullptr;
+    double* pc = nullptr;
+    double* diff_out = nullptr;
+};
+int ws_ensure_bell(aiy_ws* ws, size_t partial_slots);
 int ws_timing_begin(aiy_ws* ws, hipStream_t st);
 int ws_timing_end(aiy_ws* ws, hipStream_t st);
 int ws_timing_drain(aiy_ws* ws);
 int ws_read_diff(aiy_ws* ws, hipStream_t st, double* d);
-int vfi_sweep_dev(aiy_ws* ws, const double* v_old, const double* a, const double* s,
-                  const double* P, double r, double w, double beta, double sigma,
-                  const int* hint, int coarse_first, int mode, double* v_new, int* idx,
-                  double* pk, double* pc, double* diff_out, hipStream_t st);
-int vfi_solve_dev(aiy_ws* ws, double* v_a, double* v_b, const double* a, const double* s,
-                  const double* P, double r, double w, double beta, double sigma, double tol,
-                  int64_t max_iter, int mode, int* idx, double* pk, double* pc,
-                  const int* first_hint, int64_t* iters, int* out_new, hipStream_t st);
+int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st);
+int bell_solve_dev(aiy_ws* ws, BellCall c, double* v_a, double* v_b, double tol,
+                   int64_t max_iter, int64_t* iters, int* out_new, hipStream_t st);
+int launch_disutility(const double* L, int Nl, double psi, double eta, double* dis,
+                      hipStream_t st);
 }  // namespace aiy

@@ -100,3 +100,63 @@ class Workspace:
                                       ip(mode), ptr(idx), ptr(policy_k), ptr(policy_c),
                                       C.byref(it), C.byref(which), stream_handle(stream)))
         return it.value, which.value
+
+
+# ------------------------------------------------------------------------------------ A3
+def _labor_call(fn, v_old, a_grid, s, P, labor_choice, r, w, beta, sigma, psi, eta, extra,
+                v_new=None, pol=None):
+    v_old = np.array(v_old, dtype=np.float64, order="F", copy=True)
+    N, Na = v_old.shape
+    L = np.ascontiguousarray(labor_choice, np.float64)
+    a_grid, s = np.ascontiguousarray(a_grid, np.float64), np.ascontiguousarray(s, np.float64)
+    P = _f(P)
+    v_new = np.zeros((N, Na), order="F") if v_new is None else np.array(v_new, np.float64, order="F")
+    if pol is None:
+        pol = (np.zeros((N, Na)), np.zeros((N, Na)), np.zeros((N, Na)), np.ones((N, Na), np.int32))
+    pk, pl, pc = (np.array(p, np.float64, order="F") for p in pol[:3])
+    lin = np.array(pol[3], np.int32, order="F")
+    out = fn(ptr(v_old), ptr(a_grid), ptr(s), ptr(P), ptr(L), i64(N), i64(Na), i64(L.size), d(r),
+             d(w), d(beta), d(sigma), d(psi), d(eta), *extra(v_new, pk, pl, pc, lin))
+    check(out)
+    return v_old, v_new, pk, pl, pc, lin
+
+
+def labor_vfi_sweep(v_old, a_grid, s, P, labor_choice, r, w, beta, sigma, psi, eta,
+                    v_new=None, policies=None):
+    """Replaces Aiyagari_Endogenous_Labor_VFI.m:69-112.  v_new/policies are in/out (states
+    without a feasible (l, a') keep them, :85).  Returns v_new, policy_k, policy_l, policy_c,
+    lin (1-based column-major index into the Nl x Na choice matrix)."""
+    _, v_new, pk, pl, pc, lin = _labor_call(
+        lib().aiy_labor_vfi_sweep, v_old, a_grid, s, P, labor_choice, r, w, beta, sigma, psi,
+        eta, lambda vn, pk, pl, pc, lin: (ptr(vn), ptr(pk), ptr(pl), ptr(pc), ptr(lin)),
+        v_new, policies)
+    return v_new, pk, pl, pc, lin
+
+
+def labor_vfi_solve(v_old, a_grid, s, P, labor_choice, r, w, beta, sigma, psi, eta, tol=1e-5,
+                    max_iter=1000, v_new=None, policies=None):
+    """Replaces Aiyagari_Endogenous_Labor_VFI.m:64-122."""
+    it = C.c_int64(0)
+
+    def extra(vn, pk, pl, pc, lin):
+        return (d(tol), i64(max_iter), ptr(vn), ptr(pk), ptr(pl), ptr(pc), ptr(lin), C.byref(it))
+
+    v_old_out, v_new, pk, pl, pc, lin = _labor_call(
+        lambda *a: lib().aiy_labor_vfi_solve(*a), v_old, a_grid, s, P, labor_choice, r, w, beta,
+        sigma, psi, eta, extra, v_new, policies)
+    return dict(v_new=v_new, v_old=v_old_out, policy_k=pk, policy_l=pl, policy_c=pc, lin=lin,
+                iters=it.value)
+
+
+def _ws_labor_sweep(self, v_old, a_grid, s, P, labor_choice, r, w, beta, sigma, psi, eta, v_new,
+                    lin, policy_k=None, policy_l=None, policy_c=None, hint=None, diff=None,
+                    stream=None):
+    """A3 on device; v_new and the policies are in/out."""
+    check(lib().aiy_labor_vfi_sweep_dev(self._h, ptr(v_old), ptr(a_grid), ptr(s), ptr(P),
+                                        ptr(labor_choice), d(r), d(w), d(beta), d(sigma),
+                                        d(psi), d(eta), ptr(hint), ptr(v_new), ptr(lin),
+                                        ptr(policy_k), ptr(policy_l), ptr(policy_c), ptr(diff),
+                                        stream_handle(stream)))
+
+
+Workspace.labor_vfi_sweep = _ws_labor_sweep

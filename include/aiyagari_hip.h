@@ -60,6 +60,20 @@ int aiy_vfi_solve(double* v_old, const double* a_grid, const double* s, const do
                   double tol, int64_t max_iter, double* v_new, double* policy_k,
                   double* policy_c, int32_t* policy_idx, int64_t* iters);
 
+/* A3 — replaces Aiyagari_Endogenous_Labor_VFI.m:69-112 / :64-122.  v_new and the policies
+ * are in/out: states with no feasible (l, a') keep their incoming values (:85).
+ * policy_lin (nullable) = 1-based column-major index into the Nl x Na choice matrix. */
+int aiy_labor_vfi_sweep(const double* v_old, const double* a_grid, const double* s,
+                        const double* P, const double* labor_choice, int64_t N, int64_t Na,
+                        int64_t Nl, double r, double w, double beta, double sigma, double psi,
+                        double eta, double* v_new, double* policy_k, double* policy_l,
+                        double* policy_c, int32_t* policy_lin);
+int aiy_labor_vfi_solve(double* v_old, const double* a_grid, const double* s, const double* P,
+                        const double* labor_choice, int64_t N, int64_t Na, int64_t Nl, double r,
+                        double w, double beta, double sigma, double psi, double eta, double tol,
+                        int64_t max_iter, double* v_new, double* policy_k, double* policy_l,
+                        double* policy_c, int32_t* policy_lin, int64_t* iters);
+
 /* ======================================================================================
  * Device tier: [N][Na] (z-major) arrays in HBM, async on `stream` (hipStream_t).
  * A workspace holds the per-shape scratch (EV/D tables, init/partial buffers, events).
@@ -90,6 +104,12 @@ int aiy_vfi_solve_dev(aiy_ws* ws, double* v_a, double* v_b, const double* a_grid
                       double sigma, double tol, int64_t max_iter, int mode, int32_t* idx,
                       double* policy_k, double* policy_c, int64_t* iters, int* out_new,
                       void* stream);
+int aiy_labor_vfi_sweep_dev(aiy_ws* ws, const double* v_old, const double* a_grid,
+                            const double* s, const double* P, const double* labor_choice,
+                            double r, double w, double beta, double sigma, double psi,
+                            double eta, const int32_t* hint, double* v_new, int32_t* lin,
+                            double* policy_k, double* policy_l, double* policy_c, double* diff,
+                            void* stream);
 #ifdef __cplusplus
 }
 #endif

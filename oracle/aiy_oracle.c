@@ -141,7 +141,8 @@ int orc_labor_vfi_sweep(int64_t N, int64_t Na, int64_t Nl, const double* v_old,
                 double val;
                 if (c > 0) {
                     any = 1;
-                    double u = (sigma == 1.0) ? log(c) : (crra_p(c, sigma) - 1) / (1 - sigma);
+                    /* :95 has no sigma == 1 branch (0/0 = NaN there, as in MATLAB) */
+                    double u = (crra_p(c, sigma) - 1) / (1 - sigma);
                     val = (u - dis[l]) + ev[k];        /* :95-99 */
                 } else {
                     val = -INFINITY + ev[k];           /* utility = -Inf */

@@ -1,0 +1,67 @@
+"""GPU parity for A3 (Aiyagari_Endogenous_Labor_VFI.m:64-122): joint (l, a') max in
+column-major order, bit-exact against the golden fixture (numpy restatement) and the C oracle."""
+import numpy as np
+import pytest
+
+from oracle import corc
+from oracle import np_oracle as no
+
+pytestmark = pytest.mark.gpu
+
+
+def test_labor_solve_matches_golden_bitwise(pkg, gpu, golden):
+    g = golden("a3_labor_vfi_na100")
+    R = pkg.labor_vfi_solve(np.zeros((7, 100)), g["a_grid"], g["s"], g["P"], g["L"],
+                            float(g["r"]), float(g["w"]), 0.96, 5.0, 1.0, 2.0)
+    assert R["iters"] == int(g["iters"])
+    for k in ("v_new", "v_old", "policy_k", "policy_l", "policy_c"):
+        assert np.array_equal(R[k], g[k]), k
+    assert np.array_equal(R["lin"] - 1, g["lin"])
+
+
+@pytest.mark.parametrize("Na", [400, 1333])
+def test_labor_sweep_vs_oracle(pkg, gpu, Na):
+    cal = no.calib_aiyagari(Na=Na, rho=0.6, sigma_e=0.2)
+    a, s, P = cal["a_grid"], cal["s"], cal["P"]
+    L = 0.01 + (1.5 - 0.01) * no.matlab_linspace01(10)
+    w = no.wage(0.04, 0.36, 0.08)
+    V = corc.labor_vfi_solve(np.zeros((7, Na)), a, s, P, L, 0.04, w, 0.96, 5.0, 1.0, 2.0,
+                             1e-5, 12)["v_new"]
+    v, pk, pl, pc, lin = pkg.labor_vfi_sweep(V, a, s, P, L, 0.04, w, 0.96, 5.0, 1.0, 2.0)
+    vo, (pko, plo, pco, lino) = corc.labor_vfi_sweep(V, a, s, P, L, 0.04, w, 0.96, 5.0, 1.0, 2.0)
+    assert np.array_equal(v, vo)
+    assert np.array_equal(lin - 1, lino)
+    assert np.array_equal(pk, pko) and np.array_equal(pl, plo) and np.array_equal(pc, pco)
+
+
+def test_labor_nonuniform_levels_and_sigma(pkg, gpu):
+    """Unsorted labour grid, odd Nl (ragged last block), σ = 3 and non-integer η."""
+    cal = no.calib_aiyagari(Na=257, rho=0.6, sigma_e=0.2, sigma=3.0)
+    a, s, P = cal["a_grid"], cal["s"], cal["P"]
+    L = np.array([0.7, 0.05, 1.2, 0.3, 1.0, 0.5, 0.9])
+    w = no.wage(0.03, 0.36, 0.08)
+    V = corc.labor_vfi_solve(np.zeros((7, 257)), a, s, P, L, 0.03, w, 0.96, 3.0, 1.0, 1.5,
+                             1e-5, 8)["v_new"]
+    v, pk, pl, pc, lin = pkg.labor_vfi_sweep(V, a, s, P, L, 0.03, w, 0.96, 3.0, 1.0, 1.5)
+    vo, (pko, plo, pco, lino) = corc.labor_vfi_sweep(V, a, s, P, L, 0.03, w, 0.96, 3.0, 1.0, 1.5)
+    # eta = 1.5 → L^(2.5) via pow on both sides (device vs glibc: ulp level)
+    assert np.max(np.abs(v - vo)) < 1e-10
+    assert (lin - 1 == lino).mean() > 0.999
+
+
+def test_labor_infeasible_state_keeps_incoming(pkg, gpu):
+    """A state whose cash on hand is below a_grid(1) for every labour level keeps v_new and the
+    policies it came in with (:85)."""
+    a = np.array([5.0, 6.0, 7.0])
+    s = np.array([0.1])
+    L = np.array([0.5, 1.0])
+    v_in = np.full((1, 3), 42.0)
+    pol = (np.full((1, 3), 1.5), np.full((1, 3), 2.5), np.full((1, 3), 3.5), np.full((1, 3), 7, np.int32))
+    v, pk, pl, pc, lin = pkg.labor_vfi_sweep(np.zeros((1, 3)), a, s, np.ones((1, 1)), L, -0.5,
+                                             1.0, 0.9, 5.0, 1.0, 2.0, v_new=v_in, policies=pol)
+    vo, (pko, plo, pco, lino) = corc.labor_vfi_sweep(np.zeros((1, 3)), a, s, np.ones((1, 1)), L,
+                                                    -0.5, 1.0, 0.9, 5.0, 1.0, 2.0,
+                                                    v_new=v_in, pol=(pol[0], pol[1], pol[2], pol[3] - 1))
+    assert np.array_equal(v, vo)
+    assert np.array_equal(pk, pko) and np.array_equal(pl, plo) and np.array_equal(pc, pco)
+    assert np.array_equal(lin - 1, lino)
