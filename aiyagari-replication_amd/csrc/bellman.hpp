@@ -25,6 +25,8 @@ struct BellArgs {
     double2* T;
     double* best0;
     int* idx0;
+    int* kf;       // [Nl][N][Na] feasible prefix lengths #{k : a_k < coh(j, l)}
+    bool kf_valid; // kf already holds the values for (r, w, a, s, L)
     int* partial;
     unsigned long long* hitcount;  // nullable
     // outputs
@@ -37,6 +39,7 @@ struct BellArgs {
 };
 
 int launch_bell_table(const BellArgs& A, hipStream_t st);
+int launch_bell_kf(const BellArgs& A, hipStream_t st);
 int launch_bell_init(const BellArgs& A, hipStream_t st);
 int launch_bell_screen(const BellArgs& A, hipStream_t st);
 int launch_bell_plain(const BellArgs& A, hipStream_t st);

@@ -89,6 +89,19 @@ __global__ void bell_table_kernel(int N, int Na, const double* __restrict__ P,
     }
 }
 
+// ------------------------------------------------------------------------------ 1b. kf
+// feasible prefix per (l, i, j): depends on (r, w, a, s, L) only, so a solve computes it once
+template <bool LAB>
+__global__ void bell_kf_kernel(BellArgs A) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    int n = A.N * A.Na;
+    if (t >= n * A.Nl) return;
+    int l = t / n, ij = t - l * n;
+    int i = ij / A.Na, j = ij - i * A.Na;
+    double coh = cash<LAB>((1 + A.r) * A.a[j], A.w * A.s[i], LAB ? A.L[l] : 1.0);
+    A.kf[t] = lower_bound_dev(A.a, A.Na, coh);
+}
+
 // ------------------------------------------------------------------------------ 2. init
 template <int NP, bool LAB>
 __global__ void bell_init_kernel(BellArgs A) {
@@ -107,41 +120,52 @@ __global__ void bell_init_kernel(BellArgs A) {
         double dis = LAB ? A.dis[l] : 0.0;
         return bell_val<NP, LAB>(coh - a[k], ev[k], A.sigma, dis);
     };
+    const int n_all = A.N * Na;
+    const int S = A.coarse;
+    int hl = -1, hk = -1;
     if (A.hint) {
         int h = A.hint[t];
-        int l = h % Nl, k = h / Nl;
-        if (h >= 0 && l >= 0 && l < Nl) {
-            double coh = cash<LAB>(x, y, LAB ? A.L[l] : 1.0);
-            int kf = lower_bound_dev(a, Na, coh);
+        if (h >= 0 && h % Nl < Nl) {
+            hl = h % Nl;
+            int kf = A.kf[hl * n_all + t];
             if (kf > 0) {
-                k = k >= kf ? kf - 1 : k;
-                lexi_take(eval(l, k, coh), l + Nl * k, best, idx);
+                hk = min(h / Nl, kf - 1);
+                double coh = cash<LAB>(x, y, LAB ? A.L[hl] : 1.0);
+                lexi_take(eval(hl, hk, coh), hl + Nl * hk, best, idx);
             }
         }
     }
-    const int S = A.coarse;
     for (int l = 0; l < Nl; ++l) {
-        double coh = cash<LAB>(x, y, LAB ? A.L[l] : 1.0);
-        int kf = lower_bound_dev(a, Na, coh);
+        int kf = A.kf[l * n_all + t];
         if (kf == 0) continue;
         anyfeas = true;
-        if (S <= 0) {
-            if (!A.hint) lexi_take(eval(l, 0, coh), l, best, idx);
-            continue;
-        }
-        // coarse scan of this labour level, then bracket refinement around its best point
+        double coh = cash<LAB>(x, y, LAB ? A.L[l] : 1.0);
         double lb = __builtin_nan("");
         int lk = -1;
-        for (int k = 0; k < kf; k += S) lexi_take(eval(l, k, coh), k, lb, lk);
-        lexi_take(eval(l, kf - 1, coh), kf - 1, lb, lk);
-        if (lk >= 0) {
-            for (int step = S >> 1; step >= 1; step >>= 1) {
-                int c0 = lk;
-                if (c0 - step >= 0) lexi_take(eval(l, c0 - step, coh), c0 - step, lb, lk);
-                if (c0 + step < kf) lexi_take(eval(l, c0 + step, coh), c0 + step, lb, lk);
-            }
-            lexi_take(lb, l + Nl * lk, best, idx);
+        int step0;
+        if (A.hint && hk >= 0 && l != hl) continue;  // only the global best sets the bar
+        if (A.hint && hk >= 0) {
+            // warm start: climb from last sweep's argmax (steps S/2 .. 1, both sides)
+            lk = hk < kf ? hk : kf - 1;
+            lb = eval(l, lk, coh);
+            step0 = S >> 1;
+        } else if (S > 0) {
+            // cold start: coarse scan of the feasible prefix
+            for (int k = 0; k < kf; k += S) lexi_take(eval(l, k, coh), k, lb, lk);
+            lexi_take(eval(l, kf - 1, coh), kf - 1, lb, lk);
+            step0 = S >> 1;
+        } else {
+            lexi_take(eval(l, 0, coh), 0, lb, lk);
+            step0 = 0;
         }
+        if (lk < 0 || lb != lb) continue;
+        // bracket refinement: for a unimodal objective this lands on the maximiser
+        for (int step = step0; step >= 1; step >>= 1) {
+            int c0 = lk;
+            if (c0 - step >= 0) lexi_take(eval(l, c0 - step, coh), c0 - step, lb, lk);
+            if (c0 + step < kf) lexi_take(eval(l, c0 + step, coh), c0 + step, lb, lk);
+        }
+        lexi_take(lb, l + Nl * lk, best, idx);
     }
     A.best0[t] = best;
     A.idx0[t] = anyfeas ? idx : -2;  // -2: no feasible choice at all
@@ -218,10 +242,11 @@ __global__ __launch_bounds__(256) void bell_screen_kernel(BellArgs A, int ntile,
 #pragma unroll
                 for (int q = 0; q < LB; ++q) {
                     double c = coh[r][q] - tk.x;
-                    if (c > 0 && (tk.y - B[r][q]) * aiy_ipow(c, NP) >= kThr) {
+                    int lin = (l0 + q) + Nl * k;
+                    // the running best itself always passes; its value is already known
+                    if (lin != idx[r] && c > 0 && (tk.y - B[r][q]) * aiy_ipow(c, NP) >= kThr) {
                         ++nhits;
                         double val = bell_val<NP, LAB>(c, ev[k], A.sigma, dis[q]);
-                        int lin = (l0 + q) + Nl * k;
                         if (lexi_take(val, lin, best[r], idx[r])) {
                             imp[r] = lin;
 #pragma unroll
@@ -299,10 +324,10 @@ __global__ void bell_merge_kernel(BellArgs A, int use_partial, int nlb, int nchu
         if (use_partial && idx != -2) {
             const double* __restrict__ ev = A.EV + (size_t)i * Na;
             for (int lbk = 0; lbk < nlb; ++lbk) {
-                double cm = -__builtin_inf();
+                int kfm = 0;
                 for (int l = lbk * LB; l < min(lbk * LB + LB, Nl); ++l)
-                    cm = fmax(cm, cash<LAB>(x, y, LAB ? A.L[l] : 1.0));
-                int nch = (lower_bound_dev(a, Na, cm) + A.CK - 1) / A.CK;
+                    kfm = max(kfm, A.kf[(size_t)l * N * Na + t]);
+                int nch = (kfm + A.CK - 1) / A.CK;
                 for (int c = 0; c < nch; ++c) {
                     int q = A.partial[(((size_t)lbk * nchunk + c) * N + i) * Na + j];
                     if (q >= 0) {
@@ -367,7 +392,7 @@ __global__ void bell_plain_kernel(BellArgs A) {
     for (int l = 0; l < Nl; ++l) {
         double coh = cash<LAB>(x, y, LAB ? A.L[l] : 1.0);
         double dis = LAB ? A.dis[l] : 0.0;
-        int kf = lower_bound_dev(a, Na, coh);
+        int kf = A.kf[(size_t)l * A.N * Na + t];
         for (int k = 0; k < kf; ++k)
             lexi_take(bell_val<NP, LAB>(coh - a[k], ev[k], A.sigma, dis), l + Nl * k, best, idx);
     }
@@ -382,6 +407,14 @@ int launch_bell_table(const BellArgs& A, hipStream_t st) {
     int n = A.N * A.Na;
     bell_table_kernel<<<cdiv(n, 256), 256, 0, st>>>(A.N, A.Na, A.P, A.v_old, A.beta, A.np, A.a,
                                                     A.EV, A.np > 0 ? A.T : nullptr);
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
+}
+
+int launch_bell_kf(const BellArgs& A, hipStream_t st) {
+    int n = A.N * A.Na * A.Nl;
+    if (A.labor) bell_kf_kernel<true><<<cdiv(n, 256), 256, 0, st>>>(A);
+    else bell_kf_kernel<false><<<cdiv(n, 256), 256, 0, st>>>(A);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }

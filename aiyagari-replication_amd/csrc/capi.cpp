@@ -140,6 +140,26 @@ int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
     A.pc = c.pc;
     A.diff = ws->diff;
     if (c.labor) AIY_TRY(launch_disutility(c.L, (int)c.Nl, c.psi, c.eta, ws->dis, st));
+    // feasible prefixes: cached while (r, w, a, s, L) are unchanged (aiy_ws_invalidate resets)
+    size_t kf_need = (size_t)A.Nl * A.N * A.Na;
+    if (ws->kf && ws->kf_cap < kf_need) {
+        (void)hipFree(ws->kf);
+        ws->kf = nullptr;
+        ws->kf_ok = false;
+    }
+    if (!ws->kf) {
+        AIY_HIP(hipMalloc((void**)&ws->kf, kf_need * sizeof(int)));
+        ws->kf_cap = kf_need;
+    }
+    A.kf = ws->kf;
+    bool fresh = ws->kf_ok && ws->kf_r == c.r && ws->kf_w == c.w && ws->kf_a == c.a &&
+                 ws->kf_s == c.s && ws->kf_L == A.L && ws->kf_Nl == A.Nl && ws->kf_lab == A.labor;
+    if (!fresh) {
+        AIY_TRY(launch_bell_kf(A, st));
+        ws->kf_ok = true;
+        ws->kf_r = c.r; ws->kf_w = c.w; ws->kf_a = c.a; ws->kf_s = c.s; ws->kf_L = A.L;
+        ws->kf_Nl = A.Nl; ws->kf_lab = A.labor;
+    }
     AIY_HIP(hipMemsetAsync(ws->diff, 0, 2 * sizeof(unsigned long long), st));
     AIY_TRY(launch_bell_table(A, st));
     if (!screened) A.coarse = 0, A.hint = nullptr;
@@ -268,6 +288,12 @@ int aiy_ws_timing(aiy_ws* ws, double* total_ms, int64_t* launches, int64_t* hits
             AIY_HIP(hipMemcpy(&h, ws->hitcount, sizeof h, hipMemcpyDeviceToHost));
         *hits = (int64_t)h;
     }
+    return AIY_OK;
+}
+
+int aiy_ws_invalidate(aiy_ws* ws) {
+    if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
+    ws->kf_ok = false;
     return AIY_OK;
 }
 

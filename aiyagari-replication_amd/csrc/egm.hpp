@@ -1,0 +1,24 @@
+// Launch interface of the EGM kernels (egm_kernels.hip): A4 and A5 (labor = true).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace aiy {
+struct EgmArgs {
+    int N, Na;
+    bool labor;
+    int ns;  // sigma when sigma is an integer in [1, 63] (c^-sigma = 1/c^sigma), else 0
+    double r, w, beta, sigma, amin, phi, theta;
+    const double* c;  // policy_c [N][Na]
+    const double* a;
+    const double* s;
+    const double* P;  // row-major N x N
+    double* ahat;     // scratch [N][Na]
+    double* cnext;    // scratch [N][Na]
+    double* cout;     // policy_c_next
+    double* pk;
+    double* pl;       // A5 (nullable)
+    unsigned long long* diff;  // [2]
+    unsigned* flags;           // bit 0: a_hat not increasing
+};
+int launch_egm_step(const EgmArgs& A, hipStream_t st);
+}  // namespace aiy

@@ -100,6 +100,7 @@ int stage_common(HostCtx* c, const double* a, const double* s, const double* P, 
     AIY_HIP(hipMemcpyAsync(*ds, s, sizeof(double) * N, hipMemcpyHostToDevice, c->st));
     AIY_HIP(hipMemcpyAsync(*dP, Pr.data(), sizeof(double) * N * N, hipMemcpyHostToDevice, c->st));
     AIY_HIP(hipStreamSynchronize(c->st));
+    aiy_ws_invalidate(c->ws);  // the staged a/s contents may differ from the last call
     return AIY_OK;
 }
 

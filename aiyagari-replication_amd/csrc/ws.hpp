@@ -19,6 +19,16 @@ struct aiy_ws {
     double* best0 = nullptr;
     int* idx0 = nullptr;
     double* dis = nullptr;
+    int* kf = nullptr;
+    size_t kf_cap = 0;
+    // key of the cached kf table (feasible prefixes depend on r, w, a, s, L only)
+    bool kf_ok = false;
+    double kf_r = 0, kf_w = 0;
+    const void* kf_a = nullptr;
+    const void* kf_s = nullptr;
+    const void* kf_L = nullptr;
+    int64_t kf_Nl = 0;
+    bool kf_lab = false;
     int* partial = nullptr;
     size_t partial_cap = 0;
     unsigned long long* diff = nullptr;      // device [2]
@@ -37,11 +47,12 @@ struct aiy_ws {
     int64_t launches = 0;
 
     void free_all() {
-        void* ps[] = {EV, T, best0, idx0, dis, partial, diff, hitcount, g0, g1, g2, gi};
+        void* ps[] = {EV, T, best0, idx0, dis, kf, partial, diff, hitcount, g0, g1, g2, gi};
         for (void* p : ps)
             if (p) (void)hipFree(p);
         if (hdiff) (void)hipHostFree(hdiff);
-        EV = nullptr; T = nullptr; best0 = nullptr; dis = nullptr;
+        EV = nullptr; T = nullptr; best0 = nullptr; dis = nullptr; kf = nullptr; kf_cap = 0;
+        kf_ok = false;
         idx0 = nullptr; partial = nullptr; diff = nullptr; hitcount = nullptr; hdiff = nullptr;
         g0 = g1 = g2 = nullptr; gi = nullptr;
         partial_cap = 0;

@@ -80,6 +80,10 @@ class Workspace:
         check(lib().aiy_ws_timing(self._h, C.byref(ms), C.byref(n), C.byref(hits)))
         return ms.value, n.value, hits.value
 
+    def invalidate(self):
+        """Drop the cached feasibility table (after overwriting a_grid/s/L in place)."""
+        check(lib().aiy_ws_invalidate(self._h))
+
     def set_search(self, coarse_stride=0, k_chunk=1024):
         check(lib().aiy_ws_set_search(self._h, ip(coarse_stride), ip(k_chunk)))
 

@@ -74,6 +74,28 @@ int aiy_labor_vfi_solve(double* v_old, const double* a_grid, const double* s, co
                         int64_t max_iter, double* v_new, double* policy_k, double* policy_l,
                         double* policy_c, int32_t* policy_lin, int64_t* iters);
 
+/* A4 — replaces Aiyagari_EGM.m:75-107 (one pass) and :71-110 (the while loop).
+ * policy_c Na x N in; policy_c_next, policy_k Na x N out; dist = max|Δc|. */
+int aiy_egm_step(const double* policy_c, const double* a_grid, const double* s,
+                 const double* P, int64_t N, int64_t Na, double r, double w, double beta,
+                 double sigma, double amin, double* policy_c_next, double* policy_k,
+                 double* dist);
+int aiy_egm_solve(double* policy_c, const double* a_grid, const double* s, const double* P,
+                  int64_t N, int64_t Na, double r, double w, double beta, double sigma,
+                  double amin, double tol, int64_t max_iter, double* policy_k, double* dist,
+                  int64_t* iters);
+/* A5 — replaces Aiyagari_Endogenous_Labor_EGM.m:68-104 / :67-107. */
+int aiy_labor_egm_step(const double* policy_c, const double* a_grid, const double* s,
+                       const double* P, int64_t N, int64_t Na, double r, double w, double beta,
+                       double sigma, double phi, double theta, double amin,
+                       double* policy_c_next, double* policy_k, double* policy_l,
+                       double* dist);
+int aiy_labor_egm_solve(double* policy_c, const double* a_grid, const double* s,
+                        const double* P, int64_t N, int64_t Na, double r, double w,
+                        double beta, double sigma, double phi, double theta, double amin,
+                        double tol, int64_t max_iter, double* policy_k, double* policy_l,
+                        double* dist, int64_t* iters);
+
 /* ======================================================================================
  * Device tier: [N][Na] (z-major) arrays in HBM, async on `stream` (hipStream_t).
  * A workspace holds the per-shape scratch (EV/D tables, init/partial buffers, events).
@@ -85,6 +107,10 @@ int aiy_ws_destroy(aiy_ws* ws);
  * stream; aiy_ws_timing reads the accumulated milliseconds and launch count. */
 int aiy_ws_set_timing(aiy_ws* ws, int enable);
 int aiy_ws_timing(aiy_ws* ws, double* total_ms, int64_t* launches, int64_t* hits);
+/* The workspace caches the feasible prefixes #{k : a_k < cash(j, l)}, which depend on
+ * (r, w, a_grid, s, labor_choice) only, keyed by r, w and the pointers.  Call this after
+ * overwriting a_grid / s / labor_choice in place. */
+int aiy_ws_invalidate(aiy_ws* ws);
 /* search knobs (defaults tuned for gfx950): coarse stride for cold starts, k-chunk. */
 int aiy_ws_set_search(aiy_ws* ws, int coarse_stride, int k_chunk);
 
@@ -110,6 +136,11 @@ int aiy_labor_vfi_sweep_dev(aiy_ws* ws, const double* v_old, const double* a_gri
                             double eta, const int32_t* hint, double* v_new, int32_t* lin,
                             double* policy_k, double* policy_l, double* policy_c, double* diff,
                             void* stream);
+int aiy_egm_step_dev(aiy_ws* ws, const double* policy_c, const double* a_grid,
+                     const double* s, const double* P, double r, double w, double beta,
+                     double sigma, double amin, int labor, double phi, double theta,
+                     double* policy_c_next, double* policy_k, double* policy_l, double* diff,
+                     void* stream);
 #ifdef __cplusplus
 }
 #endif
