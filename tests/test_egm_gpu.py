@@ -59,7 +59,7 @@ def test_egm_large_and_nonint(pkg, gpu, Na, sigma, theta):
 def test_egm_nonmonotone_grid_is_reported(pkg, gpu):
     """interp1 needs a monotone endogenous grid; a decreasing one is an error, not garbage."""
     a = np.linspace(0, 10, 50)
-    pc0 = np.tile(np.linspace(5, 0.01, 50)[:, None], (1, 2))  # c decreasing in a → â folds
+    pc0 = np.tile(np.linspace(50, 0.01, 50)[:, None], (1, 2))  # steeply decreasing c → â folds
     with pytest.raises(pkg.AiyError) as e:
         pkg.egm_step(pc0, a, np.array([1.0, 1.2]), np.full((2, 2), 0.5), 0.02, 1.0, 0.96, 5.0, 0.0)
     assert e.value.status == "AIY_BAD_ARG"
