@@ -64,6 +64,42 @@ __device__ __forceinline__ unsigned long long nonneg_key(double x) {
     return (unsigned long long)aiy_dbits(x);
 }
 
+// ---------------------------------------------------------------- max |Δ| reduction
+// max|v_new - v_old| ignoring NaN (MATLAB max(..., 'all')): wave shuffles, then LDS across
+// the block's waves, then ONE atomicMax per block on IEEE bits (order-independent, hence
+// deterministic) into slot blockIdx % kDiffSlots, so no single address is contended.
+constexpr int kDiffSlots = 64;
+__device__ __forceinline__ void block_max_to_slots(bool ok, double d,
+                                                   unsigned long long* __restrict__ slots) {
+    __shared__ unsigned long long s_key[16];
+    __shared__ int s_any[16];
+    unsigned long long key = ok ? (unsigned long long)aiy_dbits(d) : 0ull;
+    int any = __ballot(ok) != 0ull;
+    for (int off = 32; off > 0; off >>= 1) {
+        unsigned long long o = __shfl_xor(key, off);
+        key = o > key ? o : key;
+    }
+    const int wave = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        s_key[wave] = key;
+        s_any[wave] = any;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long k = 0;
+        int a = 0;
+        for (int q = 0; q < nw; ++q) {
+            k = s_key[q] > k ? s_key[q] : k;
+            a |= s_any[q];
+        }
+        if (a) {
+            unsigned long long* sl = slots + 2 * (blockIdx.x % kDiffSlots);
+            atomicMax(sl, k);
+            atomicOr(sl + 1, 1ull);
+        }
+    }
+}
+
 inline int is_int_ge(double x, double lo) {
     return x >= lo && x < 64 && (double)(int64_t)x == x;
 }

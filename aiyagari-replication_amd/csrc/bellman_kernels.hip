@@ -41,8 +41,8 @@ __device__ __forceinline__ double bell_val(double c, double ev, double sigma, do
         double p = 1.0 / aiy_ipow(c, NP);  // c.^(1-sigma), sigma = NP + 1
         u = (p - 1) / (1 - sigma);
     } else {
-        if (!LAB && sigma == 1.0) u = log(c);  // Aiyagari_VFI.m:74-75 (labour script has no branch)
-        else u = (pow(c, 1.0 - sigma) - 1) / (1 - sigma);
+        if (!LAB && sigma == 1.0) u = aiy_log(c);  // Aiyagari_VFI.m:74-75 (labour script: no branch)
+        else u = (aiy_pow(c, 1.0 - sigma) - 1) / (1 - sigma);
     }
     if constexpr (LAB) return (u - dis) + ev;  // Labor_VFI.m:95-99
     else return u + ev;                        // Aiyagari_VFI.m:79
@@ -142,22 +142,18 @@ __global__ void bell_init_kernel(BellArgs A) {
         double coh = cash<LAB>(x, y, LAB ? A.L[l] : 1.0);
         double lb = __builtin_nan("");
         int lk = -1;
-        int step0;
-        if (A.hint && hk >= 0 && l != hl) continue;  // only the global best sets the bar
-        if (A.hint && hk >= 0) {
-            // warm start: climb from last sweep's argmax (steps S/2 .. 1, both sides)
-            lk = hk < kf ? hk : kf - 1;
-            lb = eval(l, lk, coh);
-            step0 = S >> 1;
-        } else if (S > 0) {
-            // cold start: coarse scan of the feasible prefix
+        // with a hint only its labour level is searched: one good candidate sets the bar
+        if (A.hint && hk >= 0 && l != hl) continue;
+        if (S > 0) {  // coarse scan of the feasible prefix (robust when the policy moved far)
             for (int k = 0; k < kf; k += S) lexi_take(eval(l, k, coh), k, lb, lk);
             lexi_take(eval(l, kf - 1, coh), kf - 1, lb, lk);
-            step0 = S >> 1;
-        } else {
-            lexi_take(eval(l, 0, coh), 0, lb, lk);
-            step0 = 0;
         }
+        if (A.hint && hk >= 0) {  // warm start: last sweep's argmax
+            int k = hk < kf ? hk : kf - 1;
+            lexi_take(eval(l, k, coh), k, lb, lk);
+        }
+        if (lk < 0) lexi_take(eval(l, 0, coh), 0, lb, lk);
+        int step0 = S > 0 ? (S >> 1) : 64;
         if (lk < 0 || lb != lb) continue;
         // bracket refinement: for a unimodal objective this lands on the maximiser
         for (int step = step0; step >= 1; step >>= 1) {
@@ -362,18 +358,7 @@ __global__ void bell_merge_kernel(BellArgs A, int use_partial, int nlb, int nchu
         d = fabs(best - vo);
         ok = (d == d);
     }
-    if (A.diff) {
-        unsigned long long key = ok ? nonneg_key(d) : 0ull;
-        unsigned long long anyok = __ballot(ok);
-        for (int off = 32; off > 0; off >>= 1) {
-            unsigned long long o = __shfl_xor(key, off);
-            key = o > key ? o : key;
-        }
-        if ((threadIdx.x & 63) == 0 && anyok) {
-            atomicMax(A.diff, key);
-            atomicOr(A.diff + 1, 1ull);
-        }
-    }
+    block_max_to_slots(ok, d, A.diff);
 }
 
 // ------------------------------------------------------------------------------ plain
@@ -501,10 +486,7 @@ __global__ void disutility_kernel(const double* __restrict__ L, int Nl, double p
                                   double* __restrict__ dis) {
     int l = blockIdx.x * blockDim.x + threadIdx.x;
     if (l >= Nl) return;
-    double e1 = 1 + eta;
-    double Lp;
-    if (e1 >= 1 && e1 < 64 && (double)(int)e1 == e1) Lp = aiy_ipow(L[l], (int)e1);
-    else Lp = pow(L[l], e1);
+    double Lp = aiy_pow(L[l], 1 + eta);
     dis[l] = psi * Lp / (1 + eta);
 }
 int launch_disutility(const double* L, int Nl, double psi, double eta, double* dis,
@@ -512,5 +494,40 @@ int launch_disutility(const double* L, int Nl, double psi, double eta, double* d
     disutility_kernel<<<(Nl + 63) / 64, 64, 0, st>>>(L, Nl, psi, eta, dis);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
+}
+}  // namespace aiy
+
+namespace aiy {
+// fold the kDiffSlots {max bits, any} slots into one {max bits, any} pair (device → device)
+__global__ void reduce_slots_kernel(const unsigned long long* __restrict__ slots,
+                                   unsigned long long* __restrict__ out) {
+    int l = threadIdx.x;
+    unsigned long long k = slots[2 * l];
+    int any = __ballot(slots[2 * l + 1] != 0ull) != 0ull;
+    for (int off = 32; off > 0; off >>= 1) {
+        unsigned long long o = __shfl_xor(k, off);
+        k = o > k ? o : k;
+    }
+    if (l == 0) {
+        out[0] = k;
+        out[1] = any ? 1ull : 0ull;
+    }
+}
+int launch_reduce_slots(const unsigned long long* slots, void* out, hipStream_t st) {
+    static_assert(kDiffSlots == 64, "one wave folds the slots");
+    reduce_slots_kernel<<<1, 64, 0, st>>>(slots, (unsigned long long*)out);
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
+}
+// host-side fold of slots copied back (pinned)
+double fold_slots_host(const unsigned long long* h) {
+    unsigned long long k = 0;
+    bool any = false;
+    for (int q = 0; q < kDiffSlots; ++q) {
+        if (h[2 * q + 1]) any = true;
+        k = h[2 * q] > k ? h[2 * q] : k;
+    }
+    if (!any) return __builtin_nan("");
+    return aiy_bitsd(k);
 }
 }  // namespace aiy

@@ -63,10 +63,11 @@ int ws_ensure_bell(aiy_ws* ws, size_t partial_slots) {
         AIY_TRY(dalloc(&ws->partial, partial_slots));
         ws->partial_cap = partial_slots;
     }
-    AIY_TRY(dalloc(&ws->diff, 2));
+    AIY_TRY(dalloc(&ws->diff, 2 * kDiffSlots));
     AIY_TRY(dalloc(&ws->hitcount, 1));
     AIY_TRY(dalloc(&ws->dis, (size_t)std::max<int64_t>(ws->Nl, 1)));
-    if (!ws->hdiff) AIY_HIP(hipHostMalloc((void**)&ws->hdiff, 4 * sizeof(unsigned long long)));
+    if (!ws->hdiff)
+        AIY_HIP(hipHostMalloc((void**)&ws->hdiff, (2 * kDiffSlots + 4) * sizeof(unsigned long long)));
     return AIY_OK;
 }
 
@@ -160,7 +161,7 @@ int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
         ws->kf_r = c.r; ws->kf_w = c.w; ws->kf_a = c.a; ws->kf_s = c.s; ws->kf_L = A.L;
         ws->kf_Nl = A.Nl; ws->kf_lab = A.labor;
     }
-    AIY_HIP(hipMemsetAsync(ws->diff, 0, 2 * sizeof(unsigned long long), st));
+    AIY_HIP(hipMemsetAsync(ws->diff, 0, 2 * kDiffSlots * sizeof(unsigned long long), st));
     AIY_TRY(launch_bell_table(A, st));
     if (!screened) A.coarse = 0, A.hint = nullptr;
     AIY_TRY(launch_bell_init(A, st));
@@ -169,19 +170,16 @@ int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
     else AIY_TRY(launch_bell_plain(A, st));
     AIY_TRY(ws_timing_end(ws, st));
     AIY_TRY(launch_bell_merge(A, screened ? 1 : 0, st));
-    if (c.diff_out)
-        AIY_HIP(hipMemcpyAsync(c.diff_out, ws->diff, 2 * sizeof(unsigned long long),
-                               hipMemcpyDeviceToDevice, st));
+    if (c.diff_out) AIY_TRY(launch_reduce_slots(ws->diff, c.diff_out, st));
     return AIY_OK;
 }
 
 // read {max|Δ| bits, any} from the workspace diff word (synchronises the stream)
 int ws_read_diff(aiy_ws* ws, hipStream_t st, double* d) {
-    AIY_HIP(hipMemcpyAsync(ws->hdiff, ws->diff, 2 * sizeof(unsigned long long),
+    AIY_HIP(hipMemcpyAsync(ws->hdiff, ws->diff, 2 * kDiffSlots * sizeof(unsigned long long),
                            hipMemcpyDeviceToHost, st));
     AIY_HIP(hipStreamSynchronize(st));
-    if (ws->hdiff[1] == 0) *d = NAN;
-    else memcpy(d, &ws->hdiff[0], sizeof(double));
+    *d = fold_slots_host(ws->hdiff);
     return AIY_OK;
 }
 

@@ -19,8 +19,10 @@ static int ensure_egm(aiy_ws* ws) {
     if (!ws->g0) AIY_HIP(hipMalloc((void**)&ws->g0, n * sizeof(double)));
     if (!ws->g1) AIY_HIP(hipMalloc((void**)&ws->g1, n * sizeof(double)));
     if (!ws->gi) AIY_HIP(hipMalloc((void**)&ws->gi, 16 * sizeof(int)));
-    if (!ws->diff) AIY_HIP(hipMalloc((void**)&ws->diff, 2 * sizeof(unsigned long long)));
-    if (!ws->hdiff) AIY_HIP(hipHostMalloc((void**)&ws->hdiff, 4 * sizeof(unsigned long long)));
+    if (!ws->diff)
+        AIY_HIP(hipMalloc((void**)&ws->diff, 2 * kDiffSlots * sizeof(unsigned long long)));
+    if (!ws->hdiff)
+        AIY_HIP(hipHostMalloc((void**)&ws->hdiff, (2 * kDiffSlots + 4) * sizeof(unsigned long long)));
     return AIY_OK;
 }
 
@@ -42,26 +44,24 @@ int egm_step_dev(aiy_ws* ws, const double* c, const double* a, const double* s, 
     A.ahat = ws->g0; A.cnext = ws->g1; A.cout = cout; A.pk = pk; A.pl = pl;
     A.diff = ws->diff;
     A.flags = (unsigned*)ws->gi;
-    AIY_HIP(hipMemsetAsync(ws->diff, 0, 2 * sizeof(unsigned long long), st));
+    AIY_HIP(hipMemsetAsync(ws->diff, 0, 2 * kDiffSlots * sizeof(unsigned long long), st));
     AIY_HIP(hipMemsetAsync(ws->gi, 0, sizeof(int), st));
     AIY_TRY(ws_timing_begin(ws, st));
     AIY_TRY(launch_egm_step(A, st));
     AIY_TRY(ws_timing_end(ws, st));
-    if (diff_out)
-        AIY_HIP(hipMemcpyAsync(diff_out, ws->diff, 2 * sizeof(unsigned long long),
-                               hipMemcpyDeviceToDevice, st));
+    if (diff_out) AIY_TRY(launch_reduce_slots(ws->diff, diff_out, st));
     return AIY_OK;
 }
 
 // dist of the last step + the non-monotone-grid flag (synchronises)
 static int read_egm(aiy_ws* ws, hipStream_t st, double* d) {
-    AIY_HIP(hipMemcpyAsync(ws->hdiff, ws->diff, 2 * sizeof(unsigned long long),
+    unsigned long long* h = ws->hdiff;
+    AIY_HIP(hipMemcpyAsync(h, ws->diff, 2 * kDiffSlots * sizeof(unsigned long long),
                            hipMemcpyDeviceToHost, st));
-    AIY_HIP(hipMemcpyAsync(ws->hdiff + 2, ws->gi, sizeof(int), hipMemcpyDeviceToHost, st));
+    AIY_HIP(hipMemcpyAsync(h + 2 * kDiffSlots, ws->gi, sizeof(int), hipMemcpyDeviceToHost, st));
     AIY_HIP(hipStreamSynchronize(st));
-    if (ws->hdiff[1] == 0) *d = NAN;
-    else memcpy(d, &ws->hdiff[0], sizeof(double));
-    if ((unsigned)ws->hdiff[2] & 1u)
+    *d = fold_slots_host(h);
+    if ((unsigned)h[2 * kDiffSlots] & 1u)
         return fail(AIY_BAD_ARG, "endogenous grid a_hat is not increasing: interp1 in the "
                                  "reference would sort it or fail (Aiyagari_EGM.m:95)");
     return AIY_OK;

@@ -19,13 +19,13 @@
 namespace aiy {
 
 __device__ __forceinline__ double uprime_dev(double c, double sigma, int ns) {
-    return ns > 0 ? 1.0 / aiy_ipow(c, ns) : pow(c, -sigma);  // c.^(-sigma)
+    return ns > 0 ? 1.0 / aiy_ipow(c, ns) : aiy_pow(c, -sigma);  // c.^(-sigma)
 }
 
 __device__ __forceinline__ double labor_dev(double c, double ws, double sigma, int ns,
                                             double phi, double theta) {
     double x = (ws * uprime_dev(c, sigma, ns)) / phi;  // u_prime_l_inv(w s .* u_prime_c(c))
-    return (1.0 / theta == 1.0) ? x : pow(x, 1.0 / theta);
+    return (1.0 / theta == 1.0) ? x : aiy_pow(x, 1.0 / theta);
 }
 
 template <int NMAX>
@@ -44,7 +44,7 @@ __global__ void egm_rhs_kernel(EgmArgs A) {
 #pragma unroll
         for (int m = 0; m < NMAX; ++m)
             if (m < N) acc = acc + (coef0 * A.P[j * N + m]) * up[m];
-        double cn = pow(acc, -1.0 / A.sigma);  // :88
+        double cn = aiy_pow(acc, -1.0 / A.sigma);  // :88
         double ws = A.w * A.s[j];
         double ah;
         if (A.labor) {
@@ -90,16 +90,7 @@ __global__ void egm_interp_kernel(EgmArgs A) {
         d = fabs(cn - A.c[t]);
         ok = (d == d);
     }
-    unsigned long long key = ok ? nonneg_key(d) : 0ull;
-    unsigned long long anyok = __ballot(ok);
-    for (int off = 32; off > 0; off >>= 1) {
-        unsigned long long o = __shfl_xor(key, off);
-        key = o > key ? o : key;
-    }
-    if ((threadIdx.x & 63) == 0 && anyok) {
-        atomicMax(A.diff, key);
-        atomicOr(A.diff + 1, 1ull);
-    }
+    block_max_to_slots(ok, d, A.diff);
 }
 
 int launch_egm_step(const EgmArgs& A, hipStream_t st) {

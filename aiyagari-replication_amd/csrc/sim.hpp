@@ -1,0 +1,22 @@
+// Launch interface of the Monte-Carlo capital-supply kernel (sim_kernels.hip, A9).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+namespace aiy {
+struct SimArgs {
+    int N, Na, T;
+    int z1;         // 0-based sim_z(1)
+    double k1;      // sim_k(1)
+    const double* pol;  // policy_k: element (z, k) at pol[z*zs + k*as]
+    size_t zs, as;
+    const double* a;
+    const double* P;    // row-major N x N
+    const double* U;    // T-1 uniforms
+    double* out;        // [1] mean(sim_k)
+    double* sim_k;      // nullable [T]
+    int* sim_z;         // nullable [T], 0-based
+    int* status;        // [1] 0 ok, 1 find() empty
+};
+int launch_sim_capital(const SimArgs& A, hipStream_t st);
+}  // namespace aiy

@@ -31,9 +31,9 @@ struct aiy_ws {
     bool kf_lab = false;
     int* partial = nullptr;
     size_t partial_cap = 0;
-    unsigned long long* diff = nullptr;      // device [2]
+    unsigned long long* diff = nullptr;      // device [2*kDiffSlots] {max bits, any}
     unsigned long long* hitcount = nullptr;  // device [1]
-    unsigned long long* hdiff = nullptr;     // pinned host [4]
+    unsigned long long* hdiff = nullptr;     // pinned host [2*kDiffSlots + 4]
     // generic scratch used by the EGM / distribution / simulation kernels
     double* g0 = nullptr;
     double* g1 = nullptr;
@@ -88,6 +88,8 @@ int ws_read_diff(aiy_ws* ws, hipStream_t st, double* d);
 int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st);
 int bell_solve_dev(aiy_ws* ws, BellCall c, double* v_a, double* v_b, double tol,
                    int64_t max_iter, int64_t* iters, int* out_new, hipStream_t st);
+int launch_reduce_slots(const unsigned long long* slots, void* out, hipStream_t st);
+double fold_slots_host(const unsigned long long* h);
 int launch_disutility(const double* L, int Nl, double psi, double eta, double* dis,
                       hipStream_t st);
 }  // namespace aiy

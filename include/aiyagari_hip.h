@@ -96,6 +96,14 @@ int aiy_labor_egm_solve(double* policy_c, const double* a_grid, const double* s,
                         double tol, int64_t max_iter, double* policy_k, double* policy_l,
                         double* dist, int64_t* iters);
 
+/* A9 — replaces the simulation block Aiyagari_VFI.m:104-129 (:174-193 in the GE loop).
+ * policy_k: N x Na (vfi_layout=1) or Na x N (vfi_layout=0, EGM scripts); z1 is 1-based
+ * (sim_z(1)); k1 = sim_k(1); uniforms = the T-1 `rand` draws of :106.  Outputs mean(sim_k)
+ * and, if non-NULL, the T-long sim_k path and 1-based sim_z path. */
+int aiy_sim_capital(const double* policy_k, int vfi_layout, const double* a_grid,
+                    const double* P, int64_t N, int64_t Na, int64_t z1, double k1, int64_t T,
+                    const double* uniforms, double* k_supply, double* sim_k, int32_t* sim_z);
+
 /* ======================================================================================
  * Device tier: [N][Na] (z-major) arrays in HBM, async on `stream` (hipStream_t).
  * A workspace holds the per-shape scratch (EV/D tables, init/partial buffers, events).
@@ -141,6 +149,12 @@ int aiy_egm_step_dev(aiy_ws* ws, const double* policy_c, const double* a_grid,
                      double sigma, double amin, int labor, double phi, double theta,
                      double* policy_c_next, double* policy_k, double* policy_l, double* diff,
                      void* stream);
+/* A9 on device: policy_rows [N][Na]; z1 0-based; k_supply (device double), sim_k/sim_z
+ * nullable (device), status (device int32: 0 ok, 1 = find() empty). */
+int aiy_sim_capital_dev(aiy_ws* ws, const double* policy_rows, const double* a_grid,
+                        const double* P, int64_t z1, double k1, int64_t T,
+                        const double* uniforms, double* k_supply, double* sim_k,
+                        int32_t* sim_z, int32_t* status, void* stream);
 #ifdef __cplusplus
 }
 #endif

@@ -23,18 +23,14 @@ int orc_num_threads(int n) {
 #endif
 }
 
-static int is_int_ge(double x, double lo) { return x >= lo && floor(x) == x && x < 64; }
 
+/* Powers and logs use the portable aiy_pow / aiy_log (aiy_math.h, shared with the kernels):
+ * integer exponents by binary powering, otherwise exp(y*log x) in plain IEEE operations, so
+ * the restatement and the HIP kernels agree bit for bit.  MATLAB's own libm is unpinned. */
 /* c.^(1-sigma)  (Aiyagari_VFI.m:77) */
-static double crra_p(double c, double sigma) {
-    if (is_int_ge(sigma, 2)) return 1.0 / aiy_ipow(c, (int)sigma - 1);
-    return pow(c, 1.0 - sigma);
-}
+static double crra_p(double c, double sigma) { return aiy_pow(c, 1.0 - sigma); }
 /* c.^(-sigma)  (Aiyagari_EGM.m:68) */
-static double uprime(double c, double sigma) {
-    if (is_int_ge(sigma, 1)) return 1.0 / aiy_ipow(c, (int)sigma);
-    return pow(c, -sigma);
-}
+static double uprime(double c, double sigma) { return aiy_pow(c, -sigma); }
 
 /* (beta*P(i,:))*v_old(:,k), m ascending (Aiyagari_VFI.m:79) */
 static void ev_rows(int64_t N, int64_t Na, const double* P, const double* V, double beta,
@@ -66,7 +62,7 @@ int orc_vfi_sweep(int64_t N, int64_t Na, const double* v_old, const double* a_gr
         for (int64_t k = 0; k < Na; ++k) {
             double c = coh - a_grid[k];
             if (c <= 0) continue; /* :73 NaN, ignored by max */
-            double u = (sigma == 1.0) ? log(c) : (crra_p(c, sigma) - 1) / (1 - sigma);
+            double u = (sigma == 1.0) ? aiy_log(c) : (crra_p(c, sigma) - 1) / (1 - sigma);
             double val = u + ev[k];
             if (isnan(val)) continue;
             if (bk < 0 || val > best) { /* first maximiser */
@@ -123,7 +119,7 @@ int orc_labor_vfi_sweep(int64_t N, int64_t Na, int64_t Nl, const double* v_old,
     ev_rows(N, Na, P, v_old, beta, EV); /* :69 EV = beta*P*v_old */
     for (int64_t l = 0; l < Nl; ++l) {
         double e1 = 1 + eta;
-        double Lp = is_int_ge(e1, 1) ? aiy_ipow(L[l], (int)e1) : pow(L[l], e1);
+        double Lp = aiy_pow(L[l], e1);
         dis[l] = psi * Lp / (1 + eta); /* :96 */
     }
 #pragma omp parallel for schedule(dynamic, 16)
@@ -234,7 +230,7 @@ int orc_egm_step(int64_t N, int64_t Na, const double* pc, const double* a_grid,
     egm_rhs(N, Na, pc, P, r, beta, sigma, RHS);
     for (int64_t ja = 0; ja < N * Na; ++ja) {
         int64_t j = ja / Na, a = ja % Na;
-        double cn = pow(RHS[ja], -1.0 / sigma);           /* :88 */
+        double cn = aiy_pow(RHS[ja], -1.0 / sigma);       /* :88 */
         ah[ja] = ((cn + a_grid[a]) - w * s[j]) / (1 + r);  /* :92 */
     }
 #pragma omp parallel for schedule(static)
@@ -271,7 +267,7 @@ int orc_egm_solve(int64_t N, int64_t Na, double* pc, const double* a_grid, const
 
 static double labor_of(double c, double ws, double sigma, double phi, double theta) {
     double x = (ws * uprime(c, sigma)) / phi;
-    return (1.0 / theta == 1.0) ? x : pow(x, 1.0 / theta);
+    return (1.0 / theta == 1.0) ? x : aiy_pow(x, 1.0 / theta);
 }
 
 int orc_labor_egm_step(int64_t N, int64_t Na, const double* pc, const double* a_grid,
@@ -286,7 +282,7 @@ int orc_labor_egm_step(int64_t N, int64_t Na, const double* pc, const double* a_
     for (int64_t ja = 0; ja < N * Na; ++ja) {
         int64_t j = ja / Na, a = ja % Na;
         double ws = w * s[j];
-        cn[ja] = pow(RHS[ja], -1.0 / sigma);                        /* :82 */
+        cn[ja] = aiy_pow(RHS[ja], -1.0 / sigma);                    /* :82 */
         double ls = labor_of(cn[ja], ws, sigma, phi, theta);          /* :86 */
         ah[ja] = ((cn[ja] + a_grid[a]) - ws * ls) / (1 + r);          /* :87 */
     }

@@ -1,0 +1,46 @@
+"""GPU parity for A9 (Aiyagari_VFI.m:104-129): the Monte-Carlo capital-supply chain with
+MATLAB's fresh-session MT19937 stream, bit-exact against the golden path (numpy restatement)."""
+import numpy as np
+import pytest
+
+from oracle import corc
+from oracle import np_oracle as no
+
+pytestmark = pytest.mark.gpu
+
+
+def test_sim_matches_golden_path(pkg, gpu, golden):
+    g = golden("a11_ge_vfi_defaults")
+    a1 = golden("a1_vfi_defaults")
+    R = corc.vfi_solve(np.zeros((7, 400)), a1["a_grid"], a1["s"], a1["P"], 0.04,
+                       float(a1["w"]), 0.96, 5.0)
+    U = no.matlab_rand_stream(2 + 9999)[2:]
+    Ks, path, zp = pkg.sim_capital(R["policy_k"], a1["a_grid"], a1["P"], int(g["z1"]) + 1,
+                                   float(g["k1"]), U, return_path=True)
+    assert Ks == float(g["Ks0"])
+    assert np.array_equal(path, g["sim_k0"])
+    assert np.array_equal(zp - 1, g["sim_z0"])
+
+
+@pytest.mark.parametrize("Na", [400, 3000, 20000])
+def test_sim_offgrid_egm_layout(pkg, gpu, Na):
+    """Off-grid (EGM) policies in the Na x N layout, LDS and L2 paths, extrapolation at both
+    ends: bit-exact vs the C restatement."""
+    cal = no.calib_aiyagari(Na=Na, shocks="rouwenhorst")
+    a, P = cal["a_grid"], cal["P"]
+    rng = np.random.default_rng(Na)
+    pol = np.sort(rng.uniform(-1, a[-1] * 1.05, (Na, 7)), axis=0)  # off-grid, beyond the ends
+    U = rng.random(9999)
+    Ks, path, zp = pkg.sim_capital(pol, a, P, 3, a[Na // 2] + 0.123, U, vfi_layout=False,
+                                   return_path=True)
+    Ko, po = corc.sim_capital(pol.T, a, P, 2, a[Na // 2] + 0.123, U, return_path=True)
+    assert np.array_equal(path, po)
+    assert Ks == Ko
+
+
+def test_sim_find_empty_is_an_error(pkg, gpu):
+    P = np.array([[0.5, 0.4999], [0.5, 0.5]])  # row 1 sums below 1
+    with pytest.raises(pkg.AiyError) as e:
+        pkg.sim_capital(np.zeros((2, 3)), np.array([0.0, 1.0, 2.0]), P, 1, 0.0,
+                        np.array([0.99995]))
+    assert e.value.status == "AIY_FIND_EMPTY"
