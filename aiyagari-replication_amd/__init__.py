@@ -7,11 +7,12 @@ There is no CPU fallback: importing works without a GPU, calling a solver withou
 library or a device raises.
 """
 from . import calibration
+from .dist import dist_stationary, dist_update_dev
 from .egm import egm_solve, egm_step, egm_step_dev, labor_egm_solve, labor_egm_step
 from ._capi import AiyError, LIB_PATH, declared_symbols, lib
 from .sim import sim_capital, sim_capital_dev
 from .vfi import Workspace, labor_vfi_solve, labor_vfi_sweep, vfi_solve, vfi_sweep
 
-__all__ = ["egm_solve", "egm_step", "egm_step_dev", "labor_egm_solve", "labor_egm_step",
+__all__ = ["dist_stationary", "dist_update_dev", "egm_solve", "egm_step", "egm_step_dev", "labor_egm_solve", "labor_egm_step",
            "AiyError", "LIB_PATH", "Workspace", "calibration", "declared_symbols", "lib",
            "labor_vfi_solve", "sim_capital", "sim_capital_dev", "labor_vfi_sweep", "vfi_solve", "vfi_sweep"]

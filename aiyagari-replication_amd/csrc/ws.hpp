@@ -34,6 +34,12 @@ struct aiy_ws {
     unsigned long long* diff = nullptr;      // device [2*kDiffSlots] {max bits, any}
     unsigned long long* hitcount = nullptr;  // device [1]
     unsigned long long* hdiff = nullptr;     // pinned host [2*kDiffSlots + 4]
+    // histogram scratch (A10)
+    int* d_key = nullptr;
+    int* d_head = nullptr;
+    double* d_wr = nullptr;
+    double* d_mass = nullptr;
+    double* d_part = nullptr;
     // generic scratch used by the EGM / distribution / simulation kernels
     double* g0 = nullptr;
     double* g1 = nullptr;
@@ -47,7 +53,8 @@ struct aiy_ws {
     int64_t launches = 0;
 
     void free_all() {
-        void* ps[] = {EV, T, best0, idx0, dis, kf, partial, diff, hitcount, g0, g1, g2, gi};
+        void* ps[] = {EV, T, best0, idx0, dis, kf, partial, diff, hitcount, g0, g1, g2, gi,
+                      d_key, d_head, d_wr, d_mass, d_part};
         for (void* p : ps)
             if (p) (void)hipFree(p);
         if (hdiff) (void)hipHostFree(hdiff);
@@ -55,6 +62,7 @@ struct aiy_ws {
         kf_ok = false;
         idx0 = nullptr; partial = nullptr; diff = nullptr; hitcount = nullptr; hdiff = nullptr;
         g0 = g1 = g2 = nullptr; gi = nullptr;
+        d_key = d_head = nullptr; d_wr = d_mass = d_part = nullptr;
         partial_cap = 0;
     }
 };

@@ -104,6 +104,16 @@ int aiy_sim_capital(const double* policy_k, int vfi_layout, const double* a_grid
                     const double* P, int64_t N, int64_t Na, int64_t z1, double k1, int64_t T,
                     const double* uniforms, double* k_supply, double* sim_k, int32_t* sim_z);
 
+/* A10 (new; no reference code) — stationary distribution by histogram iteration.
+ * On-grid policy (policy_idx, 1-based; pass policy_k = NULL) or off-grid lottery between
+ * the bracketing nodes (policy_k; policy_idx = NULL).  All arrays in the script's layout:
+ * N x Na if vfi_layout, else Na x N.  lambda in/out (in = initial guess).  Iterates until
+ * max|Δλ| < tol or max_iter; returns K = Σ_ij λ(i,j)·a_j, iters, final max|Δλ|. */
+int aiy_dist_stationary(const int32_t* policy_idx, const double* policy_k, int vfi_layout,
+                        const double* a_grid, const double* P, int64_t N, int64_t Na,
+                        double tol, int64_t max_iter, double* lambda, double* k_supply,
+                        int64_t* iters, double* dist);
+
 /* ======================================================================================
  * Device tier: [N][Na] (z-major) arrays in HBM, async on `stream` (hipStream_t).
  * A workspace holds the per-shape scratch (EV/D tables, init/partial buffers, events).
@@ -155,6 +165,13 @@ int aiy_sim_capital_dev(aiy_ws* ws, const double* policy_rows, const double* a_g
                         const double* P, int64_t z1, double k1, int64_t T,
                         const double* uniforms, double* k_supply, double* sim_k,
                         int32_t* sim_z, int32_t* status, void* stream);
+/* A10 on device: one push λ → λ' ([N][Na]); policy_idx (0-based) or policy_k (lottery);
+ * diff (nullable, device [2]) = {max|λ'−λ| bits, any}.  Synchronises once to read the
+ * monotonicity flag (non-monotone policies take an exact ordered-scan fallback). */
+int aiy_dist_update_dev(aiy_ws* ws, const double* lambda, const int32_t* policy_idx,
+                        const double* policy_k, const double* a_grid, const double* P,
+                        double* lambda_out, double* diff, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

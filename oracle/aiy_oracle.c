@@ -398,6 +398,31 @@ int orc_dist_update_lottery(int64_t N, int64_t Na, const double* lam, const doub
     return 0;
 }
 
+int orc_dist_stationary(int64_t N, int64_t Na, const int32_t* idx, const double* kp,
+                        const double* a_grid, const double* P, double tol, int64_t max_iter,
+                        double* lam, double* K, int64_t* iters, double* dist) {
+    double* nxt = (double*)malloc(sizeof(double) * N * Na);
+    if (!nxt) return 1;
+    int64_t it;
+    double d = NAN;
+    for (it = 1; it <= max_iter; ++it) {
+        if (idx) orc_dist_update_ongrid(N, Na, lam, idx, P, nxt);
+        else orc_dist_update_lottery(N, Na, lam, kp, a_grid, P, nxt);
+        d = nanmax_absdiff(N * Na, nxt, lam);
+        memcpy(lam, nxt, sizeof(double) * N * Na);
+        if (d < tol) break;
+    }
+    if (it > max_iter) it = max_iter;
+    double acc = 0.0;
+    for (int64_t i = 0; i < N; ++i)
+        for (int64_t j = 0; j < Na; ++j) acc = acc + lam[i * Na + j] * a_grid[j];
+    *K = acc;
+    *iters = it;
+    *dist = d;
+    free(nxt);
+    return 0;
+}
+
 /* ------------------------------------------------------------------ A6 / A7 */
 static int sgn(double x) { return (x > 0) - (x < 0); }
 

@@ -83,6 +83,11 @@ int orc_dist_update_ongrid(int64_t N, int64_t Na, const double* lam, const int32
 int orc_dist_update_lottery(int64_t N, int64_t Na, const double* lam, const double* kp,
                             const double* a_grid, const double* P, double* lam_out);
 
+/* A10: iterate to max|Δλ| < tol; K = Σ λ(i,j)·a_j (sequential, i-major). */
+int orc_dist_stationary(int64_t N, int64_t Na, const int32_t* idx, const double* kp,
+                        const double* a_grid, const double* P, double tol, int64_t max_iter,
+                        double* lam, double* K, int64_t* iters, double* dist);
+
 /* A6/A7 Krusell-Smith (Krusell_Smith_VFI.m:148-192, bellman_value :329-364). */
 typedef struct {
     double beta, alpha, delta, k_min, k_max, ug, ub, l_bar, mu;

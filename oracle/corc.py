@@ -27,7 +27,8 @@ def lib():
         for name in ("orc_vfi_sweep", "orc_vfi_solve", "orc_labor_vfi_sweep", "orc_labor_vfi_solve",
                      "orc_egm_step", "orc_egm_solve", "orc_labor_egm_step", "orc_labor_egm_solve",
                      "orc_sim_capital", "orc_dist_update_ongrid", "orc_dist_update_lottery",
-                     "orc_ks_policy_improve", "orc_ks_howard", "orc_num_threads"):
+                     "orc_ks_policy_improve", "orc_ks_howard", "orc_num_threads",
+                     "orc_dist_stationary"):
             getattr(L, name).restype = C.c_int
         L.orc_ks_bellman.restype = _d
         L.orc_pchip_eval.restype = _d
@@ -186,6 +187,22 @@ def dist_update_lottery(lam, kp, a_grid, P):
     assert lib().orc_dist_update_lottery(_i64(N), _i64(Na), _p(lam), _p(kp), _p(a_grid), _p(P),
                                          _p(out)) == 0
     return out
+
+
+def dist_stationary(lam, a_grid, P, idx=None, kp=None, tol=1e-12, max_iter=10000):
+    lam = f64(lam).copy()
+    a_grid, P = f64(a_grid), f64(P)
+    N, Na = lam.shape
+    K, it, dist = _d(0), _i64(0), _d(0)
+    idx_p = _p(np.ascontiguousarray(idx, np.int32)) if idx is not None else None
+    if idx is not None:
+        idx_arr = np.ascontiguousarray(idx, np.int32); idx_p = _p(idx_arr)
+    kp_arr = f64(kp) if kp is not None else None
+    rc = lib().orc_dist_stationary(_i64(N), _i64(Na), idx_p, _p(kp_arr) if kp_arr is not None else None,
+                                   _p(a_grid), _p(P), _d(tol), _i64(max_iter), _p(lam), C.byref(K),
+                                   C.byref(it), C.byref(dist))
+    assert rc == 0
+    return lam, K.value, it.value, dist.value
 
 
 # ---------------------------------------------------------------- A6/A7

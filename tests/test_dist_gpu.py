@@ -1,0 +1,79 @@
+"""GPU parity for A10 (new component, no reference code; oracle = the C restatement of its
+definition, sequential scatter): the monotone-run gather reproduces the scatter bit for bit;
+non-monotone policies take the exact ordered-scan fallback."""
+import numpy as np
+import pytest
+
+from oracle import corc
+from oracle import np_oracle as no
+
+pytestmark = pytest.mark.gpu
+
+
+def _vfi_policy(Na, shocks="tauchen"):
+    cal = no.calib_aiyagari(Na=Na, shocks=shocks)
+    w = no.wage(0.04, 0.36, 0.08)
+    R = corc.vfi_solve(np.zeros((7, Na)), cal["a_grid"], cal["s"], cal["P"], 0.04, w, 0.96, 5.0)
+    return cal, R
+
+
+def test_one_push_matches_golden(pkg, gpu, golden):
+    g = golden("a10_dist_defaults")
+    a1 = golden("a1_vfi_defaults")
+    lam, K, it, dist = pkg.dist_stationary(a1["a_grid"], a1["P"], policy_idx=g["idx"] + 1,
+                                           lam0=g["lam0"], tol=0.0, max_iter=1)
+    assert it == 1 and np.array_equal(lam, g["lam1"])
+    lamL, _, _, _ = pkg.dist_stationary(a1["a_grid"], a1["P"], policy_k=g["kp_egm"],
+                                        lam0=g["lam0"], tol=0.0, max_iter=1)
+    assert np.array_equal(lamL, g["lam1_lottery"])
+
+
+@pytest.mark.parametrize("Na", [400, 4000])
+def test_stationary_ongrid_bitwise(pkg, gpu, Na):
+    cal, R = _vfi_policy(Na)
+    lam0 = np.full((7, Na), 1.0 / (7 * Na))
+    lam, K, it, dist = pkg.dist_stationary(cal["a_grid"], cal["P"], policy_idx=R["idx"] + 1,
+                                           lam0=lam0, tol=1e-13, max_iter=5000)
+    lo, Ko, ito, disto = corc.dist_stationary(lam0, cal["a_grid"], cal["P"], idx=R["idx"],
+                                              tol=1e-13, max_iter=5000)
+    assert it == ito
+    assert np.array_equal(lam, lo)
+    assert abs(K - Ko) <= 1e-12 * abs(Ko)       # K: fixed-order tree sum vs sequential sum
+    assert abs(lam.sum() - 1.0) < 1e-10
+
+
+def test_stationary_lottery_bitwise(pkg, gpu, golden):
+    g = golden("a4_egm_defaults")
+    kp = g["policy_k"].T  # [N][Na]
+    lam0 = np.full((7, 400), 1.0 / 2800)
+    lam, K, it, dist = pkg.dist_stationary(g["a_grid"], g["P"], policy_k=kp, lam0=lam0,
+                                           tol=1e-13, max_iter=5000)
+    lo, Ko, ito, _ = corc.dist_stationary(lam0, g["a_grid"], g["P"], kp=kp, tol=1e-13,
+                                          max_iter=5000)
+    assert it == ito and np.array_equal(lam, lo)
+    assert abs(K - Ko) <= 1e-12 * abs(Ko)
+
+
+def test_non_monotone_policy_fallback(pkg, gpu):
+    rng = np.random.default_rng(0)
+    Na = 300
+    cal = no.calib_aiyagari(Na=Na)
+    idx = rng.integers(0, Na, (7, Na)).astype(np.int32)  # arbitrary, non-monotone
+    lam0 = rng.random((7, Na)); lam0 /= lam0.sum()
+    lam, K, it, _ = pkg.dist_stationary(cal["a_grid"], cal["P"], policy_idx=idx + 1, lam0=lam0,
+                                        tol=0.0, max_iter=3)
+    lo, _, _, _ = corc.dist_stationary(lam0, cal["a_grid"], cal["P"], idx=idx, tol=0.0,
+                                       max_iter=3)
+    assert np.array_equal(lam, lo)
+    kp = rng.uniform(-1, cal["a_grid"][-1] + 1, (7, Na))
+    lam, _, _, _ = pkg.dist_stationary(cal["a_grid"], cal["P"], policy_k=kp, lam0=lam0, tol=0.0,
+                                       max_iter=2)
+    lo, _, _, _ = corc.dist_stationary(lam0, cal["a_grid"], cal["P"], kp=kp, tol=0.0, max_iter=2)
+    assert np.array_equal(lam, lo)
+
+
+def test_bad_index_rejected(pkg, gpu):
+    cal = no.calib_aiyagari(Na=50)
+    idx = np.ones((7, 50), np.int32); idx[2, 7] = 51
+    with pytest.raises(pkg.AiyError):
+        pkg.dist_stationary(cal["a_grid"], cal["P"], policy_idx=idx, tol=0.0, max_iter=1)
