@@ -145,7 +145,16 @@ __global__ void bell_init_kernel(BellArgs A) {
         // with a hint only its labour level is searched: one good candidate sets the bar
         if (A.hint && hk >= 0 && l != hl) continue;
         if (S > 0) {  // coarse scan of the feasible prefix (robust when the policy moved far)
-            for (int k = 0; k < kf; k += S) lexi_take(eval(l, k, coh), k, lb, lk);
+            int k = 0;
+            for (; k + 3 * S < kf; k += 4 * S) {  // 4 independent evaluations in flight
+                double v0 = eval(l, k, coh), v1 = eval(l, k + S, coh);
+                double v2 = eval(l, k + 2 * S, coh), v3 = eval(l, k + 3 * S, coh);
+                lexi_take(v0, k, lb, lk);
+                lexi_take(v1, k + S, lb, lk);
+                lexi_take(v2, k + 2 * S, lb, lk);
+                lexi_take(v3, k + 3 * S, lb, lk);
+            }
+            for (; k < kf; k += S) lexi_take(eval(l, k, coh), k, lb, lk);
             lexi_take(eval(l, kf - 1, coh), kf - 1, lb, lk);
         }
         if (A.hint && hk >= 0) {  // warm start: last sweep's argmax

@@ -11,7 +11,7 @@ struct aiy_ws {
     int64_t N = 0, Na = 0, Nl = 1;
     int dev = 0;
     // search knobs (aiy_ws_set_search)
-    int coarse = 128;
+    int coarse = 512;
     int CK = 1024;
     // VFI scratch
     double* EV = nullptr;
