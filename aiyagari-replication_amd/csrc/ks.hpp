@@ -1,0 +1,39 @@
+// Launch interface of the Krusell-Smith kernels (ks_kernels.hip, A6/A7).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+namespace aiy {
+struct KsSlice {   // per (K_i, s_i), computed on the host with libm (Krusell_Smith_VFI.m)
+    int kp_idx;    // nearest K_grid index of the ALM forecast K' (:335-343)
+    double a1;     // r_val + 1 - delta at the flipped current z (:332, :353-355)
+    double a2;     // w_val * (eps * l_bar)
+    double b1;     // r_table + 1 - delta (correct z, :152)
+    double b2;     // w_table * (eps*l_bar + (1-eps)*mu) (:153)
+};
+struct KsArgs {
+    int nk, nK;
+    int node0, n_local;  // node range handled by this launch (sharding)
+    const double* k_grid;
+    const double* P;     // 4 x 4 row-major
+    const KsSlice* slice;  // [s][K]
+    double beta, k_min, k_max, tol;
+    int howard, max_vfi;
+};
+struct KsOut {
+    int iters;
+    double rel;
+};
+bool ks_fused_fits(int nk, int nK);
+int launch_ks_fused(const KsArgs& A, double* V, double* kopt, int* nfev, KsOut* out,
+                    hipStream_t st);
+int launch_ks_slopes(const KsArgs& A, const double* V, double* dV, hipStream_t st);
+int launch_ks_slopes_cols(const KsArgs& A, const int* cols, int ncols, const double* V,
+                          double* dV, hipStream_t st);
+int launch_ks_improve(const KsArgs& A, const double* V, const double* dV, double* kopt,
+                      int* nfev, hipStream_t st);
+int launch_ks_howard(const KsArgs& A, const double* V, const double* dV, const double* kopt,
+                     double* Vn, hipStream_t st);
+int launch_ks_reldiff(const KsArgs& A, const double* V, const double* Vold,
+                      unsigned long long* slots, hipStream_t st);
+}  // namespace aiy

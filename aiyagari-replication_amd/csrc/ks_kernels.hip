@@ -1,0 +1,408 @@
+// A6/A7 — Krusell-Smith VFI on gfx950 (Krusell_Smith_VFI.m:143-204; bellman_value :329-364).
+//
+// Node = (k_i, K_i, s_i); value/k_opt are k x K x S column-major (node n = (s*K + Ki)*nk + ki).
+// Everything that depends only on the slice (K_i, s_i) — the ALM forecast K' and its nearest
+// grid index, the prices r, w at the (flipped, :332) current z, the budget coefficients — is
+// computed on the host (libm) once per B and passed as a KsSlice table.  Per node:
+//   bellman(kp) = log(max((a1·k + a2) − kp, 1e-10)) + β Σ_s' P(s,s')·pchip_{K',s'}(clamp(kp))
+// with pchip slopes (Fritsch–Butland, MATLAB end rules) rebuilt from the current value after
+// every Howard sweep (the .Values refresh at :186-191) and evaluated in MATLAB's pwch/ppval form.
+//   improve  fminbnd(−bellman, k_min, min(res, k_max)) per node — MATLAB's Brent/FMM with
+//            seps = sqrt(eps), TolX = 1e-4, MaxFunEvals = MaxIter = 500 (:157-167)
+//   howard   Jacobi: value_new(n) = bellman_n(k_opt(n)) from the previous sweep's value
+// log is aiy_log (fdlibm, identical on host and device), so fminbnd's value-dependent branches
+// take the same path as in the C oracle: k_opt and value are bit-exact.
+//
+// Two execution shapes:
+//   fused    one workgroup holds the whole problem in LDS (reference size: 1,600 nodes) and runs
+//            the complete VFI loop — improvement every 5th iteration, H Howard sweeps, the
+//            relative-difference stop (:195-203) — in ONE launch (barriers between phases).
+//   tiled    slopes / improve / howard / reldiff as separate grid-wide kernels (any size).
+#include "aiy_common.hpp"
+#include "ks.hpp"
+
+namespace aiy {
+
+__device__ __forceinline__ int sgn_dev(double x) { return (x > 0) - (x < 0); }
+
+// pchip slope at point q of a column (x = k_grid), MATLAB pchipslopes
+__device__ double pchip_slope(const double* __restrict__ x, const double* __restrict__ y, int n,
+                              int q) {
+    if (q == 0 || q == n - 1) {
+        double h0, h1, e0, e1;
+        if (q == 0) {
+            h0 = x[1] - x[0];
+            h1 = x[2] - x[1];
+            e0 = (y[1] - y[0]) / h0;
+            e1 = (y[2] - y[1]) / h1;
+        } else {
+            h0 = x[n - 1] - x[n - 2];
+            h1 = x[n - 2] - x[n - 3];
+            e0 = (y[n - 1] - y[n - 2]) / h0;
+            e1 = (y[n - 2] - y[n - 3]) / h1;
+        }
+        double d = ((2 * h0 + h1) * e0 - h0 * e1) / (h0 + h1);
+        if (sgn_dev(d) != sgn_dev(e0)) d = 0.0;
+        else if (sgn_dev(e0) != sgn_dev(e1) && fabs(d) > fabs(3 * e0)) d = 3 * e0;
+        return d;
+    }
+    int k = q - 1;
+    double h1 = x[k + 1] - x[k], h2 = x[k + 2] - x[k + 1];
+    double d1 = (y[k + 1] - y[k]) / h1, d2 = (y[k + 2] - y[k + 1]) / h2;
+    if (sgn_dev(d1) * sgn_dev(d2) > 0) {
+        double hs = h1 + h2;
+        double w1 = (h1 + hs) / (3 * hs);
+        double w2 = (hs + h2) / (3 * hs);
+        double dmax = fmax(fabs(d1), fabs(d2));
+        double dmin = fmin(fabs(d1), fabs(d2));
+        return dmin / (w1 * (d1 / dmax) + w2 * (d2 / dmax));
+    }
+    return 0.0;
+}
+
+// pwch coefficients + ppval Horner on segment i
+__device__ __forceinline__ double pchip_at(const double* __restrict__ x,
+                                           const double* __restrict__ y,
+                                           const double* __restrict__ d, int i, double xq) {
+    double h = x[i + 1] - x[i];
+    double dl = (y[i + 1] - y[i]) / h;
+    double dzzdx = (dl - d[i]) / h;
+    double dzdxdx = (d[i + 1] - dl) / h;
+    double c3 = (dzdxdx - dzzdx) / h;
+    double c2 = 2 * dzzdx - dzdxdx;
+    double sx = xq - x[i];
+    double v = c3;
+    v = sx * v + c2;
+    v = sx * v + d[i];
+    v = sx * v + y[i];
+    return v;
+}
+
+struct KsView {  // where the value/slope columns and the grid live (LDS or global)
+    const double* kg;
+    const double* V;
+    const double* dV;
+};
+
+__device__ __forceinline__ double ks_bellman_dev(const KsArgs& A, const KsView& W,
+                                                 const KsSlice& sl, int si, double k, double kp) {
+    const int nk = A.nk;
+    double kq = fmax(fmin(kp, W.kg[nk - 1]), W.kg[0]);
+    int seg = seg_of_dev(W.kg, nk, kq);
+    double expec = 0;
+#pragma unroll
+    for (int sn = 0; sn < 4; ++sn) {
+        size_t col = ((size_t)sn * A.nK + sl.kp_idx) * nk;
+        expec = expec + A.P[si * 4 + sn] * pchip_at(W.kg, W.V + col, W.dV + col, seg, kq);
+    }
+    double c = (sl.a1 * k + sl.a2) - kp;
+    c = fmax(c, 1e-10);
+    return aiy_log(c) + A.beta * expec;
+}
+
+// MATLAB fminbnd on −bellman over [ax, bx]
+__device__ double ks_fminbnd_dev(const KsArgs& A, const KsView& W, const KsSlice& sl, int si,
+                                 double k, double ax, double bx, int* nfev) {
+#define F(X) (-ks_bellman_dev(A, W, sl, si, k, (X)))
+    const double seps = 1.4901161193847656e-08;  // sqrt(eps)
+    const double tolx = 1e-4;
+    const double cg = 0.5 * (3.0 - 2.23606797749978969641);  // 0.5*(3 - sqrt(5))
+    double a = ax, b = bx, v = a + cg * (b - a), w = v, xf = v, d = 0, e = 0, x = xf;
+    double fx = F(x);
+    int num = 1, it = 0;
+    double fv = fx, fw = fx, xm = 0.5 * (a + b);
+    double tol1 = seps * fabs(xf) + tolx / 3.0, tol2 = 2.0 * tol1;
+    while (fabs(xf - xm) > (tol2 - 0.5 * (b - a))) {
+        int gs = 1;
+        if (fabs(e) > tol1) {
+            gs = 0;
+            double r = (xf - w) * (fx - fv);
+            double q = (xf - v) * (fx - fw);
+            double pp = (xf - v) * q - (xf - w) * r;
+            q = 2.0 * (q - r);
+            if (q > 0.0) pp = -pp;
+            q = fabs(q);
+            r = e;
+            e = d;
+            if (fabs(pp) < fabs(0.5 * q * r) && pp > q * (a - xf) && pp < q * (b - xf)) {
+                d = pp / q;
+                x = xf + d;
+                if ((x - a) < tol2 || (b - x) < tol2) {
+                    double si2 = sgn_dev(xm - xf) + ((xm - xf) == 0);
+                    d = tol1 * si2;
+                }
+            } else {
+                gs = 1;
+            }
+        }
+        if (gs) {
+            e = (xf >= xm) ? (a - xf) : (b - xf);
+            d = cg * e;
+        }
+        double si2 = sgn_dev(d) + (d == 0);
+        x = xf + si2 * fmax(fabs(d), tol1);
+        double fu = F(x);
+        ++num;
+        ++it;
+        if (fu <= fx) {
+            if (x >= xf) a = xf;
+            else b = xf;
+            v = w; fv = fw;
+            w = xf; fw = fx;
+            xf = x; fx = fu;
+        } else {
+            if (x < xf) a = x;
+            else b = x;
+            if (fu <= fw || w == xf) {
+                v = w; fv = fw;
+                w = x; fw = fu;
+            } else if (fu <= fv || v == xf || v == w) {
+                v = x; fv = fu;
+            }
+        }
+        xm = 0.5 * (a + b);
+        tol1 = seps * fabs(xf) + tolx / 3.0;
+        tol2 = 2.0 * tol1;
+        if (num >= 500 || it >= 500) break;
+    }
+    *nfev = num;
+    return xf;
+#undef F
+}
+
+__device__ __forceinline__ void node_coords(const KsArgs& A, int n, int& ki, int& Ki, int& si) {
+    ki = n % A.nk;
+    int r = n / A.nk;
+    Ki = r % A.nK;
+    si = r / A.nK;
+}
+
+__device__ __forceinline__ double improve_node(const KsArgs& A, const KsView& W, int n,
+                                               int* nfev) {
+    int ki, Ki, si;
+    node_coords(A, n, ki, Ki, si);
+    const KsSlice sl = A.slice[si * A.nK + Ki];
+    double k = W.kg[ki];
+    double res = sl.b1 * k + sl.b2;                 // :152-153
+    double kpmax = fmin(res, A.k_max);              // :159
+    return ks_fminbnd_dev(A, W, sl, si, k, A.k_min, kpmax, nfev);  // :164
+}
+
+__device__ __forceinline__ double howard_node(const KsArgs& A, const KsView& W, int n,
+                                              double kp) {
+    int ki, Ki, si;
+    node_coords(A, n, ki, Ki, si);
+    const KsSlice sl = A.slice[si * A.nK + Ki];
+    return ks_bellman_dev(A, W, sl, si, W.kg[ki], kp);
+}
+
+// ------------------------------------------------------------------------------ tiled
+__global__ void ks_slopes_kernel(KsArgs A, const double* __restrict__ V, double* __restrict__ dV) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    int n = A.nk * A.nK * 4;
+    if (t >= n) return;
+    int q = t % A.nk;
+    size_t col = (size_t)(t / A.nk) * A.nk;
+    dV[t] = pchip_slope(A.k_grid, V + col, A.nk, q);
+}
+
+// slopes for a list of columns only (the columns a shard reads)
+__global__ void ks_slopes_cols_kernel(KsArgs A, const int* __restrict__ cols, int ncols,
+                                      const double* __restrict__ V, double* __restrict__ dV) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ncols * A.nk) return;
+    int q = t % A.nk;
+    size_t col = (size_t)cols[t / A.nk] * A.nk;
+    dV[col + q] = pchip_slope(A.k_grid, V + col, A.nk, q);
+}
+
+__global__ void ks_improve_kernel(KsArgs A, const double* __restrict__ V,
+                                  const double* __restrict__ dV, double* __restrict__ k_opt,
+                                  int* __restrict__ nfev) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= A.n_local) return;
+    int n = A.node0 + t;
+    KsView W{A.k_grid, V, dV};
+    int nf = 0;
+    k_opt[n] = improve_node(A, W, n, &nf);
+    if (nfev) nfev[n] = nf;
+}
+
+__global__ void ks_howard_kernel(KsArgs A, const double* __restrict__ V,
+                                 const double* __restrict__ dV, const double* __restrict__ k_opt,
+                                 double* __restrict__ Vn) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= A.n_local) return;
+    int n = A.node0 + t;
+    KsView W{A.k_grid, V, dV};
+    Vn[n] = howard_node(A, W, n, k_opt[n]);
+}
+
+// max |v - v_old| / (|v_old| + 1e-10) ignoring NaN (:195)
+__global__ void ks_reldiff_kernel(KsArgs A, const double* __restrict__ V,
+                                  const double* __restrict__ Vold,
+                                  unsigned long long* __restrict__ slots) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    bool ok = false;
+    double d = 0;
+    if (t < A.n_local) {
+        int n = A.node0 + t;
+        d = fabs(V[n] - Vold[n]) / (fabs(Vold[n]) + 1e-10);
+        ok = d == d;
+    }
+    block_max_to_slots(ok, d, slots);
+}
+
+// ------------------------------------------------------------------------------ fused
+// One workgroup, everything in LDS: kg | V | dV | Vn ; k_opt and v_old stay in registers.
+constexpr int kFusedThreads = 1024;
+constexpr int kFusedMaxPerThread = 4;  // nodes per thread
+
+__global__ __launch_bounds__(kFusedThreads) void ks_fused_vfi_kernel(KsArgs A, double* V_io,
+                                                                     double* kopt_io,
+                                                                     int* nfev_io, KsOut* out) {
+    extern __shared__ double lds[];
+    const int nk = A.nk, n_all = A.nk * A.nK * 4;
+    double* kg = lds;
+    double* V = kg + nk;
+    double* dV = V + n_all;
+    double* Vn = dV + n_all;
+    __shared__ double s_red[kFusedThreads / 64];
+    __shared__ int s_flag;
+    const int tid = threadIdx.x;
+    for (int q = tid; q < nk; q += blockDim.x) kg[q] = A.k_grid[q];
+    for (int q = tid; q < n_all; q += blockDim.x) V[q] = V_io[q];
+    double kopt[kFusedMaxPerThread], vold[kFusedMaxPerThread];
+#pragma unroll
+    for (int r = 0; r < kFusedMaxPerThread; ++r) {
+        int n = tid + r * kFusedThreads;
+        kopt[r] = n < n_all ? kopt_io[n] : 0.0;
+        vold[r] = 0.0;
+    }
+    __syncthreads();
+    auto slopes = [&]() {
+        for (int q = tid; q < n_all; q += blockDim.x)
+            dV[q] = pchip_slope(kg, V + (q / nk) * nk, nk, q % nk);
+        __syncthreads();
+    };
+    int it = 0;
+    double rel = __builtin_nan("");
+    for (it = 1; it <= A.max_vfi; ++it) {
+#pragma unroll
+        for (int r = 0; r < kFusedMaxPerThread; ++r) {
+            int n = tid + r * kFusedThreads;
+            if (n < n_all) vold[r] = V[n];  // value_old = value (:145)
+        }
+        KsView W{kg, V, dV};
+        if ((it - 1) % 5 == 0) {  // policy improvement (:148-168)
+            slopes();
+#pragma unroll
+            for (int r = 0; r < kFusedMaxPerThread; ++r) {
+                int n = tid + r * kFusedThreads;
+                if (n < n_all) {
+                    int nf = 0;
+                    kopt[r] = improve_node(A, W, n, &nf);
+                    if (nfev_io) nfev_io[n] = nf;
+                }
+            }
+            __syncthreads();
+        }
+        for (int h = 0; h < A.howard; ++h) {  // Jacobi Howard sweeps (:172-192)
+            slopes();
+            KsView Wh{kg, V, dV};
+#pragma unroll
+            for (int r = 0; r < kFusedMaxPerThread; ++r) {
+                int n = tid + r * kFusedThreads;
+                if (n < n_all) Vn[n] = howard_node(A, Wh, n, kopt[r]);
+            }
+            __syncthreads();
+            for (int q = tid; q < n_all; q += blockDim.x) V[q] = Vn[q];
+            __syncthreads();
+        }
+        // relative difference, NaN ignored (:195)
+        double m = -1.0;
+#pragma unroll
+        for (int r = 0; r < kFusedMaxPerThread; ++r) {
+            int n = tid + r * kFusedThreads;
+            if (n < n_all) {
+                double d = fabs(V[n] - vold[r]) / (fabs(vold[r]) + 1e-10);
+                if (d == d) m = fmax(m, d);
+            }
+        }
+        for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off));
+        if ((tid & 63) == 0) s_red[tid >> 6] = m;
+        __syncthreads();
+        if (tid == 0) {
+            double mm = -1.0;
+            for (int q = 0; q < kFusedThreads / 64; ++q) mm = fmax(mm, s_red[q]);
+            rel = mm < 0 ? __builtin_nan("") : mm;
+            s_flag = (rel < A.tol) ? 1 : 0;
+            s_red[0] = rel;
+        }
+        __syncthreads();
+        rel = s_red[0];
+        if (s_flag) break;
+        __syncthreads();
+    }
+    if (it > A.max_vfi) it = A.max_vfi;
+    for (int q = tid; q < n_all; q += blockDim.x) V_io[q] = V[q];
+#pragma unroll
+    for (int r = 0; r < kFusedMaxPerThread; ++r) {
+        int n = tid + r * kFusedThreads;
+        if (n < n_all) kopt_io[n] = kopt[r];
+    }
+    if (tid == 0) {
+        out->iters = it;
+        out->rel = rel;
+    }
+}
+
+// ------------------------------------------------------------------------------ launchers
+static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+size_t ks_fused_lds_bytes(int nk, int nK) { return sizeof(double) * ((size_t)nk + 3ull * nk * nK * 4); }
+bool ks_fused_fits(int nk, int nK) {
+    return (long long)nk * nK * 4 <= (long long)kFusedThreads * kFusedMaxPerThread &&
+           ks_fused_lds_bytes(nk, nK) <= 150 * 1024;
+}
+
+int launch_ks_fused(const KsArgs& A, double* V, double* kopt, int* nfev, KsOut* out,
+                    hipStream_t st) {
+    ks_fused_vfi_kernel<<<1, kFusedThreads, ks_fused_lds_bytes(A.nk, A.nK), st>>>(A, V, kopt,
+                                                                                  nfev, out);
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
+}
+int launch_ks_slopes(const KsArgs& A, const double* V, double* dV, hipStream_t st) {
+    int n = A.nk * A.nK * 4;
+    ks_slopes_kernel<<<cdiv(n, 256), 256, 0, st>>>(A, V, dV);
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
+}
+int launch_ks_slopes_cols(const KsArgs& A, const int* cols, int ncols, const double* V,
+                          double* dV, hipStream_t st) {
+    if (ncols <= 0) return AIY_OK;
+    ks_slopes_cols_kernel<<<cdiv((long long)ncols * A.nk, 256), 256, 0, st>>>(A, cols, ncols, V, dV);
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
+}
+int launch_ks_improve(const KsArgs& A, const double* V, const double* dV, double* kopt,
+                      int* nfev, hipStream_t st) {
+    ks_improve_kernel<<<cdiv(A.n_local, 128), 128, 0, st>>>(A, V, dV, kopt, nfev);
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
+}
+int launch_ks_howard(const KsArgs& A, const double* V, const double* dV, const double* kopt,
+                     double* Vn, hipStream_t st) {
+    ks_howard_kernel<<<cdiv(A.n_local, 256), 256, 0, st>>>(A, V, dV, kopt, Vn);
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
+}
+int launch_ks_reldiff(const KsArgs& A, const double* V, const double* Vold,
+                      unsigned long long* slots, hipStream_t st) {
+    ks_reldiff_kernel<<<cdiv(A.n_local, 256), 256, 0, st>>>(A, V, Vold, slots);
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
+}
+
+}  // namespace aiy

@@ -114,6 +114,29 @@ int aiy_dist_stationary(const int32_t* policy_idx, const double* policy_k, int v
                         double tol, int64_t max_iter, double* lambda, double* k_supply,
                         int64_t* iters, double* dist);
 
+/* A6 — replaces Krusell_Smith_VFI.m:149-168 (policy improvement with fminbnd).
+ * value, k_opt: k x K x S column-major (S = 4); B 4; P 4 x 4; params = 13 doubles {beta, alpha,
+ * delta, k_min, k_max, ug, ub, l_bar, mu, z_grid(1), z_grid(2), eps_grid(1), eps_grid(2)}.  nfev (nullable,
+ * k x K x S) = fminbnd function evaluations per node. */
+int ks_policy_improve(const double* value, const double* k_grid, const double* K_grid,
+                      const double* B, const double* P, const double* params, int64_t nk,
+                      int64_t nK, double* k_opt, int32_t* nfev);
+/* A7 — replaces Krusell_Smith_VFI.m:172-192 (`steps` Jacobi Howard sweeps). value in/out. */
+int ks_howard(double* value, const double* k_opt, const double* k_grid, const double* K_grid,
+              const double* B, const double* P, const double* params, int64_t nk, int64_t nK,
+              int64_t steps);
+/* A6+A7 — replaces the VFI loop Krusell_Smith_VFI.m:143-204 for one ALM coefficient B:
+ * improvement every 5th iteration, `howard_steps` sweeps, relative-diff stop (:195-203).
+ * n_devices > 1 shards the K range (all four s) over n_devices shards on devices
+ * (shard % visible devices) in one process; after every Howard sweep each shard refreshes
+ * only the value columns (K'_idx, s') its slices read, by peer copies over xGMI.  Results
+ * equal the single-device solve bit for bit.  k_opt is in/out (used until the first
+ * improvement).  iters = VFI iterations run, rel_diff = last max relative change. */
+int ks_vfi_solve(double* value, double* k_opt, const double* k_grid, const double* K_grid,
+                 const double* B, const double* P, const double* params, int64_t nk,
+                 int64_t nK, int64_t howard_steps, double tol, int64_t max_vfi,
+                 int n_devices, int64_t* iters, double* rel_diff);
+
 /* ======================================================================================
  * Device tier: [N][Na] (z-major) arrays in HBM, async on `stream` (hipStream_t).
  * A workspace holds the per-shape scratch (EV/D tables, init/partial buffers, events).

@@ -245,3 +245,21 @@ def ks_howard(p, k_grid, K_grid, V, k_opt, B, P, steps):
                              _i64(steps))
     assert rc == 0
     return V
+
+
+def ks_vfi_solve(p, k_grid, K_grid, V, k_opt, B, P, howard=50, tol=1e-6, max_vfi=10000):
+    """Krusell_Smith_VFI.m:143-204 with the C pieces (improve every 5th iteration)."""
+    V = np.array(V, dtype=np.float64, order="F", copy=True)
+    k_opt = np.array(k_opt, dtype=np.float64, order="F", copy=True)
+    rel = float("nan")
+    it = 0
+    for it in range(1, max_vfi + 1):
+        V_old = V.copy(order="F")
+        if (it - 1) % 5 == 0:
+            k_opt, _ = ks_policy_improve(p, k_grid, K_grid, V, B, P)
+        V = ks_howard(p, k_grid, K_grid, V, k_opt, B, P, howard)
+        d = np.abs(V - V_old) / (np.abs(V_old) + 1e-10)
+        rel = float(np.nanmax(d)) if not np.all(np.isnan(d)) else float("nan")
+        if rel < tol:
+            break
+    return dict(value=V, k_opt=k_opt, iters=it, rel_diff=rel)

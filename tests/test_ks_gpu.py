@@ -1,0 +1,64 @@
+"""GPU parity for A6/A7 (Krusell_Smith_VFI.m:143-204): MATLAB-fminbnd policy improvement and
+Jacobi Howard sweeps with pchip refresh.  log is the shared fdlibm aiy_log, so fminbnd's
+value-dependent branches match the C oracle and results are bit-exact."""
+import numpy as np
+import pytest
+
+from oracle import corc
+from oracle import np_oracle as no
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(golden):
+    g = golden("ks_defaults")
+    prm = np.array([g["beta"], g["alpha"], g["delta"], g["k_min"], g["k_max"], g["ug"], g["ub"],
+                    g["l_bar"], g["mu"], 1.01, 0.99, 1.0, 0.0])
+    return g, prm
+
+
+def test_improve_and_howard_match_golden(pkg, gpu, golden):
+    g, prm = _setup(golden)
+    ko, nf = pkg.ks_policy_improve(g["V0"], g["k_grid"], g["K_grid"], g["B"], g["P"], prm)
+    assert np.array_equal(ko, g["k_opt"]) and np.array_equal(nf, g["nfev"])
+    V2 = pkg.ks_howard(g["V0"], ko, g["k_grid"], g["K_grid"], g["B"], g["P"], prm, steps=2)
+    assert np.array_equal(V2, g["V_howard2"])
+
+
+def _ks_oracle_params(prm):
+    return corc.ks_params(beta=prm[0], alpha=prm[1], delta=prm[2], k_min=prm[3], k_max=prm[4],
+                          ug=prm[5], ub=prm[6], l_bar=prm[7], mu=prm[8], z_grid=(prm[9], prm[10]),
+                          eps_grid=(prm[11], prm[12]))
+
+
+def test_fused_vfi_matches_oracle(pkg, gpu, golden):
+    """The single-workgroup LDS-resident loop (whole VFI in one launch) vs the C pieces, with
+    a non-identity ALM so K'_idx differs from K."""
+    g, prm = _setup(golden)
+    B = np.array([0.1, 0.97, 0.08, 0.975])
+    R = pkg.ks_vfi_solve(g["V0"], g["V0"] * 0 + 1.0, g["k_grid"], g["K_grid"], B, g["P"], prm,
+                         howard_steps=10, tol=1e-6, max_vfi=12)
+    Ro = corc.ks_vfi_solve(_ks_oracle_params(prm), g["k_grid"], g["K_grid"], g["V0"],
+                           g["V0"] * 0 + 1.0, B, g["P"], howard=10, tol=1e-6, max_vfi=12)
+    assert R["iters"] == Ro["iters"]
+    assert np.array_equal(R["value"], Ro["value"])
+    assert np.array_equal(R["k_opt"], Ro["k_opt"])
+    assert R["rel_diff"] == Ro["rel_diff"]
+
+
+@pytest.mark.parametrize("shards", [1, 3, 4])
+def test_tiled_and_sharded_match_fused(pkg, gpu, shards):
+    """A grid too large for one workgroup (tiled kernels) and the same problem sharded over
+    K-ranges (peer/local copies of the needed columns): identical results."""
+    p, kg, Kg, P, _, _ = no.ks_setup(k_size=300, K_size=12)
+    prm = pkg.ks_params()
+    V0 = np.log(0.1 / 0.9 * 0.9 * np.repeat(np.repeat(kg[:, None, None], 12, 1), 4, 2)) / (1 - 0.99)
+    B = np.array([0.05, 0.985, 0.04, 0.99])
+    k0 = 0.9 * np.repeat(np.repeat(kg[:, None, None], 12, 1), 4, 2)
+    R = pkg.ks_vfi_solve(V0, k0, kg, Kg, B, P, prm, howard_steps=6, tol=1e-8, max_vfi=11,
+                         n_devices=shards)
+    Ro = corc.ks_vfi_solve(_ks_oracle_params(prm), kg, Kg, V0, k0, B, P, howard=6, tol=1e-8,
+                           max_vfi=11)
+    assert R["iters"] == Ro["iters"]
+    assert np.array_equal(R["value"], Ro["value"])
+    assert np.array_equal(R["k_opt"], Ro["k_opt"])
