@@ -44,9 +44,9 @@ def test_labor_nonuniform_levels_and_sigma(pkg, gpu):
                              1e-5, 8)["v_new"]
     v, pk, pl, pc, lin = pkg.labor_vfi_sweep(V, a, s, P, L, 0.03, w, 0.96, 3.0, 1.0, 1.5)
     vo, (pko, plo, pco, lino) = corc.labor_vfi_sweep(V, a, s, P, L, 0.03, w, 0.96, 3.0, 1.0, 1.5)
-    # eta = 1.5 → L^(2.5) via pow on both sides (device vs glibc: ulp level)
-    assert np.max(np.abs(v - vo)) < 1e-10
-    assert (lin - 1 == lino).mean() > 0.999
+    # eta = 1.5 → L^(2.5) through the shared aiy_pow: bit-exact
+    assert np.array_equal(v, vo) and np.array_equal(lin - 1, lino)
+    assert np.array_equal(pk, pko) and np.array_equal(pl, plo) and np.array_equal(pc, pco)
 
 
 def test_labor_infeasible_state_keeps_incoming(pkg, gpu):
