@@ -19,7 +19,8 @@ step() {  # name, seconds, command...
 echo "host: $(nproc) cpus, OMP_NUM_THREADS=$OMP_NUM_THREADS"; rocm-smi --showproductname 2>/dev/null | grep -i -m2 "card\|gfx" || true
 for s in ${STEPS:-tests smoke bench prof}; do
   case $s in
-    tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS} ;;
+    tests) if [ -n "$PYTEST_K" ]; then step pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -k "$PYTEST_K";
+           else step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread; fi ;;
     smoke) step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python -u bench.py ${BENCH_ARGS} ;;
     prof)  step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/prof" -o run -- python3 "$PWD/bench.py" --no-cpu-baseline ${BENCH_ARGS} ;;
