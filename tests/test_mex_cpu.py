@@ -1,0 +1,58 @@
+"""CPU: the MEX/mkoctfile gateways (compiled against the stub mx API) validate their arguments
+the way a MATLAB caller sees it — errors come back as mexErrMsgIdAndTxt identifiers — and report
+the library status when no device is present."""
+import numpy as np
+import pytest
+
+from tests import mexstub
+from oracle import np_oracle as no
+
+
+@pytest.fixture(scope="module")
+def cal():
+    if not mexstub.LIB.exists():
+        pytest.skip("libmexstub.so not built")
+    return no.calib_aiyagari(Na=20)
+
+
+def test_usage_error(cal):
+    with pytest.raises(mexstub.MexError) as e:
+        mexstub.call("aiy_vfi_sweep_mex", 3, np.zeros((7, 20)))
+    assert e.value.id == "aiy:usage"
+
+
+def test_shape_errors(cal):
+    with pytest.raises(mexstub.MexError) as e:  # P not N x N
+        mexstub.call("aiy_vfi_sweep_mex", 3, np.zeros((7, 20)), cal["a_grid"], cal["s"],
+                     np.eye(6), 0.04, 1.0, 0.96, 5.0)
+    assert e.value.id == "aiy:shape"
+    with pytest.raises(mexstub.MexError) as e:  # a_grid length != size(v_old, 2)
+        mexstub.call("aiy_vfi_sweep_mex", 3, np.zeros((7, 20)), cal["a_grid"][:-1], cal["s"],
+                     cal["P"], 0.04, 1.0, 0.96, 5.0)
+    assert e.value.id == "aiy:shape"
+    with pytest.raises(mexstub.MexError) as e:  # scalar expected
+        mexstub.call("aiy_vfi_sweep_mex", 3, np.zeros((7, 20)), cal["a_grid"], cal["s"],
+                     cal["P"], np.array([0.04, 0.05]), 1.0, 0.96, 5.0)
+    assert e.value.id == "aiy:type"
+
+
+def test_library_status_surfaces_as_mex_error(cal):
+    import torch
+    a = cal["a_grid"][::-1].copy()  # unsorted grid: rejected by the library before any device work
+    with pytest.raises(mexstub.MexError) as e:
+        mexstub.call("aiy_vfi_sweep_mex", 3, np.zeros((7, 20)), a, cal["s"], cal["P"], 0.04,
+                     1.0, 0.96, 5.0)
+    assert e.value.id == "aiy:BAD_ARG"
+    if not torch.cuda.is_available():
+        with pytest.raises(mexstub.MexError) as e:
+            mexstub.call("aiy_vfi_sweep_mex", 3, np.zeros((7, 20)), cal["a_grid"], cal["s"],
+                         cal["P"], 0.04, 1.0, 0.96, 5.0)
+        assert e.value.id == "aiy:NO_DEVICE"
+
+
+def test_ks_shape_check(cal):
+    with pytest.raises(mexstub.MexError) as e:
+        mexstub.call("ks_vfi_solve_mex", 2, np.zeros((10, 4, 4)), np.zeros((10, 4, 4)),
+                     np.linspace(0, 1, 11), np.linspace(30, 50, 4), np.array([0, 1, 0, 1.0]),
+                     np.eye(4), np.zeros(13), 50.0, 1e-6, 10.0, 1.0)
+    assert e.value.id == "aiy:shape"

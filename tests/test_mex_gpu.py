@@ -1,0 +1,65 @@
+"""GPU: the MEX gateways end to end (stub mx API → C ABI → HIP), against the Python host
+mirror and the C oracle: same numbers through the MATLAB-facing boundary."""
+import numpy as np
+import pytest
+
+from tests import mexstub
+from oracle import corc
+from oracle import np_oracle as no
+
+pytestmark = pytest.mark.gpu
+
+
+def test_vfi_solve_gateway(pkg, gpu, golden):
+    g = golden("a1_vfi_defaults")
+    v_new, v_old, pk, pc, it = mexstub.call("aiy_vfi_solve_mex", 5, np.zeros((7, 400)),
+                                            g["a_grid"], g["s"], g["P"], float(g["r"]),
+                                            float(g["w"]), 0.96, 5.0, 1e-5, 1000.0)
+    assert int(it[0, 0]) == 249
+    assert np.array_equal(v_new, g["solve_v_new"]) and np.array_equal(v_old, g["solve_v_old"])
+    v2, pk2, pc2, idx = mexstub.call("aiy_vfi_sweep_mex", 4, g["v20"], g["a_grid"], g["s"], g["P"],
+                                     float(g["r"]), float(g["w"]), 0.96, 5.0)
+    assert np.array_equal(v2, g["v21"]) and np.array_equal(idx - 1, g["idx21"])
+
+
+def test_egm_and_sim_gateways(pkg, gpu, golden):
+    g = golden("a4_egm_defaults")
+    pc, pk, dist, it = mexstub.call("aiy_egm_solve_mex", 4, g["policy_c0"], g["a_grid"], g["s"],
+                                    g["P"], float(g["r"]), float(g["w"]), 0.96, 5.0,
+                                    float(g["amin"]), 1e-5, 1000.0)
+    R = pkg.egm_solve(g["policy_c0"], g["a_grid"], g["s"], g["P"], float(g["r"]), float(g["w"]),
+                      0.96, 5.0, float(g["amin"]))
+    assert int(it[0, 0]) == R["iters"] and np.array_equal(pc, R["policy_c"])
+    U = no.matlab_rand_stream(100)
+    K, path, zs = mexstub.call("aiy_sim_capital_mex", 3, pk, g["a_grid"], g["P"], 3.0,
+                               float(g["a_grid"][50]), U)
+    Ko, po = corc.sim_capital(pk.T, g["a_grid"], g["P"], 2, float(g["a_grid"][50]), U,
+                              return_path=True)
+    assert K[0, 0] == Ko and np.array_equal(path[:, 0], po)
+
+
+def test_labor_vfi_and_dist_gateways(pkg, gpu, golden):
+    g = golden("a3_labor_vfi_na100")
+    out = mexstub.call("aiy_labor_vfi_solve_mex", 6, np.zeros((7, 100)), g["a_grid"], g["s"],
+                       g["P"], g["L"], float(g["r"]), float(g["w"]), 0.96, 5.0, 1.0, 2.0, 1e-5,
+                       1000.0)
+    v_new, v_old, pk, pl, pc, it = out
+    assert int(it[0, 0]) == int(g["iters"])
+    assert np.array_equal(v_new, g["v_new"]) and np.array_equal(pl, g["policy_l"])
+    a1 = golden("a1_vfi_defaults")
+    d = golden("a10_dist_defaults")
+    lam, K, it2, dist = mexstub.call("aiy_dist_stationary_mex", 4, d["idx"] + 1.0, a1["a_grid"],
+                                     a1["P"], d["lam0"], 0.0, 1.0, 1.0)
+    assert np.array_equal(lam, corc.dist_update_ongrid(d["lam0"], d["idx"], a1["P"]))
+
+
+def test_ks_gateway(pkg, gpu, golden):
+    g = golden("ks_defaults")
+    prm = pkg.ks_params()
+    B = np.array([0.0, 1.0, 0.0, 1.0])
+    V, ko, it, rel = mexstub.call("ks_vfi_solve_mex", 4, g["V0"], g["V0"] * 0 + 1, g["k_grid"],
+                                  g["K_grid"], B, g["P"], prm, 5.0, 1e-6, 3.0, 1.0)
+    R = pkg.ks_vfi_solve(g["V0"], g["V0"] * 0 + 1, g["k_grid"], g["K_grid"], B, g["P"], prm,
+                         howard_steps=5, tol=1e-6, max_vfi=3)
+    assert int(it[0, 0]) == R["iters"]
+    assert np.array_equal(V.reshape(R["value"].shape, order="F"), R["value"])

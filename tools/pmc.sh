@@ -1,0 +1,21 @@
+#!/bin/bash
+# PMC passes over a short bench run, one counter group per pass (gfx950 slot limits:
+# <= 8 SQ, <= 4 TCC (FETCH_SIZE uses 3, WRITE_SIZE 2), <= 2 GRBM).  Each pass is KILL-bounded.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=${OUT:-gpurun_out/pmc}
+ARGS=${BENCH_ARGS:---no-cpu-baseline --steps 3 --warmup 2}
+mkdir -p "$OUT"
+pass() {  # name, counters...
+  local name=$1; shift
+  echo "=== pmc $name: $*"
+  timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv -d "$PWD/$OUT/$name" -o run -- python3 "$PWD/bench.py" $ARGS > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== pmc $name rc=$rc"
+  if [ $rc -ne 0 ]; then tail -5 "$OUT/$name.log"; exit $rc; fi
+}
+pass sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU
+pass grbm GRBM_GUI_ACTIVE GRBM_COUNT
+pass fetch FETCH_SIZE
+pass write WRITE_SIZE
+echo "=== pmc done"
