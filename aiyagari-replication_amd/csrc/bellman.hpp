@@ -12,6 +12,7 @@ struct BellArgs {
     int np;          // sigma-1 when sigma is an integer in [2, 9]; 0 = generic sigma
     int coarse;      // init coarse stride S (0 = no coarse scan)
     int CK;          // candidates a' per work item
+    int variant;     // screen kernel geometry (tuning): bit0 R=4, bit1 register cap
     double r, w, beta, sigma;
     const double* v_old;
     const double* a;

@@ -177,9 +177,9 @@ __global__ void bell_init_kernel(BellArgs A) {
 }
 
 // ------------------------------------------------------------------------------ 3. screen
-template <int NP, bool LAB, int R, int LB, int KB>
-__global__ __launch_bounds__(256) void bell_screen_kernel(BellArgs A, int ntile, int nlb,
-                                                          int nchunk) {
+template <int NP, bool LAB, int R, int LB, int KB, int MINW>
+__global__ __launch_bounds__(256, MINW) void bell_screen_kernel(BellArgs A, int ntile, int nlb,
+                                                                int nchunk) {
     const int wave = readfirst(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int item = readfirst(blockIdx.x * 4 + wave);
@@ -197,20 +197,19 @@ __global__ __launch_bounds__(256) void bell_screen_kernel(BellArgs A, int ntile,
     const int l0 = lbk * LB;
     const int l1 = min(l0 + LB, Nl);
     const double y = A.w * A.s[i];
-    // wave-uniform feasible range: smallest / largest cash on hand in this item
-    double cmin = __builtin_inf(), cmax = -__builtin_inf();
+    // wave-uniform feasible range from the cached prefixes (kf is monotone in j)
+    int kmax = 0, kmin = 0x7fffffff;
     {
-        double xb = (1 + A.r) * a[jbase], xl = (1 + A.r) * a[jlast];
+        const size_t nall = (size_t)N * Na;
         for (int l = l0; l < l1; ++l) {
-            double Ll = LAB ? A.L[l] : 1.0;
-            cmin = fmin(cmin, cash<LAB>(xb, y, Ll));
-            cmax = fmax(cmax, cash<LAB>(xl, y, Ll));
+            kmax = max(kmax, A.kf[l * nall + (size_t)i * Na + jlast]);
+            kmin = min(kmin, A.kf[l * nall + (size_t)i * Na + jbase]);
         }
+        kmax = readfirst(kmax);
+        kmin = readfirst(kmin);
     }
-    const int kmax = readfirst(lower_bound_dev(a, Na, cmax));
     const int k_lo = chunk * CK;
     if (k_lo >= kmax) return;
-    const int kmin = readfirst(lower_bound_dev(a, Na, cmin));
     const int k_hi = min(k_lo + CK, kmax);
 
     double coh[R][LB], B[R][LB], best[R], dis[LB];
@@ -270,7 +269,8 @@ __global__ __launch_bounds__(256) void bell_screen_kernel(BellArgs A, int ntile,
     auto run = [&](auto guard, int kb, int ke) {
         int k = kb;
         for (; k + KB <= ke; k += KB) {
-            bool hit = false;
+            // max of t over the block (NaN from invalid sub-states drops out of fmax)
+            double tm = -__builtin_inf();
 #pragma unroll
             for (int kk = 0; kk < KB; ++kk) {
                 const double2 tk = Trow[k + kk];  // wave-uniform address → scalar loads
@@ -280,23 +280,23 @@ __global__ __launch_bounds__(256) void bell_screen_kernel(BellArgs A, int ntile,
                     for (int q = 0; q < LB; ++q) {
                         double c = coh[r][q] - tk.x;
                         if constexpr (decltype(guard)::value) c = fmax(c, 0.0);
-                        hit |= ((tk.y - B[r][q]) * aiy_ipow(c, NP) >= kThr);
+                        tm = fmax(tm, (tk.y - B[r][q]) * aiy_ipow(c, NP));
                     }
                 }
             }
-            if (__any(hit)) exact_block(k, k + KB);
+            if (__any(tm >= kThr)) exact_block(k, k + KB);
         }
         if (k < ke) {
-            bool hit = false;
+            double tm = -__builtin_inf();
             for (int kk = k; kk < ke; ++kk) {
                 const double2 tk = Trow[kk];
 #pragma unroll
                 for (int r = 0; r < R; ++r)
 #pragma unroll
                     for (int q = 0; q < LB; ++q)
-                        hit |= ((tk.y - B[r][q]) * aiy_ipow(fmax(coh[r][q] - tk.x, 0.0), NP) >= kThr);
+                        tm = fmax(tm, (tk.y - B[r][q]) * aiy_ipow(fmax(coh[r][q] - tk.x, 0.0), NP));
             }
-            if (__any(hit)) exact_block(k, ke);
+            if (__any(tm >= kThr)) exact_block(k, ke);
         }
     };
     const int r1_end = min(k_hi, max(k_lo, kmin));
@@ -413,9 +413,12 @@ int launch_bell_kf(const BellArgs& A, hipStream_t st) {
     return AIY_OK;
 }
 
+#ifndef AIY_BELL_R
+#define AIY_BELL_R 2
+#endif
 template <int NP, bool LAB>
 struct Geo {
-    static constexpr int R = LAB ? 1 : 2;
+    static constexpr int R = LAB ? 1 : AIY_BELL_R;
     static constexpr int LB = LAB ? 5 : 1;
 };
 
@@ -423,13 +426,27 @@ template <int NP, bool LAB>
 static void run_init(const BellArgs& A, hipStream_t st) {
     bell_init_kernel<NP, LAB><<<cdiv(A.N * A.Na, 128), 128, 0, st>>>(A);
 }
+template <int NP, bool LAB, int R, int MINW>
+static void screen_geo(const BellArgs& A, hipStream_t st) {
+    constexpr int LB = LAB ? 5 : 1;
+    int ntile = cdiv(A.Na, 64 * R), nlb = cdiv(A.Nl, LB), nchunk = cdiv(A.Na, A.CK);
+    long long items = (long long)A.N * ntile * nlb * nchunk;
+    bell_screen_kernel<NP, LAB, R, LB, 8, MINW><<<cdiv(items, 4), 256, 0, st>>>(A, ntile, nlb, nchunk);
+}
 template <int NP, bool LAB>
 static void run_screen(const BellArgs& A, hipStream_t st) {
     if constexpr (NP > 0) {
-        constexpr int R = Geo<NP, LAB>::R, LB = Geo<NP, LAB>::LB;
-        int ntile = cdiv(A.Na, 64 * R), nlb = cdiv(A.Nl, LB), nchunk = cdiv(A.Na, A.CK);
-        long long items = (long long)A.N * ntile * nlb * nchunk;
-        bell_screen_kernel<NP, LAB, R, LB, 8><<<cdiv(items, 4), 256, 0, st>>>(A, ntile, nlb, nchunk);
+        if constexpr (LAB) {
+            screen_geo<NP, LAB, 1, 1>(A, st);
+        } else {
+            // variant: bit 0 → 4 states per lane (else 2); bit 1 → cap registers for 8 waves/SIMD
+            switch (A.variant & 3) {
+                case 1: screen_geo<NP, LAB, 4, 1>(A, st); break;
+                case 2: screen_geo<NP, LAB, 2, 8>(A, st); break;
+                case 3: screen_geo<NP, LAB, 4, 8>(A, st); break;
+                default: screen_geo<NP, LAB, 2, 1>(A, st); break;
+            }
+        }
     }
 }
 template <int NP, bool LAB>
@@ -483,7 +500,7 @@ int launch_bell_merge(const BellArgs& A, int use_partial, hipStream_t st) {
 }
 
 size_t bell_partial_slots(const BellArgs& A) {
-    int LB = A.labor ? 5 : 1;
+    int LB = A.labor ? 5 : 1;  // independent of the per-lane state count R (indexed by j)
     return (size_t)cdiv(A.Nl, LB) * cdiv(A.Na, A.CK) * A.N * A.Na;
 }
 

@@ -116,6 +116,7 @@ int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
     bool screened = (c.mode != 2) && A.np > 0;
     A.coarse = ws->coarse;
     A.CK = ws->CK;
+    A.variant = ws->variant;
     A.r = c.r;
     A.w = c.w;
     A.beta = c.beta;
@@ -292,6 +293,13 @@ int aiy_ws_timing(aiy_ws* ws, double* total_ms, int64_t* launches, int64_t* hits
 int aiy_ws_invalidate(aiy_ws* ws) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
     ws->kf_ok = false;
+    return AIY_OK;
+}
+
+int aiy_ws_set_variant(aiy_ws* ws, int variant) {
+    if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
+    if (variant < 0 || variant > 3) return fail(AIY_BAD_ARG, "variant in [0, 3]");
+    ws->variant = variant;
     return AIY_OK;
 }
 

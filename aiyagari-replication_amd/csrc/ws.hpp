@@ -13,6 +13,7 @@ struct aiy_ws {
     // search knobs (aiy_ws_set_search)
     int coarse = 512;
     int CK = 1024;
+    int variant = 0;
     // VFI scratch
     double* EV = nullptr;
     double2* T = nullptr;

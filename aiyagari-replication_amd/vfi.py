@@ -84,6 +84,10 @@ class Workspace:
         """Drop the cached feasibility table (after overwriting a_grid/s/L in place)."""
         check(lib().aiy_ws_invalidate(self._h))
 
+    def set_variant(self, variant: int):
+        """Screen-kernel geometry (tuning; results identical): 0 R=2, 1 R=4, 2/3 capped regs."""
+        check(lib().aiy_ws_set_variant(self._h, ip(variant)))
+
     def set_search(self, coarse_stride=0, k_chunk=1024):
         check(lib().aiy_ws_set_search(self._h, ip(coarse_stride), ip(k_chunk)))
 

@@ -39,10 +39,13 @@ def test_solve_max_iter_exhausted(pkg, gpu, golden):
     assert np.array_equal(R["v_old"], R["v_new"])  # :88 ran after the last sweep
 
 
-def _device_sweep(pkg, torch, V, a, s, P, r, w, beta, sigma, mode, hint=None, ws=None):
+def _device_sweep(pkg, torch, V, a, s, P, r, w, beta, sigma, mode, hint=None, ws=None,
+                  variant=0, k_chunk=1024):
     dev = torch.device("cuda:0")
     N, Na = V.shape
     ws = ws or pkg.Workspace(N, Na)
+    ws.set_variant(variant)
+    ws.set_search(0, k_chunk)
     t = lambda x: torch.as_tensor(np.ascontiguousarray(x), device=dev)
     vo, at, st, Pt = t(V), t(a), t(s), t(P)
     vn = torch.empty_like(vo); pk = torch.empty_like(vo); pc = torch.empty_like(vo)
@@ -53,15 +56,17 @@ def _device_sweep(pkg, torch, V, a, s, P, r, w, beta, sigma, mode, hint=None, ws
     return vn.cpu().numpy(), idx.cpu().numpy(), pk.cpu().numpy(), pc.cpu().numpy()
 
 
+@pytest.mark.parametrize("variant,k_chunk", [(0, 1024), (1, 1024), (1, 512), (3, 256)])
 @pytest.mark.parametrize("Na,shocks", [(1500, "rouwenhorst"), (777, "tauchen")])
-def test_screened_equals_plain_and_oracle(pkg, gpu, Na, shocks):
+def test_screened_equals_plain_and_oracle(pkg, gpu, Na, shocks, variant, k_chunk):
     import torch
     cal = no.calib_aiyagari(Na=Na, shocks=shocks)
     a, s, P = cal["a_grid"], cal["s"], cal["P"]
     r = 0.02
     w = no.wage(r, 0.36, 0.08)
     V = corc.vfi_solve(np.zeros((7, Na)), a, s, P, r, w, 0.96, 5.0, 1e-5, 15)["v_new"]
-    vs, is_, pks, pcs = _device_sweep(pkg, torch, V, a, s, P, r, w, 0.96, 5.0, mode=1)
+    vs, is_, pks, pcs = _device_sweep(pkg, torch, V, a, s, P, r, w, 0.96, 5.0, mode=1,
+                                      variant=variant, k_chunk=k_chunk)
     vp, ip_, _, _ = _device_sweep(pkg, torch, V, a, s, P, r, w, 0.96, 5.0, mode=2)
     vo, io, pko, pco = corc.vfi_sweep(V, a, s, P, r, w, 0.96, 5.0)
     assert np.array_equal(vs, vo) and np.array_equal(is_, io)

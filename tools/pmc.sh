@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/pmc}
-ARGS=${BENCH_ARGS:---no-cpu-baseline --steps 3 --warmup 2}
+ARGS=${BENCH_ARGS:---no-cpu-baseline --no-ge --steps 3 --warmup 2}
 mkdir -p "$OUT"
 pass() {  # name, counters...
   local name=$1; shift
