@@ -12,7 +12,7 @@ struct BellArgs {
     int np;          // sigma-1 when sigma is an integer in [2, 9]; 0 = generic sigma
     int coarse;      // init coarse stride S (0 = no coarse scan)
     int CK;          // candidates a' per work item
-    int variant;     // screen kernel geometry (tuning): bit0 R=4, bit1 register cap
+    int variant;     // screen kernel geometry (tuning): bit0 R=4, bit1 register cap, bit2 fp64-only screen
     double r, w, beta, sigma;
     const double* v_old;
     const double* a;
@@ -24,6 +24,7 @@ struct BellArgs {
     // scratch
     double* EV;
     double2* T;
+    float* T32;     // chunk-relative fp32 screening table (nullable: fp64 screen only)
     double* best0;
     int* idx0;
     int* kf;       // [Nl][N][Na] feasible prefix lengths #{k : a_k < coh(j, l)}

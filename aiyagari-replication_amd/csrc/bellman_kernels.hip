@@ -19,6 +19,12 @@
 //              evaluating exactly only the candidates that pass, and merging with the
 //              (max value, first column-major index) rule, reproduces the plain exhaustive
 //              scan bit for bit.
+//              Mixed precision: each work item first screens in packed fp32 (v_pk_* — two
+//              candidates per VALU op) against a chunk-relative table rounded OUTWARD
+//              (a' rounded down, D' up, coh' up, B' down) with threshold 1 − 2^-19, which
+//              bounds every fp32 rounding of the product; a passing 16-candidate block is
+//              re-screened in fp64 and evaluated exactly, so the fp32 stage only ever adds
+//              work, never drops a candidate.
 //   4. merge   per state: init ⊕ every chunk's improvement → v_new, index, policy_k = a(k),
 //              policy_l = L(l), policy_c = c(l,k), and max|v_new − v_old| ignoring NaN via an
 //              order-independent atomicMax on IEEE bits.
@@ -32,6 +38,30 @@ namespace aiy {
 
 constexpr double kTau = 9.094947017729282e-13;  // 2^-40
 constexpr double kThr = 0.99999999999999644729;  // 1 - 2^-48
+constexpr float kThr32 = 0.999998092651367f;      // 1 - 2^-19 (exact in fp32)
+constexpr float kBig32 = 1.152921504606847e18f;   // 2^60: fp32-path range guard
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// fp64 → fp32 rounded outward by one step past round-to-nearest: a rigorous upper (lower)
+// bound of the real value even with the fp64 rounding of x's own computation
+__device__ __forceinline__ float f32_up(double x) { return nextafterf((float)x, __builtin_inff()); }
+__device__ __forceinline__ float f32_dn(double x) { return nextafterf((float)x, -__builtin_inff()); }
+
+template <int NP>
+__device__ __forceinline__ f32x2 ipow2(f32x2 c) {
+    static_assert(NP >= 1 && NP <= 8, "screen exponent");
+    if constexpr (NP == 1) return c;
+    f32x2 c2 = c * c;
+    if constexpr (NP == 2) return c2;
+    if constexpr (NP == 3) return c2 * c;
+    f32x2 c4 = c2 * c2;
+    if constexpr (NP == 4) return c4;
+    if constexpr (NP == 5) return c4 * c;
+    if constexpr (NP == 6) return c4 * c2;
+    if constexpr (NP == 7) return (c4 * c2) * c;
+    return c4 * c4;
+}
 
 // exact value of candidate (c, l, k) in the literal MATLAB order
 template <int NP, bool LAB>
@@ -73,19 +103,37 @@ __device__ __forceinline__ double cash(double x, double y, double Ll) {
 }
 
 // ------------------------------------------------------------------------------ 1. table
+__device__ __forceinline__ double table_ev(int N, int Na, const double* __restrict__ P,
+                                           const double* __restrict__ V, double beta, int i,
+                                           int k) {
+    double acc = 0.0;
+    for (int m = 0; m < N; ++m) acc = acc + (beta * P[i * N + m]) * V[m * Na + k];
+    return acc;
+}
+__device__ __forceinline__ double table_D(double ev, int np) {
+    double ne = (double)np * ev;
+    return (ne + 1.0) + kTau * (fabs(ne) + 1.0);
+}
+
 __global__ void bell_table_kernel(int N, int Na, const double* __restrict__ P,
                                   const double* __restrict__ V, double beta, int np,
                                   const double* __restrict__ a, double* __restrict__ EV,
-                                  double2* __restrict__ T) {
+                                  double2* __restrict__ T, float* __restrict__ T32, int CK) {
     int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= N * Na) return;
     int i = t / Na, k = t - i * Na;
-    double acc = 0.0;
-    for (int m = 0; m < N; ++m) acc = acc + (beta * P[i * N + m]) * V[m * Na + k];
+    double acc = table_ev(N, Na, P, V, beta, i, k);
     EV[t] = acc;
     if (T) {
-        double ne = (double)np * acc;
-        T[t] = make_double2(a[k], (ne + 1.0) + kTau * (fabs(ne) + 1.0));
+        double D = table_D(acc, np);
+        T[t] = make_double2(a[k], D);
+        if (T32) {  // relative to the chunk origin (a, D at k0): small magnitudes, fine ulps
+            int k0 = k - k % CK;
+            double D0 = table_D(table_ev(N, Na, P, V, beta, i, k0), np);
+            float* pr = T32 + 2 * (size_t)i * (Na + (Na & 1)) + 2 * (k & ~1) + (k & 1);
+            pr[0] = f32_dn(a[k] - a[k0]);  // pair layout {a_k, a_k+1, D_k, D_k+1}
+            pr[2] = f32_up(D - D0);
+        }
     }
 }
 
@@ -300,8 +348,83 @@ __global__ __launch_bounds__(256, MINW) void bell_screen_kernel(BellArgs A, int 
         }
     };
     const int r1_end = min(k_hi, max(k_lo, kmin));
-    run(std::false_type{}, k_lo, r1_end);
-    run(std::true_type{}, r1_end, k_hi);
+
+    // ---- packed fp32 pre-screen (all quantities relative to the chunk origin k_lo)
+    bool use32 = A.T32 != nullptr;
+    float cp[R][LB], bp[R][LB];
+    const float* __restrict__ T32row = use32 ? A.T32 + 2 * (size_t)i * (Na + (Na & 1)) : nullptr;
+    double A0 = 0.0, S0 = 0.0;
+    auto set_bp = [&]() {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int q = 0; q < LB; ++q)
+                bp[r][q] = (B[r][q] == B[r][q]) ? f32_dn(B[r][q] - S0) : __builtin_nanf("");
+    };
+    if (use32) {
+        A0 = a[k_lo];
+        S0 = Trow[k_lo].y;
+        bool ok = true;
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int q = 0; q < LB; ++q) cp[r][q] = f32_up(coh[r][q] - A0);
+        set_bp();
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int q = 0; q < LB; ++q) {
+                ok = ok && fabsf(cp[r][q]) <= kBig32;
+                ok = ok && (bp[r][q] != bp[r][q] || fabsf(bp[r][q]) <= kBig32);
+            }
+        // the chunk's table must be finite and moderate (else t = inf·0 could hide a pass)
+        for (int k = k_lo + lane; k < k_hi; k += 64)
+            ok = ok && fabsf(T32row[2 * (k & ~1) + 2 + (k & 1)]) <= kBig32;
+        use32 = __all(ok);
+    }
+    auto run32 = [&](auto guard, int kb, int ke) {
+        int k = kb;
+        for (; k + KB <= ke; k += KB) {
+            float tm = -__builtin_inff();
+#pragma unroll
+            for (int kk = 0; kk < KB; kk += 2) {
+                // pair layout {a_k, a_k+1, D_k, D_k+1}: 64-bit scalar operands as loaded
+                const float4 tq = *reinterpret_cast<const float4*>(T32row + 2 * (k + kk));
+                const f32x2 av = {tq.x, tq.y}, dv = {tq.z, tq.w};
+                f32x2 tt[R][LB];
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int q = 0; q < LB; ++q) {
+                        f32x2 c = f32x2{cp[r][q], cp[r][q]} - av;
+                        if constexpr (decltype(guard)::value) {
+                            c.x = fmaxf(c.x, 0.0f);
+                            c.y = fmaxf(c.y, 0.0f);
+                        }
+                        tt[r][q] = (dv - f32x2{bp[r][q], bp[r][q]}) * ipow2<NP>(c);
+                    }
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int q = 0; q < LB; ++q) tm = fmaxf(fmaxf(tm, tt[r][q].x), tt[r][q].y);
+            }
+            if (__any(tm >= kThr32)) {
+                exact_block(k, k + KB);  // fp64 screen + exact values on this block
+                set_bp();
+            }
+        }
+        if (k < ke) run(guard, k, ke);  // ragged tail: fp64
+    };
+    if (use32) {
+        // the pair layout needs even block starts: move the region split down to even
+        // (the guarded loop is valid for feasible candidates too)
+        const int r1_even = max(k_lo, r1_end & ~1);
+        run32(std::false_type{}, k_lo, r1_even);
+        run32(std::true_type{}, r1_even, k_hi);
+    } else {
+        run(std::false_type{}, k_lo, r1_end);
+        run(std::true_type{}, r1_end, k_hi);
+    }
 
     const size_t slab = ((size_t)lbk * nchunk + chunk) * N + i;
 #pragma unroll
@@ -400,7 +523,8 @@ static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b)
 int launch_bell_table(const BellArgs& A, hipStream_t st) {
     int n = A.N * A.Na;
     bell_table_kernel<<<cdiv(n, 256), 256, 0, st>>>(A.N, A.Na, A.P, A.v_old, A.beta, A.np, A.a,
-                                                    A.EV, A.np > 0 ? A.T : nullptr);
+                                                    A.EV, A.np > 0 ? A.T : nullptr,
+                                                    A.np > 0 ? A.T32 : nullptr, A.CK);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }

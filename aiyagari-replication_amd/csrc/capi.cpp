@@ -56,6 +56,7 @@ int ws_ensure_bell(aiy_ws* ws, size_t partial_slots) {
     size_t n = (size_t)ws->N * ws->Na;
     AIY_TRY(dalloc(&ws->EV, n));
     AIY_TRY(dalloc(&ws->T, n));
+    AIY_TRY(dalloc(&ws->T32, 2 * (size_t)ws->N * (ws->Na + (ws->Na & 1))));
     AIY_TRY(dalloc(&ws->best0, n));
     AIY_TRY(dalloc(&ws->idx0, n));
     if (ws->partial && ws->partial_cap < partial_slots) dfree(ws->partial);
@@ -131,6 +132,7 @@ int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
     A.dis = c.labor ? ws->dis : nullptr;
     A.EV = ws->EV;
     A.T = ws->T;
+    A.T32 = (ws->variant & 4) ? nullptr : ws->T32;
     A.best0 = ws->best0;
     A.idx0 = ws->idx0;
     A.partial = ws->partial;
@@ -298,7 +300,7 @@ int aiy_ws_invalidate(aiy_ws* ws) {
 
 int aiy_ws_set_variant(aiy_ws* ws, int variant) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
-    if (variant < 0 || variant > 3) return fail(AIY_BAD_ARG, "variant in [0, 3]");
+    if (variant < 0 || variant > 7) return fail(AIY_BAD_ARG, "variant in [0, 7]");
     ws->variant = variant;
     return AIY_OK;
 }

@@ -20,63 +20,10 @@
 //   tiled    slopes / improve / howard / reldiff as separate grid-wide kernels (any size).
 #include "aiy_common.hpp"
 #include "ks.hpp"
+#include "pchip_dev.hpp"
 
 namespace aiy {
 
-__device__ __forceinline__ int sgn_dev(double x) { return (x > 0) - (x < 0); }
-
-// pchip slope at point q of a column (x = k_grid), MATLAB pchipslopes
-__device__ double pchip_slope(const double* __restrict__ x, const double* __restrict__ y, int n,
-                              int q) {
-    if (q == 0 || q == n - 1) {
-        double h0, h1, e0, e1;
-        if (q == 0) {
-            h0 = x[1] - x[0];
-            h1 = x[2] - x[1];
-            e0 = (y[1] - y[0]) / h0;
-            e1 = (y[2] - y[1]) / h1;
-        } else {
-            h0 = x[n - 1] - x[n - 2];
-            h1 = x[n - 2] - x[n - 3];
-            e0 = (y[n - 1] - y[n - 2]) / h0;
-            e1 = (y[n - 2] - y[n - 3]) / h1;
-        }
-        double d = ((2 * h0 + h1) * e0 - h0 * e1) / (h0 + h1);
-        if (sgn_dev(d) != sgn_dev(e0)) d = 0.0;
-        else if (sgn_dev(e0) != sgn_dev(e1) && fabs(d) > fabs(3 * e0)) d = 3 * e0;
-        return d;
-    }
-    int k = q - 1;
-    double h1 = x[k + 1] - x[k], h2 = x[k + 2] - x[k + 1];
-    double d1 = (y[k + 1] - y[k]) / h1, d2 = (y[k + 2] - y[k + 1]) / h2;
-    if (sgn_dev(d1) * sgn_dev(d2) > 0) {
-        double hs = h1 + h2;
-        double w1 = (h1 + hs) / (3 * hs);
-        double w2 = (hs + h2) / (3 * hs);
-        double dmax = fmax(fabs(d1), fabs(d2));
-        double dmin = fmin(fabs(d1), fabs(d2));
-        return dmin / (w1 * (d1 / dmax) + w2 * (d2 / dmax));
-    }
-    return 0.0;
-}
-
-// pwch coefficients + ppval Horner on segment i
-__device__ __forceinline__ double pchip_at(const double* __restrict__ x,
-                                           const double* __restrict__ y,
-                                           const double* __restrict__ d, int i, double xq) {
-    double h = x[i + 1] - x[i];
-    double dl = (y[i + 1] - y[i]) / h;
-    double dzzdx = (dl - d[i]) / h;
-    double dzdxdx = (d[i + 1] - dl) / h;
-    double c3 = (dzdxdx - dzzdx) / h;
-    double c2 = 2 * dzzdx - dzdxdx;
-    double sx = xq - x[i];
-    double v = c3;
-    v = sx * v + c2;
-    v = sx * v + d[i];
-    v = sx * v + y[i];
-    return v;
-}
 
 struct KsView {  // where the value/slope columns and the grid live (LDS or global)
     const double* kg;

@@ -17,6 +17,7 @@ struct aiy_ws {
     // VFI scratch
     double* EV = nullptr;
     double2* T = nullptr;
+    float* T32 = nullptr;
     double* best0 = nullptr;
     int* idx0 = nullptr;
     double* dis = nullptr;
@@ -54,12 +55,12 @@ struct aiy_ws {
     int64_t launches = 0;
 
     void free_all() {
-        void* ps[] = {EV, T, best0, idx0, dis, kf, partial, diff, hitcount, g0, g1, g2, gi,
+        void* ps[] = {EV, T, T32, best0, idx0, dis, kf, partial, diff, hitcount, g0, g1, g2, gi,
                       d_key, d_head, d_wr, d_mass, d_part};
         for (void* p : ps)
             if (p) (void)hipFree(p);
         if (hdiff) (void)hipHostFree(hdiff);
-        EV = nullptr; T = nullptr; best0 = nullptr; dis = nullptr; kf = nullptr; kf_cap = 0;
+        EV = nullptr; T = nullptr; T32 = nullptr; best0 = nullptr; dis = nullptr; kf = nullptr; kf_cap = 0;
         kf_ok = false;
         idx0 = nullptr; partial = nullptr; diff = nullptr; hitcount = nullptr; hdiff = nullptr;
         g0 = g1 = g2 = nullptr; gi = nullptr;

@@ -154,8 +154,9 @@ int aiy_ws_timing(aiy_ws* ws, double* total_ms, int64_t* launches, int64_t* hits
 int aiy_ws_invalidate(aiy_ws* ws);
 /* search knobs (defaults tuned for gfx950): coarse stride for cold starts, k-chunk. */
 int aiy_ws_set_search(aiy_ws* ws, int coarse_stride, int k_chunk);
-/* screen-kernel geometry (tuning only; results are identical): 0 = 2 states/lane (default),
- * 1 = 4 states/lane, 2/3 = the same with registers capped for 8 waves per SIMD. */
+/* screen-kernel shape (tuning only; results are identical): bit 0 = 4 states per lane (else 2),
+ * bit 1 = registers capped for 8 waves per SIMD, bit 2 = fp64-only screen (else the packed
+ * fp32 pre-screen with directed-rounding bounds runs first).  Default 0. */
 int aiy_ws_set_variant(aiy_ws* ws, int variant);
 
 /* A1 on device.  hint (nullable, [N][Na] int32 0-based) = previous sweep's argmax; the result

@@ -65,3 +65,21 @@ def test_labor_infeasible_state_keeps_incoming(pkg, gpu):
     assert np.array_equal(v, vo)
     assert np.array_equal(pk, pko) and np.array_equal(pl, plo) and np.array_equal(pc, pco)
     assert np.array_equal(lin - 1, lino)
+
+
+@pytest.mark.parametrize("scale", [1e-9, 1e-2])
+def test_labor_screen_stress_noisy_value(pkg, gpu, scale):
+    """Noisy v_old (many near-ties across (l, a')) through the fp32/fp64 screen: bit-exact."""
+    rng = np.random.default_rng(11)
+    Na = 611
+    cal = no.calib_aiyagari(Na=Na, rho=0.6, sigma_e=0.2)
+    a, s, P = cal["a_grid"], cal["s"], cal["P"]
+    L = 0.01 + (1.5 - 0.01) * no.matlab_linspace01(10)
+    w = no.wage(0.04, 0.36, 0.08)
+    V = corc.labor_vfi_solve(np.zeros((7, Na)), a, s, P, L, 0.04, w, 0.96, 5.0, 1.0, 2.0,
+                             1e-5, 15)["v_new"]
+    V = V + scale * rng.standard_normal(V.shape)
+    v, pk, pl, pc, lin = pkg.labor_vfi_sweep(V, a, s, P, L, 0.04, w, 0.96, 5.0, 1.0, 2.0)
+    vo, (pko, plo, pco, lino) = corc.labor_vfi_sweep(V, a, s, P, L, 0.04, w, 0.96, 5.0, 1.0, 2.0)
+    assert np.array_equal(v, vo) and np.array_equal(lin - 1, lino)
+    assert np.array_equal(pk, pko) and np.array_equal(pl, plo) and np.array_equal(pc, pco)

@@ -56,7 +56,7 @@ def _device_sweep(pkg, torch, V, a, s, P, r, w, beta, sigma, mode, hint=None, ws
     return vn.cpu().numpy(), idx.cpu().numpy(), pk.cpu().numpy(), pc.cpu().numpy()
 
 
-@pytest.mark.parametrize("variant,k_chunk", [(0, 1024), (1, 1024), (1, 512), (3, 256)])
+@pytest.mark.parametrize("variant,k_chunk", [(0, 1024), (1, 512), (3, 256), (4, 1024), (5, 256)])
 @pytest.mark.parametrize("Na,shocks", [(1500, "rouwenhorst"), (777, "tauchen")])
 def test_screened_equals_plain_and_oracle(pkg, gpu, Na, shocks, variant, k_chunk):
     import torch
@@ -139,3 +139,25 @@ def test_full_size_bitwise_vs_oracle(pkg, gpu):
     # size-independent properties: policy monotone in a (Topkis), policy_c > 0
     assert (np.diff(is_, axis=1) >= 0).all()
     assert (pcs > 0).all()
+
+
+@pytest.mark.parametrize("variant", [0, 1, 4])
+def test_screen_stress_noisy_value(pkg, gpu, variant):
+    """Rough value functions put many candidates within rounding distance of the running best
+    (near-ties everywhere, multi-modal objectives): the fp32 pre-screen, the fp64 screen and
+    the exact merge must still reproduce the plain exhaustive scan bit for bit — with and
+    without hints, including odd chunk/region boundaries (Na odd, small k_chunk)."""
+    import torch
+    rng = np.random.default_rng(7 + variant)
+    for Na, scale in ((2001, 1e-9), (1537, 1e-3), (999, 1.0)):
+        cal = no.calib_aiyagari(Na=Na, shocks="rouwenhorst")
+        a, s, P = cal["a_grid"], cal["s"], cal["P"]
+        w = no.wage(0.03, 0.36, 0.08)
+        V = corc.vfi_solve(np.zeros((7, Na)), a, s, P, 0.03, w, 0.96, 5.0, 1e-5, 25)["v_new"]
+        V = V + scale * rng.standard_normal(V.shape)
+        vo, io, pko, pco = corc.vfi_sweep(V, a, s, P, 0.03, w, 0.96, 5.0)
+        for hint in (None, rng.integers(0, Na, (7, Na))):
+            vs, is_, pks, pcs = _device_sweep(pkg, torch, V, a, s, P, 0.03, w, 0.96, 5.0,
+                                              mode=1, hint=hint, variant=variant, k_chunk=264)
+            assert np.array_equal(vs, vo) and np.array_equal(is_, io), (Na, scale)
+            assert np.array_equal(pks, pko) and np.array_equal(pcs, pco)
