@@ -33,6 +33,20 @@ int fail(int code, const char* fmt, ...);
 
 // ---------------------------------------------------------------- device helpers
 __device__ __forceinline__ int readfirst(int x) { return __builtin_amdgcn_readfirstlane(x); }
+// bijective XCD-aware block order (cdna_hip_programming.md T1): blocks with equal b % 8 share
+// an XCD and receive consecutive logical ids
+__device__ __forceinline__ int xcd_remap(int b, int G) {
+    const int q = G / 8, r = G % 8, x = b % 8, slot = b / 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + slot;
+}
+__device__ __forceinline__ int readlane_i(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+// lane l's double (l wave-uniform) as a wave-uniform value: two v_readlane_b32, no memory
+__device__ __forceinline__ double readlane_d(double x, int l) {
+    unsigned long long u = __builtin_bit_cast(unsigned long long, x);
+    unsigned lo = __builtin_amdgcn_readlane((int)(unsigned)u, l);
+    unsigned hi = __builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
 
 // first k in [0, n) with a[k] >= x  (== count of a[k] < x), a non-decreasing.
 __device__ __forceinline__ int lower_bound_dev(const double* __restrict__ a, int n, double x) {

@@ -25,12 +25,20 @@ struct BellArgs {
     double* EV;
     double2* T;
     float* T32;     // chunk-relative fp32 screening table (nullable: fp64 screen only)
+    double* Dm;     // [N][nb] max of the screening key D over each 64-candidate block (chunked screen)
+    double* Dt;     // [N][Na] the screening key D alone (tree screen)
+    double* Dm8;    // [N][nb8] ... over each aligned 8-candidate block (tree screen)
+    double* Dm512;  // [N][nb512] ... over each aligned 512-candidate block (tree screen)
+    int nb, nb8, nb512;  // ceil(Na / 64), ceil(Na / 8), ceil(Na / 512)
+    bool tree;      // tree screen (default) instead of the chunked screen + merge
     double* best0;
     int* idx0;
     int* kf;       // [Nl][N][Na] feasible prefix lengths #{k : a_k < coh(j, l)}
     bool kf_valid; // kf already holds the values for (r, w, a, s, L)
-    int* partial;
-    unsigned long long* hitcount;  // nullable
+    int* partial;   // [nlb][nchunk][N][Na] chunk improvements; -1 between sweeps
+    int* touched;   // [N][Na] 1 when some chunk wrote `partial` for the state this sweep
+    unsigned long long* hitcount;  // nullable, [4]: exact evals, superblock, block, fine tests
+    long long* trace;  // nullable: per tree work item {t0, t1, xcc, nsup, nblk, nfine, nhits, item}
     // outputs
     double* v_new;
     int* idx;   // linear index l + Nl*k (== k for A1)
@@ -44,6 +52,7 @@ int launch_bell_table(const BellArgs& A, hipStream_t st);
 int launch_bell_kf(const BellArgs& A, hipStream_t st);
 int launch_bell_init(const BellArgs& A, hipStream_t st);
 int launch_bell_screen(const BellArgs& A, hipStream_t st);
+int launch_bell_tree(const BellArgs& A, hipStream_t st);
 int launch_bell_plain(const BellArgs& A, hipStream_t st);
 int launch_bell_merge(const BellArgs& A, int use_partial, hipStream_t st);
 size_t bell_partial_slots(const BellArgs& A);

@@ -36,7 +36,7 @@
 
 namespace aiy {
 
-constexpr double kTau = 9.094947017729282e-13;  // 2^-40
+constexpr double kTau = 1.4210854715202004e-14;  // 2^-46 (error analysis: DESIGN.md §5 A1)
 constexpr double kThr = 0.99999999999999644729;  // 1 - 2^-48
 constexpr float kThr32 = 0.999998092651367f;      // 1 - 2^-19 (exact in fp32)
 constexpr float kBig32 = 1.152921504606847e18f;   // 2^60: fp32-path range guard
@@ -69,7 +69,10 @@ __device__ __forceinline__ double bell_val(double c, double ev, double sigma, do
     double u;
     if constexpr (NP > 0) {
         double p = 1.0 / aiy_ipow(c, NP);  // c.^(1-sigma), sigma = NP + 1
-        u = (p - 1) / (1 - sigma);
+        if constexpr ((NP & (NP - 1)) == 0)
+            u = (p - 1) * (-1.0 / NP);  // 1 - sigma = -2^m: the division is exact scaling
+        else
+            u = (p - 1) / (1 - sigma);
     } else {
         if (!LAB && sigma == 1.0) u = aiy_log(c);  // Aiyagari_VFI.m:74-75 (labour script: no branch)
         else u = (aiy_pow(c, 1.0 - sigma) - 1) / (1 - sigma);
@@ -115,24 +118,58 @@ __device__ __forceinline__ double table_D(double ev, int np) {
     return (ne + 1.0) + kTau * (fabs(ne) + 1.0);
 }
 
-__global__ void bell_table_kernel(int N, int Na, const double* __restrict__ P,
-                                  const double* __restrict__ V, double beta, int np,
-                                  const double* __restrict__ a, double* __restrict__ EV,
-                                  double2* __restrict__ T, float* __restrict__ T32, int CK) {
-    int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= N * Na) return;
-    int i = t / Na, k = t - i * Na;
-    double acc = table_ev(N, Na, P, V, beta, i, k);
-    EV[t] = acc;
-    if (T) {
-        double D = table_D(acc, np);
-        T[t] = make_double2(a[k], D);
-        if (T32) {  // relative to the chunk origin (a, D at k0): small magnitudes, fine ulps
-            int k0 = k - k % CK;
-            double D0 = table_D(table_ev(N, Na, P, V, beta, i, k0), np);
-            float* pr = T32 + 2 * (size_t)i * (Na + (Na & 1)) + 2 * (k & ~1) + (k & 1);
-            pr[0] = f32_dn(a[k] - a[k0]);  // pair layout {a_k, a_k+1, D_k, D_k+1}
-            pr[2] = f32_up(D - D0);
+// 2-D grid (x: 512 candidates of a row, y: row i).  Besides EV and the (a_k, D_k) pairs the
+// kernel writes the screening bounds: the maxima of D over aligned 8-, 64- and 512-candidate
+// blocks of the row (lane butterflies, then LDS across the block's 8 waves).  Block (0, 0)
+// clears the diff slots of the coming sweep.
+constexpr int kTableBlock = 512;
+__global__ __launch_bounds__(kTableBlock) void bell_table_kernel(
+    int N, int Na, const double* __restrict__ P, const double* __restrict__ V, double beta,
+    int np, const double* __restrict__ a, double* __restrict__ EV, double2* __restrict__ T,
+    float* __restrict__ T32, int CK, double* __restrict__ Dm, double* __restrict__ Dm8,
+    double* __restrict__ Dm512, int nb, int nb8, int nb512,
+    unsigned long long* __restrict__ diff, double* __restrict__ Dt) {
+    __shared__ double s_max[kTableBlock / 64];
+    const int i = blockIdx.y;
+    const int k = blockIdx.x * kTableBlock + threadIdx.x;
+    if (diff && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2 * kDiffSlots)
+        diff[threadIdx.x] = 0ull;
+    const bool ok = k < Na;
+    double D = -__builtin_inf();
+    if (ok) {
+        const size_t t = (size_t)i * Na + k;
+        double acc = table_ev(N, Na, P, V, beta, i, k);
+        EV[t] = acc;
+        if (T) {
+            D = table_D(acc, np);
+            T[t] = make_double2(a[k], D);
+            if (Dt) Dt[t] = D;
+            if (T32) {  // relative to the chunk origin (a, D at k0): small magnitudes, fine ulps
+                int k0 = k - k % CK;
+                double D0 = table_D(table_ev(N, Na, P, V, beta, i, k0), np);
+                float* pr = T32 + 2 * (size_t)i * (Na + (Na & 1)) + 2 * (k & ~1) + (k & 1);
+                pr[0] = f32_dn(a[k] - a[k0]);  // pair layout {a_k, a_k+1, D_k, D_k+1}
+                pr[2] = f32_up(D - D0);
+            }
+        }
+    }
+    if (!T) return;  // uniform per launch
+    // block maxima (NaN keys drop out of fmax: a NaN candidate is never a maximiser)
+    D = fmax(D, __shfl_xor(D, 1));
+    D = fmax(D, __shfl_xor(D, 2));
+    D = fmax(D, __shfl_xor(D, 4));
+    if (Dm8 && ok && (k & 7) == 0) Dm8[(size_t)i * nb8 + (k >> 3)] = D;
+    D = fmax(D, __shfl_xor(D, 8));
+    D = fmax(D, __shfl_xor(D, 16));
+    D = fmax(D, __shfl_xor(D, 32));
+    if (Dm && ok && (k & 63) == 0) Dm[(size_t)i * nb + (k >> 6)] = D;
+    if (Dm512) {
+        if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = D;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double m = s_max[0];
+            for (int q = 1; q < kTableBlock / 64; ++q) m = fmax(m, s_max[q]);
+            Dm512[(size_t)i * nb512 + blockIdx.x] = m;
         }
     }
 }
@@ -192,7 +229,7 @@ __global__ void bell_init_kernel(BellArgs A) {
         int lk = -1;
         // with a hint only its labour level is searched: one good candidate sets the bar
         if (A.hint && hk >= 0 && l != hl) continue;
-        if (S > 0) {  // coarse scan of the feasible prefix (robust when the policy moved far)
+        if (S > 0 && hk < 0) {  // cold start: coarse scan of the feasible prefix
             int k = 0;
             for (; k + 3 * S < kf; k += 4 * S) {  // 4 independent evaluations in flight
                 double v0 = eval(l, k, coh), v1 = eval(l, k + S, coh);
@@ -284,9 +321,9 @@ __global__ __launch_bounds__(256, MINW) void bell_screen_kernel(BellArgs A, int 
     }
     const double2* __restrict__ Trow = A.T + (size_t)i * Na;
     const double* __restrict__ ev = A.EV + (size_t)i * Na;
-    unsigned nhits = 0;
+    unsigned nhits = 0, nfine = 0;
 
-    auto exact_block = [&](int k0, int kend) {
+    auto exact_block = [&](int k0, int kend) __attribute__((always_inline)) {
         for (int k = k0; k < kend; ++k) {
             const double2 tk = Trow[k];
 #pragma unroll
@@ -314,7 +351,7 @@ __global__ __launch_bounds__(256, MINW) void bell_screen_kernel(BellArgs A, int 
 
     // region 1: every sub-state feasible (k < kmin); region 2: c clamped at 0 so that
     // infeasible candidates (NaN / -Inf in the reference) never pass the screen
-    auto run = [&](auto guard, int kb, int ke) {
+    auto run = [&](auto guard, int kb, int ke) __attribute__((always_inline)) {
         int k = kb;
         for (; k + KB <= ke; k += KB) {
             // max of t over the block (NaN from invalid sub-states drops out of fmax)
@@ -347,22 +384,22 @@ __global__ __launch_bounds__(256, MINW) void bell_screen_kernel(BellArgs A, int 
             if (__any(tm >= kThr)) exact_block(k, ke);
         }
     };
-    const int r1_end = min(k_hi, max(k_lo, kmin));
 
-    // ---- packed fp32 pre-screen (all quantities relative to the chunk origin k_lo)
-    bool use32 = A.T32 != nullptr;
+    // ---- packed fp32 pre-screen (all quantities relative to the chunk origin k_lo), set up
+    // lazily: most work items never reach the candidate level
+    int st32 = A.T32 != nullptr ? 0 : -1;  // 0 = not set up, 1 = on, -1 = off
     float cp[R][LB], bp[R][LB];
-    const float* __restrict__ T32row = use32 ? A.T32 + 2 * (size_t)i * (Na + (Na & 1)) : nullptr;
-    double A0 = 0.0, S0 = 0.0;
-    auto set_bp = [&]() {
+    const float* __restrict__ T32row = A.T32 ? A.T32 + 2 * (size_t)i * (Na + (Na & 1)) : nullptr;
+    double S0 = 0.0;
+    auto set_bp = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
 #pragma unroll
             for (int q = 0; q < LB; ++q)
                 bp[r][q] = (B[r][q] == B[r][q]) ? f32_dn(B[r][q] - S0) : __builtin_nanf("");
     };
-    if (use32) {
-        A0 = a[k_lo];
+    auto setup32 = [&]() __attribute__((always_inline)) {
+        const double A0 = a[k_lo];
         S0 = Trow[k_lo].y;
         bool ok = true;
 #pragma unroll
@@ -378,11 +415,11 @@ __global__ __launch_bounds__(256, MINW) void bell_screen_kernel(BellArgs A, int 
                 ok = ok && (bp[r][q] != bp[r][q] || fabsf(bp[r][q]) <= kBig32);
             }
         // the chunk's table must be finite and moderate (else t = inf·0 could hide a pass)
-        for (int k = k_lo + lane; k < k_hi; k += 64)
-            ok = ok && fabsf(T32row[2 * (k & ~1) + 2 + (k & 1)]) <= kBig32;
-        use32 = __all(ok);
-    }
-    auto run32 = [&](auto guard, int kb, int ke) {
+        for (int k = k_lo + lane; k < k_hi; k += 64)  // no short circuit: loads overlap
+            ok &= fabsf(T32row[2 * (k & ~1) + 2 + (k & 1)]) <= kBig32;
+        st32 = __all(ok) ? 1 : -1;
+    };
+    auto run32 = [&](auto guard, int kb, int ke) __attribute__((always_inline)) {
         int k = kb;
         for (; k + KB <= ke; k += KB) {
             float tm = -__builtin_inff();
@@ -415,24 +452,462 @@ __global__ __launch_bounds__(256, MINW) void bell_screen_kernel(BellArgs A, int 
         }
         if (k < ke) run(guard, k, ke);  // ragged tail: fp64
     };
-    if (use32) {
-        // the pair layout needs even block starts: move the region split down to even
-        // (the guarded loop is valid for feasible candidates too)
-        const int r1_even = max(k_lo, r1_end & ~1);
-        run32(std::false_type{}, k_lo, r1_even);
-        run32(std::true_type{}, r1_even, k_hi);
-    } else {
-        run(std::false_type{}, k_lo, r1_end);
-        run(std::true_type{}, r1_end, k_hi);
+    // one whole 64-candidate block in packed fp32 with a single wave vote: no branch between
+    // the table loads, so they are all in flight together (a pass re-screens per 8 in fp64)
+    auto block32 = [&](auto guard, int b0) __attribute__((always_inline)) {
+        float tm = -__builtin_inff();
+#pragma unroll 8
+        for (int kk = 0; kk < 64; kk += 2) {
+            const float4 tq = *reinterpret_cast<const float4*>(T32row + 2 * (b0 + kk));
+            const f32x2 av = {tq.x, tq.y}, dv = {tq.z, tq.w};
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int q = 0; q < LB; ++q) {
+                    f32x2 c = f32x2{cp[r][q], cp[r][q]} - av;
+                    if constexpr (decltype(guard)::value) {
+                        c.x = fmaxf(c.x, 0.0f);
+                        c.y = fmaxf(c.y, 0.0f);
+                    }
+                    const f32x2 tt = (dv - f32x2{bp[r][q], bp[r][q]}) * ipow2<NP>(c);
+                    tm = fmaxf(fmaxf(tm, tt.x), tt.y);
+                }
+        }
+        if (__any(tm >= kThr32)) {
+            run(guard, b0, b0 + 64);
+            set_bp();
+        }
+    };
+    // candidate level on [b0, b1): b0 is 64-aligned, so the fp32 pair layout lines up
+    auto fine = [&](int b0, int b1) __attribute__((always_inline)) {
+        if (st32 == 0) setup32();
+        if (A.hitcount) nfine += b1 - b0;
+        const bool guard = b1 > kmin;  // some sub-state's feasible prefix ends inside
+        if (st32 == 1) {
+            if (!LAB && b1 - b0 == 64) {  // (labour: 5 sub-states per lane, per-8 votes)
+                if (guard) block32(std::true_type{}, b0);
+                else block32(std::false_type{}, b0);
+            } else {
+                if (guard) run32(std::true_type{}, b0, b1);
+                else run32(std::false_type{}, b0, b1);
+            }
+        } else {
+            if (guard) run(std::true_type{}, b0, b1);
+            else run(std::false_type{}, b0, b1);
+        }
+    };
+    // block bound: for k in [b0, b1) the reference's own ordering gives c_k <= c_b0 and
+    // D_k <= Dmax exactly (fp subtraction/multiplication are monotone), so
+    // t_k = (D_k - B)·c_k^n <= (Dmax - B)·max(c_b0, 0)^n in floating point: a block whose
+    // bound fails the threshold holds no candidate that can reach the running best.
+    auto bound_pass = [&](double dmax, double a0) __attribute__((always_inline)) {
+        double tm = -__builtin_inf();
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int q = 0; q < LB; ++q)
+                tm = fmax(tm, (dmax - B[r][q]) * aiy_ipow(fmax(coh[r][q] - a0, 0.0), NP));
+        return __any(tm >= kThr);
+    };
+    // the chunk's block bounds (Dmax, a at the block start) are fetched one block per lane in
+    // a single round trip; superblock (8-block) maxima by butterfly; tests read them back with
+    // v_readlane — the search itself never waits on memory
+    const double* __restrict__ Dmrow = A.Dm + (size_t)i * A.nb;
+    unsigned nsup = 0, nblk = 0;
+    const int nbk = (k_hi - k_lo + 63) >> 6;
+    for (int g = 0; g < nbk; g += 64) {
+        const int gb = (k_lo >> 6) + g + lane;
+        const bool okb = g + lane < nbk;
+        const double dmv = okb ? Dmrow[gb] : -__builtin_inf();
+        const double a0v = okb ? a[gb << 6] : 0.0;
+        double smv = dmv;
+        smv = fmax(smv, __shfl_xor(smv, 1));
+        smv = fmax(smv, __shfl_xor(smv, 2));
+        smv = fmax(smv, __shfl_xor(smv, 4));
+        const int ng = min(64, nbk - g);
+        for (int sb = 0; sb < ng; sb += 8) {
+            ++nsup;
+            if (!bound_pass(readlane_d(smv, sb), readlane_d(a0v, sb))) continue;
+            const int se = min(sb + 8, ng);
+            for (int b = sb; b < se; ++b) {
+                if (se - sb > 1) {
+                    ++nblk;
+                    if (!bound_pass(readlane_d(dmv, b), readlane_d(a0v, b))) continue;
+                }
+                const int b0 = k_lo + ((g + b) << 6);
+                fine(b0, min(b0 + 64, k_hi));
+            }
+        }
+    }
+    if (A.hitcount) {
+        const unsigned ns = 64 * R * (l1 - l0);
+        nsup *= ns;
+        nblk *= ns;
     }
 
     const size_t slab = ((size_t)lbk * nchunk + chunk) * N + i;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         int j = jbase + r * 64 + lane;
-        if (j < Na) A.partial[slab * Na + j] = imp[r];
+        if (j < Na && imp[r] >= 0) {  // rare: the merge reads and resets only touched states
+            A.partial[slab * Na + j] = imp[r];
+            A.touched[(size_t)i * Na + j] = 1;
+        }
     }
-    if (A.hitcount && nhits) atomicAdd(A.hitcount, (unsigned long long)nhits);
+    if (A.hitcount) {  // instrumentation (aiy_ws_set_timing bit 1): 64 spread slot groups
+        unsigned long long* hc = A.hitcount + 4 * (item % kDiffSlots);
+        if (nhits) atomicAdd(hc, (unsigned long long)nhits);
+        if (lane == 0) {
+            atomicAdd(hc + 1, (unsigned long long)nsup);
+            atomicAdd(hc + 2, (unsigned long long)nblk);
+            if (nfine) atomicAdd(hc + 3, (unsigned long long)nfine * 64 * R * (l1 - l0));
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------ 3'. tree
+// The default screened sweep.  One workgroup of W waves owns 64·R consecutive states of row i
+// and searches all their candidates (every labour level, the whole feasible prefix) through a
+// bound tree, then writes the final outputs itself (no per-chunk partials, no merge pass).
+//   level 0: 512-candidate superblocks — bounds (Dmax512, a at the block start) fetched one
+//            superblock per lane in a single round trip and read back with v_readlane
+//   level 1/2: inside a passing superblock, one round trip fetches its 64 sub-block maxima
+//            (Dmax8) and sub-block starts; 64-blocks are their 8-lane butterfly maxima
+//   level 3: the candidates of every passing 64-block are staged in LDS together (one round
+//            trip); each candidate of a passing sub-block gets the exact fp64 screen test, and
+//            the candidates that pass get their exact value in the literal MATLAB order
+// Every bound is t_blk = (Dmax − B)·max(c_start, 0)^n ≥ t_k for all k in the block, exactly in
+// floating point (monotone rounding), so no candidate that can reach a wave's running best is
+// ever skipped; the (max value, first index) merge is order-independent, hence the result
+// equals the plain exhaustive scan bit for bit, whatever the split of work between waves.
+// Cooperation: the W waves first split the blocks of the superblock holding the current argmax
+// (best first), exchange their bests through LDS so that all hold the same near-optimal bar,
+// then take the remaining superblocks round-robin; a last exchange folds the results.
+// The starting bar is the hint (last sweep's argmax) and its two neighbours, or — on a cold
+// start — the init kernel's candidate (best0/idx0).
+template <int NP, bool LAB, int R, int LB, int W>
+__global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A, int ntile) {
+    const int lane = threadIdx.x & 63;
+    const int wave = readfirst(threadIdx.x >> 6);
+    const int item = (A.variant & 16) ? xcd_remap((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+    const int tile = item % ntile;
+    const int i = item / ntile;
+    const int N = A.N, Na = A.Na, Nl = A.Nl;
+    const size_t nall = (size_t)N * Na;
+    const double* __restrict__ a = A.a;
+    const double* __restrict__ Drow = A.Dt + (size_t)i * Na;
+    const double* __restrict__ ev = A.EV + (size_t)i * Na;
+    const double y = A.w * A.s[i];
+    const int jbase = tile * (64 * R);
+    __shared__ double2 s_cand[W][512];  // each wave's current superblock: (a_k, D_k)
+    __shared__ double s_ev[W][512];     // ... and EV_k for the exact values
+    __shared__ double s_xb[W][64 * R];  // best exchange
+    __shared__ int s_xi[W][64 * R];
+
+    double x[R], best[R];
+    int idx[R];
+    bool okr[R], feas[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int j = jbase + r * 64 + lane;
+        okr[r] = j < Na;
+        const size_t t = (size_t)i * Na + (okr[r] ? j : 0);
+        x[r] = okr[r] ? (1 + A.r) * a[j] : 0.0;
+        best[r] = __builtin_nan("");
+        idx[r] = -1;
+        feas[r] = false;
+        if (!okr[r]) continue;
+        for (int l = 0; l < Nl; ++l) feas[r] = feas[r] || A.kf[l * nall + t] > 0;
+        if (A.hint) {
+            const int h = A.hint[t];
+            if (h >= 0) {
+                const int hl = h % Nl;
+                const int kf = A.kf[hl * nall + t];
+                if (kf > 0) {
+                    const int hk = min(h / Nl, kf - 1);
+                    const double coh = cash<LAB>(x[r], y, LAB ? A.L[hl] : 1.0);
+                    const double dis = LAB ? A.dis[hl] : 0.0;
+                    for (int k = max(hk - 1, 0); k <= min(hk + 1, kf - 1); ++k)
+                        lexi_take(bell_val<NP, LAB>(coh - a[k], ev[k], A.sigma, dis), hl + Nl * k,
+                                  best[r], idx[r]);
+                }
+            }
+        } else {
+            best[r] = A.best0[t];
+            idx[r] = A.idx0[t] == -2 ? -1 : A.idx0[t];
+        }
+    }
+    unsigned nhits = 0, nsup = 0, nblk = 0, nfine = 0;
+    const long long t_start = A.trace ? (long long)wall_clock64() : 0;
+    // phase cycle counters (trace mode): startup, superblock() calls, fine screens, exact paths
+    long long cyc[4] = {0, 0, 0, 0}, c_mark = A.trace ? (long long)__builtin_amdgcn_s_memtime() : 0;
+    auto stamp = [&](int ph) __attribute__((always_inline)) {
+        if (A.trace) {
+            const long long now = (long long)__builtin_amdgcn_s_memtime();
+            cyc[ph] += now - c_mark;
+            c_mark = now;
+        }
+    };
+    stamp(0);
+
+    // every wave leaves with the (max value, first index) of all waves' bests
+    auto exchange = [&]() __attribute__((always_inline)) {
+        if constexpr (W > 1) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                s_xb[wave][r * 64 + lane] = best[r];
+                s_xi[wave][r * 64 + lane] = idx[r];
+            }
+            __syncthreads();
+            for (int v = 0; v < W; ++v)
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    if (v != wave && s_xi[v][r * 64 + lane] >= 0)
+                        lexi_take(s_xb[v][r * 64 + lane], s_xi[v][r * 64 + lane], best[r], idx[r]);
+            __syncthreads();
+        }
+    };
+
+    for (int l0 = 0; l0 < Nl; l0 += LB) {  // labour levels in groups of LB sub-states per lane
+        double coh[R][LB], B[R][LB], dis[LB];
+        int kg = 0;  // the group's feasible range over the tile (identical in every wave)
+#pragma unroll
+        for (int q = 0; q < LB; ++q) dis[q] = (LAB && l0 + q < Nl) ? A.dis[l0 + q] : 0.0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const size_t t = (size_t)i * Na + (okr[r] ? jbase + r * 64 + lane : 0);
+#pragma unroll
+            for (int q = 0; q < LB; ++q) {
+                const bool okq = okr[r] && l0 + q < Nl;
+                coh[r][q] = okq ? cash<LAB>(x[r], y, LAB ? A.L[l0 + q] : 1.0) : 0.0;
+                if (okq) kg = max(kg, A.kf[(l0 + q) * nall + t]);
+            }
+        }
+        for (int off = 32; off > 0; off >>= 1) kg = max(kg, __shfl_xor(kg, off));
+        kg = readfirst(kg);
+        if (kg == 0) continue;
+        if (l0 > 0) exchange();  // the previous group left per-wave bests
+        auto set_B = [&]() __attribute__((always_inline)) {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int q = 0; q < LB; ++q)  // invalid sub-states: NaN bar, every test false
+                    B[r][q] = (okr[r] && l0 + q < Nl) ? screen_B(best[r], idx[r], dis[q], NP)
+                                                      : __builtin_nan("");
+        };
+        set_B();
+
+        auto bound_pass = [&](double dmax, double a0) __attribute__((always_inline)) {
+            double tm = -__builtin_inf();
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int q = 0; q < LB; ++q)
+                    tm = fmax(tm, (dmax - B[r][q]) * aiy_ipow(fmax(coh[r][q] - a0, 0.0), NP));
+            return __any(tm >= kThr);
+        };
+        // candidates [k0, k1), k1 - k0 <= 8, of superblock sbase staged in LDS.  First the
+        // exact screen test on all of them without a branch (the current argmax itself is
+        // masked: its value is known); only when some lane passes, the branchy exact path:
+        // re-test, exact value in the literal MATLAB order, (max value, first index) merge
+        auto fine = [&](int sbase, int k0, int k1) __attribute__((always_inline)) {
+            if (A.hitcount || A.trace) nfine += k1 - k0;
+            double2 tk[8];
+#pragma unroll
+            for (int kk = 0; kk < 8; ++kk)  // broadcast reads, all in flight together
+                tk[kk] = s_cand[wave][min(k0 + kk, k1 - 1) - sbase];
+            double tm = -__builtin_inf();
+#pragma unroll
+            for (int kk = 0; kk < 8; ++kk) {
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int q = 0; q < LB; ++q) {
+                        const double c = fmax(coh[r][q] - tk[kk].x, 0.0);
+                        const double t = (tk[kk].y - B[r][q]) * aiy_ipow(c, NP);
+                        const int lin = (l0 + q) + Nl * (k0 + kk);
+                        tm = (lin == idx[r]) ? tm : fmax(tm, t);
+                    }
+            }
+            if (!__any(tm >= kThr)) return;
+            stamp(2);
+            for (int kk = 0; kk < 8; ++kk) {
+                const int k = k0 + kk;
+                if (k >= k1) break;
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int q = 0; q < LB; ++q) {
+                        const double c = coh[r][q] - tk[kk].x;
+                        const int lin = (l0 + q) + Nl * k;
+                        if (lin != idx[r] && c > 0 &&
+                            (tk[kk].y - B[r][q]) * aiy_ipow(c, NP) >= kThr) {
+                            ++nhits;
+                            const double val =
+                                bell_val<NP, LAB>(c, s_ev[wave][k - sbase], A.sigma, dis[q]);
+                            if (lexi_take(val, lin, best[r], idx[r])) {
+#pragma unroll
+                                for (int q2 = 0; q2 < LB; ++q2)
+                                    if (B[r][q2] == B[r][q2])
+                                        B[r][q2] = screen_B(best[r], idx[r], dis[q2], NP);
+                            }
+                        }
+                    }
+            }
+            stamp(3);
+        };
+        // one superblock, blocks b with b % bstep == bsel: one round trip for the 64 sub-block
+        // bounds, then all bound tests (v_readlane, no memory), then ONE round trip staging the
+        // candidates of every passing block in LDS
+        auto superblock = [&](int sb, int bsel, int bstep) __attribute__((always_inline)) {
+            stamp(0);
+            const int sbase = sb << 9;  // first candidate of the superblock
+            const int sub = (sbase >> 3) + lane;
+            const bool oku = sub < A.nb8;
+            const double dm8 = oku ? A.Dm8[(size_t)i * A.nb8 + sub] : -__builtin_inf();
+            const double a8 = oku ? a[sub << 3] : 0.0;
+            double dm64 = dm8;
+            dm64 = fmax(dm64, __shfl_xor(dm64, 1));
+            dm64 = fmax(dm64, __shfl_xor(dm64, 2));
+            dm64 = fmax(dm64, __shfl_xor(dm64, 4));
+            unsigned long long pass = 0;  // bit 8b+u: sub-block u of block b passes
+            for (int b = bsel; b < 8; b += bstep) {
+                const int bbase = sbase + (b << 6);
+                if (bbase >= kg) break;
+                ++nblk;
+                if (!bound_pass(readlane_d(dm64, 8 * b), readlane_d(a8, 8 * b))) continue;
+                for (int u = 0; u < 8; ++u) {
+                    if (bbase + (u << 3) >= kg) break;
+                    ++nblk;
+                    if (bound_pass(readlane_d(dm8, 8 * b + u), readlane_d(a8, 8 * b + u)))
+                        pass |= 1ull << (8 * b + u);
+                }
+            }
+            if (!pass) {
+                stamp(1);
+                return;
+            }
+#pragma unroll
+            for (int b = 0; b < 8; ++b)  // all loads issued before any is used
+                if ((pass >> (8 * b)) & 0xffull) {
+                    const int k = min(sbase + (b << 6) + lane, Na - 1);
+                    s_cand[wave][(b << 6) + lane] = make_double2(a[k], Drow[k]);
+                    s_ev[wave][(b << 6) + lane] = ev[k];
+                }
+            __builtin_amdgcn_wave_barrier();  // a wave reads only its own slice
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            stamp(1);
+            for (int b = 0; b < 8; ++b) {
+                const unsigned pb = (unsigned)(pass >> (8 * b)) & 0xffu;
+                if (!pb) continue;
+                const int bbase = sbase + (b << 6);
+                for (int u = 0; u < 8; ++u)
+                    if (pb & (1u << u)) {
+                        const int k0 = bbase + (u << 3);
+                        fine(sbase, k0, min(k0 + 8, kg));
+                    }
+            }
+            stamp(2);
+            __builtin_amdgcn_wave_barrier();  // reads done before the next superblock's writes
+        };
+
+        const int nsb = (kg + 511) >> 9;
+        // best first: the superblock holding the tile's current argmax, its blocks split over
+        // the waves; then one exchange gives every wave the same near-optimal bar
+        int sfirst = -1;
+        {
+            int hk = -1;
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (idx[r] >= 0) hk = idx[r] / Nl;
+            const unsigned long long m = __ballot(hk >= 0);
+            if (m) sfirst = min(readlane_i(hk, __builtin_ctzll(m)) >> 9, nsb - 1);
+        }
+        if (sfirst >= 0) {  // (its bound would pass: it holds the bar's candidate)
+            ++nsup;
+            superblock(sfirst, wave, W);
+            exchange();
+            set_B();
+        }
+        for (int g = 0; g < nsb; g += 64) {
+            const int sbl = g + lane;
+            const bool oks = sbl < nsb;
+            const double dm0 = oks ? A.Dm512[(size_t)i * A.nb512 + sbl] : -__builtin_inf();
+            const double a0 = oks ? a[sbl << 9] : 0.0;
+            const int ns = min(64, nsb - g);
+            for (int sq = 0; sq < ns; ++sq) {
+                if (g + sq == sfirst || (g + sq) % W != wave) continue;
+                ++nsup;
+                if (!bound_pass(readlane_d(dm0, sq), readlane_d(a0, sq))) continue;
+                superblock(g + sq, 0, 1);
+            }
+        }
+    }
+    exchange();
+
+    // final outputs, wave 0 (the merge kernel's rules: Aiyagari_VFI.m:79-81,
+    // Labor_VFI.m:85,106-109)
+    bool okd = false;
+    double dmax = 0.0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (!okr[r] || wave != 0) continue;
+        const size_t t = (size_t)i * Na + jbase + r * 64 + lane;
+        double b = best[r];
+        int q = idx[r];
+        const double vo = A.v_old[t];
+        if (!feas[r] && LAB) {
+            b = A.keep_incoming ? A.v_new[t] : vo;
+        } else {
+            if (q < 0) {  // all candidates NaN: max returns NaN at index 1
+                q = 0;
+                b = __builtin_nan("");
+            }
+            const int l = q % Nl, k = q / Nl;
+            const double kp = a[k];
+            A.idx[t] = q;
+            if (A.pk) A.pk[t] = kp;
+            if (A.pc) A.pc[t] = cash<LAB>(x[r], y, LAB ? A.L[l] : 1.0) - kp;
+            if (LAB && A.pl) A.pl[t] = A.L[l];
+        }
+        A.v_new[t] = b;
+        const double d = fabs(b - vo);
+        if (d == d) {
+            dmax = okd ? fmax(dmax, d) : d;
+            okd = true;
+        }
+    }
+    block_max_to_slots(okd, dmax, A.diff);
+    if (A.trace) {  // instrumentation (aiy_ws_set_timing bit 2): per-wave sums into wave 0
+        __shared__ unsigned s_cnt[W][4];
+        if (lane == 0) {
+            s_cnt[wave][0] = nsup; s_cnt[wave][1] = nblk; s_cnt[wave][2] = nfine; s_cnt[wave][3] = nhits;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            long long* tr = A.trace + 16 * (size_t)item;
+            tr[0] = t_start;
+            tr[1] = (long long)wall_clock64();
+            tr[2] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));  // HW_REG_XCC_ID
+            for (int c = 0; c < 4; ++c) {
+                long long sum = 0;
+                for (int v = 0; v < W; ++v) sum += s_cnt[v][c];
+                tr[3 + c] = sum;
+            }
+            tr[7] = blockIdx.x;
+            for (int c = 0; c < 4; ++c) tr[8 + c] = cyc[c];
+        }
+    }
+    if (A.hitcount) {  // instrumentation (aiy_ws_set_timing bit 1)
+        unsigned long long* hc = A.hitcount + 4 * (blockIdx.x % kDiffSlots);
+        if (nhits) atomicAdd(hc, (unsigned long long)nhits);
+        if (lane == 0) {
+            const unsigned long long ns = 64ull * R * LB;
+            atomicAdd(hc + 1, nsup * ns);
+            atomicAdd(hc + 2, nblk * ns);
+            if (nfine) atomicAdd(hc + 3, nfine * ns);
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------ 4. merge
@@ -449,7 +924,8 @@ __global__ void bell_merge_kernel(BellArgs A, int use_partial, int nlb, int nchu
         double y = A.w * A.s[i];
         double best = A.best0[t];
         int idx = A.idx0[t];
-        if (use_partial && idx != -2) {
+        if (use_partial && A.touched[t]) {
+            A.touched[t] = 0;
             const double* __restrict__ ev = A.EV + (size_t)i * Na;
             for (int lbk = 0; lbk < nlb; ++lbk) {
                 int kfm = 0;
@@ -457,8 +933,10 @@ __global__ void bell_merge_kernel(BellArgs A, int use_partial, int nlb, int nchu
                     kfm = max(kfm, A.kf[(size_t)l * N * Na + t]);
                 int nch = (kfm + A.CK - 1) / A.CK;
                 for (int c = 0; c < nch; ++c) {
-                    int q = A.partial[(((size_t)lbk * nchunk + c) * N + i) * Na + j];
+                    int* pq = A.partial + (((size_t)lbk * nchunk + c) * N + i) * Na + j;
+                    int q = *pq;
                     if (q >= 0) {
+                        *pq = -1;
                         int l = q % Nl, k = q / Nl;
                         double coh = cash<LAB>(x, y, LAB ? A.L[l] : 1.0);
                         lexi_take(bell_val<NP, LAB>(coh - a[k], ev[k], A.sigma,
@@ -521,10 +999,13 @@ __global__ void bell_plain_kernel(BellArgs A) {
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 int launch_bell_table(const BellArgs& A, hipStream_t st) {
-    int n = A.N * A.Na;
-    bell_table_kernel<<<cdiv(n, 256), 256, 0, st>>>(A.N, A.Na, A.P, A.v_old, A.beta, A.np, A.a,
-                                                    A.EV, A.np > 0 ? A.T : nullptr,
-                                                    A.np > 0 ? A.T32 : nullptr, A.CK);
+    static_assert(2 * kDiffSlots <= kTableBlock, "table block clears the diff slots");
+    dim3 grid(cdiv(A.Na, kTableBlock), A.N);
+    const bool scr = A.np > 0;
+    bell_table_kernel<<<grid, kTableBlock, 0, st>>>(
+        A.N, A.Na, A.P, A.v_old, A.beta, A.np, A.a, A.EV, scr ? A.T : nullptr,
+        scr ? A.T32 : nullptr, A.CK, scr ? A.Dm : nullptr, scr ? A.Dm8 : nullptr,
+        scr ? A.Dm512 : nullptr, A.nb, A.nb8, A.nb512, A.diff, scr ? A.Dt : nullptr);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }
@@ -573,6 +1054,34 @@ static void run_screen(const BellArgs& A, hipStream_t st) {
         }
     }
 }
+template <int NP, bool LAB, int R, int W>
+static void tree_geo(const BellArgs& A, hipStream_t st) {
+    constexpr int LB = LAB ? 5 : 1;
+    const int ntile = cdiv(A.Na, 64 * R);
+    bell_tree_kernel<NP, LAB, R, LB, W><<<A.N * ntile, 64 * W, 0, st>>>(A, ntile);
+}
+// variant bit 0: 2 states per lane (A1 only); bits 1-2: waves per tile 1 (default), 2, 4, 8
+template <int NP, bool LAB, int R>
+static void tree_w(const BellArgs& A, hipStream_t st) {
+    switch ((A.variant >> 1) & 3) {
+        case 1: tree_geo<NP, LAB, R, 2>(A, st); break;
+        case 2: tree_geo<NP, LAB, R, 4>(A, st); break;
+        case 3: tree_geo<NP, LAB, R, 8>(A, st); break;
+        default: tree_geo<NP, LAB, R, 1>(A, st); break;
+    }
+}
+template <int NP, bool LAB>
+static void run_tree(const BellArgs& A, hipStream_t st) {
+    if constexpr (NP > 0) {
+        // the tuning geometries are instantiated for the reference sigma = 5 (NP = 4) only
+        if constexpr (!LAB && NP == 4) {
+            if (A.variant & 1) tree_w<NP, LAB, 2>(A, st);
+            else tree_w<NP, LAB, 1>(A, st);
+        } else {
+            tree_geo<NP, LAB, 1, 1>(A, st);
+        }
+    }
+}
 template <int NP, bool LAB>
 static void run_plain(const BellArgs& A, hipStream_t st) {
     bell_plain_kernel<NP, LAB><<<cdiv(A.N * A.Na, 128), 128, 0, st>>>(A);
@@ -607,6 +1116,8 @@ struct InitF { static void go(const BellArgs& A, hipStream_t st) { run_init<NP, 
 template <int NP, bool LAB>
 struct ScreenF { static void go(const BellArgs& A, hipStream_t st) { run_screen<NP, LAB>(A, st); } };
 template <int NP, bool LAB>
+struct TreeF { static void go(const BellArgs& A, hipStream_t st) { run_tree<NP, LAB>(A, st); } };
+template <int NP, bool LAB>
 struct PlainF { static void go(const BellArgs& A, hipStream_t st) { run_plain<NP, LAB>(A, st); } };
 template <int NP, bool LAB>
 struct MergeF {
@@ -617,6 +1128,10 @@ int launch_bell_init(const BellArgs& A, hipStream_t st) { return dispatch<InitF>
 int launch_bell_screen(const BellArgs& A, hipStream_t st) {
     if (A.np < 1 || A.np > 8) return fail(AIY_BAD_ARG, "screened sweep needs integer sigma in [2, 9]");
     return dispatch<ScreenF>(A.np, A.labor, A, st);
+}
+int launch_bell_tree(const BellArgs& A, hipStream_t st) {
+    if (A.np < 1 || A.np > 8) return fail(AIY_BAD_ARG, "screened sweep needs integer sigma in [2, 9]");
+    return dispatch<TreeF>(A.np, A.labor, A, st);
 }
 int launch_bell_plain(const BellArgs& A, hipStream_t st) { return dispatch<PlainF>(A.np, A.labor, A, st); }
 int launch_bell_merge(const BellArgs& A, int use_partial, hipStream_t st) {

@@ -57,15 +57,24 @@ int ws_ensure_bell(aiy_ws* ws, size_t partial_slots) {
     AIY_TRY(dalloc(&ws->EV, n));
     AIY_TRY(dalloc(&ws->T, n));
     AIY_TRY(dalloc(&ws->T32, 2 * (size_t)ws->N * (ws->Na + (ws->Na & 1))));
+    AIY_TRY(dalloc(&ws->Dm, (size_t)ws->N * ((ws->Na + 63) / 64)));
+    AIY_TRY(dalloc(&ws->Dm8, (size_t)ws->N * ((ws->Na + 7) / 8)));
+    AIY_TRY(dalloc(&ws->Dt, n));
+    AIY_TRY(dalloc(&ws->Dm512, (size_t)ws->N * ((ws->Na + 511) / 512)));
     AIY_TRY(dalloc(&ws->best0, n));
     AIY_TRY(dalloc(&ws->idx0, n));
+    if (!ws->touched) {  // the merge kernel leaves touched = 0 and partial = -1 behind
+        AIY_TRY(dalloc(&ws->touched, n));
+        AIY_HIP(hipMemset(ws->touched, 0, n * sizeof(int)));
+    }
     if (ws->partial && ws->partial_cap < partial_slots) dfree(ws->partial);
     if (!ws->partial) {
         AIY_TRY(dalloc(&ws->partial, partial_slots));
+        AIY_HIP(hipMemset(ws->partial, 0xff, partial_slots * sizeof(int)));
         ws->partial_cap = partial_slots;
     }
     AIY_TRY(dalloc(&ws->diff, 2 * kDiffSlots));
-    AIY_TRY(dalloc(&ws->hitcount, 1));
+    AIY_TRY(dalloc(&ws->hitcount, 4 * kDiffSlots));
     AIY_TRY(dalloc(&ws->dis, (size_t)std::max<int64_t>(ws->Nl, 1)));
     if (!ws->hdiff)
         AIY_HIP(hipHostMalloc((void**)&ws->hdiff, (2 * kDiffSlots + 4) * sizeof(unsigned long long)));
@@ -132,11 +141,30 @@ int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
     A.dis = c.labor ? ws->dis : nullptr;
     A.EV = ws->EV;
     A.T = ws->T;
-    A.T32 = (ws->variant & 4) ? nullptr : ws->T32;
+    A.tree = (ws->variant & 8) == 0;
+    A.T32 = (A.tree || (ws->variant & 4)) ? nullptr : ws->T32;
+    A.Dm = A.tree ? nullptr : ws->Dm;
+    A.Dm8 = A.tree ? ws->Dm8 : nullptr;
+    A.Dt = A.tree ? ws->Dt : nullptr;
+    A.Dm512 = A.tree ? ws->Dm512 : nullptr;
+    A.nb = (int)((ws->Na + 63) / 64);
+    A.nb8 = (int)((ws->Na + 7) / 8);
+    A.nb512 = (int)((ws->Na + 511) / 512);
     A.best0 = ws->best0;
     A.idx0 = ws->idx0;
     A.partial = ws->partial;
+    A.touched = ws->touched;
     A.hitcount = ws->count_hits ? ws->hitcount : nullptr;
+    A.trace = nullptr;
+    if (ws->tracing) {
+        const int64_t cap = (int64_t)ws->N * ((ws->Na + 63) / 64);
+        if (ws->trace_cap < cap) {
+            dfree(ws->trace);
+            AIY_TRY(dalloc(&ws->trace, 16 * (size_t)cap));
+            ws->trace_cap = cap;
+        }
+        A.trace = ws->trace;
+    }
     A.v_new = c.v_new;
     A.idx = c.idx;
     A.pk = c.pk;
@@ -164,15 +192,23 @@ int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
         ws->kf_r = c.r; ws->kf_w = c.w; ws->kf_a = c.a; ws->kf_s = c.s; ws->kf_L = A.L;
         ws->kf_Nl = A.Nl; ws->kf_lab = A.labor;
     }
-    AIY_HIP(hipMemsetAsync(ws->diff, 0, 2 * kDiffSlots * sizeof(unsigned long long), st));
-    AIY_TRY(launch_bell_table(A, st));
+    AIY_TRY(launch_bell_table(A, st));  // also clears the diff slots
     if (!screened) A.coarse = 0, A.hint = nullptr;
-    AIY_TRY(launch_bell_init(A, st));
-    AIY_TRY(ws_timing_begin(ws, st));
-    if (screened) AIY_TRY(launch_bell_screen(A, st));
-    else AIY_TRY(launch_bell_plain(A, st));
-    AIY_TRY(ws_timing_end(ws, st));
-    AIY_TRY(launch_bell_merge(A, screened ? 1 : 0, st));
+    if (screened && A.tree) {
+        // tree screen: the hint (or, cold, the init kernel's candidate) sets the first bar;
+        // the tree kernel writes the outputs itself
+        if (!A.hint) AIY_TRY(launch_bell_init(A, st));
+        AIY_TRY(ws_timing_begin(ws, st));
+        AIY_TRY(launch_bell_tree(A, st));
+        AIY_TRY(ws_timing_end(ws, st));
+    } else {
+        AIY_TRY(launch_bell_init(A, st));
+        AIY_TRY(ws_timing_begin(ws, st));
+        if (screened) AIY_TRY(launch_bell_screen(A, st));
+        else AIY_TRY(launch_bell_plain(A, st));
+        AIY_TRY(ws_timing_end(ws, st));
+        AIY_TRY(launch_bell_merge(A, screened ? 1 : 0, st));
+    }
     if (c.diff_out) AIY_TRY(launch_reduce_slots(ws->diff, c.diff_out, st));
     return AIY_OK;
 }
@@ -270,11 +306,12 @@ int aiy_ws_destroy(aiy_ws* ws) {
 int aiy_ws_set_timing(aiy_ws* ws, int enable) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
     AIY_TRY(ws_timing_drain(ws));
-    ws->timing = enable != 0;
-    ws->count_hits = enable != 0;
+    ws->timing = (enable & 1) != 0;
+    ws->count_hits = (enable & 2) != 0;
+    ws->tracing = (enable & 4) != 0;
     ws->tot_ms = 0;
     ws->launches = 0;
-    if (ws->hitcount) AIY_HIP(hipMemset(ws->hitcount, 0, sizeof(unsigned long long)));
+    if (ws->hitcount) AIY_HIP(hipMemset(ws->hitcount, 0, 4 * kDiffSlots * sizeof(unsigned long long)));
     return AIY_OK;
 }
 
@@ -284,11 +321,34 @@ int aiy_ws_timing(aiy_ws* ws, double* total_ms, int64_t* launches, int64_t* hits
     if (total_ms) *total_ms = ws->tot_ms;
     if (launches) *launches = ws->launches;
     if (hits) {
-        unsigned long long h = 0;
-        if (ws->hitcount)
-            AIY_HIP(hipMemcpy(&h, ws->hitcount, sizeof h, hipMemcpyDeviceToHost));
-        *hits = (int64_t)h;
+        int64_t c[4];
+        AIY_TRY(aiy_ws_counters(ws, c));
+        *hits = c[0];
     }
+    return AIY_OK;
+}
+
+int aiy_ws_counters(aiy_ws* ws, int64_t out[4]) {
+    if (!ws || !out) return fail(AIY_BAD_ARG, "NULL workspace/out");
+    std::vector<unsigned long long> h(4 * kDiffSlots, 0ull);
+    if (ws->hitcount)
+        AIY_HIP(hipMemcpy(h.data(), ws->hitcount, h.size() * sizeof(unsigned long long),
+                          hipMemcpyDeviceToHost));
+    for (int q = 0; q < 4; ++q) {
+        unsigned long long t = 0;
+        for (int sl = 0; sl < kDiffSlots; ++sl) t += h[4 * sl + q];
+        out[q] = (int64_t)t;
+    }
+    return AIY_OK;
+}
+
+int aiy_ws_trace(aiy_ws* ws, int64_t* out, int64_t cap, int64_t* n) {
+    if (!ws || !out || !n) return fail(AIY_BAD_ARG, "NULL argument");
+    *n = 0;
+    if (!ws->trace) return AIY_OK;
+    int64_t m = std::min(cap, ws->trace_cap);
+    AIY_HIP(hipMemcpy(out, ws->trace, 16 * (size_t)m * sizeof(int64_t), hipMemcpyDeviceToHost));
+    *n = m;
     return AIY_OK;
 }
 
@@ -300,15 +360,15 @@ int aiy_ws_invalidate(aiy_ws* ws) {
 
 int aiy_ws_set_variant(aiy_ws* ws, int variant) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
-    if (variant < 0 || variant > 7) return fail(AIY_BAD_ARG, "variant in [0, 7]");
+    if (variant < 0 || variant > 31) return fail(AIY_BAD_ARG, "variant in [0, 31]");
     ws->variant = variant;
     return AIY_OK;
 }
 
 int aiy_ws_set_search(aiy_ws* ws, int coarse_stride, int k_chunk) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
-    if (coarse_stride < 0 || k_chunk < 64 || k_chunk % 8)
-        return fail(AIY_BAD_ARG, "coarse_stride >= 0, k_chunk >= 64 and a multiple of 8");
+    if (coarse_stride < 0 || k_chunk < 64 || k_chunk % 64)
+        return fail(AIY_BAD_ARG, "coarse_stride >= 0, k_chunk >= 64 and a multiple of 64");
     if (coarse_stride) ws->coarse = coarse_stride;
     if (k_chunk != ws->CK) {
         ws->CK = k_chunk;

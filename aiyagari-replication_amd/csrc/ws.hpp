@@ -18,8 +18,13 @@ struct aiy_ws {
     double* EV = nullptr;
     double2* T = nullptr;
     float* T32 = nullptr;
+    double* Dm = nullptr;
+    double* Dm8 = nullptr;
+    double* Dt = nullptr;
+    double* Dm512 = nullptr;
     double* best0 = nullptr;
     int* idx0 = nullptr;
+    int* touched = nullptr;
     double* dis = nullptr;
     int* kf = nullptr;
     size_t kf_cap = 0;
@@ -34,7 +39,10 @@ struct aiy_ws {
     int* partial = nullptr;
     size_t partial_cap = 0;
     unsigned long long* diff = nullptr;      // device [2*kDiffSlots] {max bits, any}
-    unsigned long long* hitcount = nullptr;  // device [1]
+    unsigned long long* hitcount = nullptr;  // device [4 * kDiffSlots]
+    long long* trace = nullptr;              // device [8 * trace_cap] (instrumentation)
+    int64_t trace_cap = 0;
+    bool tracing = false;
     unsigned long long* hdiff = nullptr;     // pinned host [2*kDiffSlots + 4]
     // histogram scratch (A10)
     int* d_key = nullptr;
@@ -55,14 +63,14 @@ struct aiy_ws {
     int64_t launches = 0;
 
     void free_all() {
-        void* ps[] = {EV, T, T32, best0, idx0, dis, kf, partial, diff, hitcount, g0, g1, g2, gi,
+        void* ps[] = {EV, T, T32, Dm, Dm8, Dt, Dm512, touched, best0, idx0, dis, kf, partial, diff, hitcount, trace, g0, g1, g2, gi,
                       d_key, d_head, d_wr, d_mass, d_part};
         for (void* p : ps)
             if (p) (void)hipFree(p);
         if (hdiff) (void)hipHostFree(hdiff);
-        EV = nullptr; T = nullptr; T32 = nullptr; best0 = nullptr; dis = nullptr; kf = nullptr; kf_cap = 0;
+        EV = nullptr; T = nullptr; T32 = nullptr; Dm = nullptr; Dm8 = nullptr; Dt = nullptr; Dm512 = nullptr; touched = nullptr; best0 = nullptr; dis = nullptr; kf = nullptr; kf_cap = 0;
         kf_ok = false;
-        idx0 = nullptr; partial = nullptr; diff = nullptr; hitcount = nullptr; hdiff = nullptr;
+        idx0 = nullptr; partial = nullptr; diff = nullptr; hitcount = nullptr; trace = nullptr; trace_cap = 0; hdiff = nullptr;
         g0 = g1 = g2 = nullptr; gi = nullptr;
         d_key = d_head = nullptr; d_wr = d_mass = d_part = nullptr;
         partial_cap = 0;

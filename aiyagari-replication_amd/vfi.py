@@ -72,20 +72,40 @@ class Workspace:
     def handle(self):
         return self._h
 
-    def set_timing(self, on: bool):
-        check(lib().aiy_ws_set_timing(self._h, ip(1 if on else 0)))
+    def set_timing(self, on: bool, count: bool = False, trace: bool = False):
+        """on: HIP-event timing of the dominant kernel; count: work counters (slows it);
+        trace: per-work-item records of the tree sweep (see trace())."""
+        check(lib().aiy_ws_set_timing(self._h, ip((1 if on else 0) | (2 if count else 0)
+                                                  | (4 if trace else 0))))
+
+    def trace(self):
+        """Records of the last tree sweep: int64 array (items, 16) = start, end (100 MHz clock),
+        XCD id, superblock tests, block tests, candidates, exact evaluations, block id, then
+        wave-0 shader cycles in startup+superblock tests, block tests, fine screens, exact."""
+        cap = self.N * ((self.Na + 63) // 64)
+        out = np.zeros((cap, 16), np.int64)
+        n = C.c_int64(0)
+        check(lib().aiy_ws_trace(self._h, out.ctypes.data_as(C.c_void_p), i64(cap), C.byref(n)))
+        return out[:n.value]
 
     def timing(self):
         ms, n, hits = C.c_double(0), C.c_int64(0), C.c_int64(0)
         check(lib().aiy_ws_timing(self._h, C.byref(ms), C.byref(n), C.byref(hits)))
         return ms.value, n.value, hits.value
 
+    def counters(self):
+        """Per-state work counters of the screened sweep since set_timing(count=True):
+        (exact evaluations, superblock tests, block tests, candidates screened)."""
+        out = (C.c_int64 * 4)()
+        check(lib().aiy_ws_counters(self._h, out))
+        return tuple(int(x) for x in out)
+
     def invalidate(self):
         """Drop the cached feasibility table (after overwriting a_grid/s/L in place)."""
         check(lib().aiy_ws_invalidate(self._h))
 
     def set_variant(self, variant: int):
-        """Screen-kernel geometry (tuning; results identical): 0 R=2, 1 R=4, 2/3 capped regs."""
+        """Screen-kernel geometry (tuning; results identical), see aiy_ws_set_variant."""
         check(lib().aiy_ws_set_variant(self._h, ip(variant)))
 
     def set_search(self, coarse_stride=0, k_chunk=1024):

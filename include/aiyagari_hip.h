@@ -144,19 +144,34 @@ int ks_vfi_solve(double* value, double* k_opt, const double* k_grid, const doubl
 typedef struct aiy_ws aiy_ws;
 int aiy_ws_create(int64_t N, int64_t Na, int64_t Nl, aiy_ws** ws);
 int aiy_ws_destroy(aiy_ws* ws);
-/* kernel timing: when enabled, HIP events bracket the dominant kernel of every call on its
- * stream; aiy_ws_timing reads the accumulated milliseconds and launch count. */
+/* instrumentation.  enable bit 0: HIP events bracket the dominant kernel of every call on its
+ * stream (aiy_ws_timing reads the accumulated milliseconds and launch count); bit 1: the
+ * screened sweep counts its work (aiy_ws_counters; atomics, so never together with timing
+ * when the time matters). */
 int aiy_ws_set_timing(aiy_ws* ws, int enable);
 int aiy_ws_timing(aiy_ws* ws, double* total_ms, int64_t* launches, int64_t* hits);
+/* work counters of the screened Bellman sweep since aiy_ws_set_timing(ws, 2): out[0] exact
+ * candidate evaluations, out[1] superblock (512-candidate) tests, out[2] block (64) tests,
+ * out[3] candidates screened individually — each counted per state.  Instrumentation only. */
+int aiy_ws_counters(aiy_ws* ws, int64_t out[4]);
+/* per-work-item trace of the last tree sweep (aiy_ws_set_timing bit 2): 16 int64 per item
+ * {start clock, end clock (100 MHz wall clock), XCD id, superblock tests, block tests,
+ * candidates, exact evaluations, hardware block id, wave-0 shader cycles in: startup and
+ * superblock tests, superblock bound tests, fine screens, exact paths; 4 reserved}.
+ * Instrumentation only. */
+int aiy_ws_trace(aiy_ws* ws, int64_t* out, int64_t cap, int64_t* n);
 /* The workspace caches the feasible prefixes #{k : a_k < cash(j, l)}, which depend on
  * (r, w, a_grid, s, labor_choice) only, keyed by r, w and the pointers.  Call this after
  * overwriting a_grid / s / labor_choice in place. */
 int aiy_ws_invalidate(aiy_ws* ws);
-/* search knobs (defaults tuned for gfx950): coarse stride for cold starts, k-chunk. */
+/* search knobs (defaults tuned for gfx950): coarse stride for cold starts, k-chunk (a multiple
+ * of 64: candidates a' per screen work item). */
 int aiy_ws_set_search(aiy_ws* ws, int coarse_stride, int k_chunk);
-/* screen-kernel shape (tuning only; results are identical): bit 0 = 4 states per lane (else 2),
- * bit 1 = registers capped for 8 waves per SIMD, bit 2 = fp64-only screen (else the packed
- * fp32 pre-screen with directed-rounding bounds runs first).  Default 0. */
+/* screen-kernel shape (tuning only; results are identical).  bit 3 clear (default): the bound
+ * tree screen, bit 0 = 2 states per lane (else 1), bits 1-2 = 1, 2, 4 or 8 cooperating waves
+ * per tile, bit 4 = XCD-aware tile order.  bit 3 set: the chunked screen + merge, with
+ * bit 0 = 4 states per lane (else 2), bit 1 = registers capped for 8 waves per SIMD, bit 2 =
+ * fp64-only screen (else the packed fp32 pre-screen with directed-rounding bounds first). */
 int aiy_ws_set_variant(aiy_ws* ws, int variant);
 
 /* A1 on device.  hint (nullable, [N][Na] int32 0-based) = previous sweep's argmax; the result

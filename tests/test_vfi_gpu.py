@@ -56,7 +56,8 @@ def _device_sweep(pkg, torch, V, a, s, P, r, w, beta, sigma, mode, hint=None, ws
     return vn.cpu().numpy(), idx.cpu().numpy(), pk.cpu().numpy(), pc.cpu().numpy()
 
 
-@pytest.mark.parametrize("variant,k_chunk", [(0, 1024), (1, 512), (3, 256), (4, 1024), (5, 256)])
+@pytest.mark.parametrize("variant,k_chunk", [(0, 1024), (1, 1024), (2, 1024), (6, 1024), (16, 1024),
+                                             (8, 1024), (9, 512), (11, 256), (12, 1024), (13, 256)])
 @pytest.mark.parametrize("Na,shocks", [(1500, "rouwenhorst"), (777, "tauchen")])
 def test_screened_equals_plain_and_oracle(pkg, gpu, Na, shocks, variant, k_chunk):
     import torch
@@ -141,7 +142,7 @@ def test_full_size_bitwise_vs_oracle(pkg, gpu):
     assert (pcs > 0).all()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 6, 8, 12])
 def test_screen_stress_noisy_value(pkg, gpu, variant):
     """Rough value functions put many candidates within rounding distance of the running best
     (near-ties everywhere, multi-modal objectives): the fp32 pre-screen, the fp64 screen and
@@ -158,6 +159,6 @@ def test_screen_stress_noisy_value(pkg, gpu, variant):
         vo, io, pko, pco = corc.vfi_sweep(V, a, s, P, 0.03, w, 0.96, 5.0)
         for hint in (None, rng.integers(0, Na, (7, Na))):
             vs, is_, pks, pcs = _device_sweep(pkg, torch, V, a, s, P, 0.03, w, 0.96, 5.0,
-                                              mode=1, hint=hint, variant=variant, k_chunk=264)
+                                              mode=1, hint=hint, variant=variant, k_chunk=320)
             assert np.array_equal(vs, vo) and np.array_equal(is_, io), (Na, scale)
             assert np.array_equal(pks, pko) and np.array_equal(pcs, pco)

@@ -23,7 +23,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
            else step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread; fi ;;
     smoke) step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python -u bench.py ${BENCH_ARGS} ;;
-    prof)  step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/prof" -o run -- python3 "$PWD/bench.py" --no-cpu-baseline --no-ge ${BENCH_ARGS} ;;
+    prof)  step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/prof" -o run -- python3 "$PWD/bench.py" --no-cpu-baseline --no-ge --no-solve ${BENCH_ARGS} ;;
     pmc)   step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$PWD/$OUT/pmc_fetch" -o run -- python3 "$PWD/bench.py" --no-cpu-baseline --steps 3 --warmup 2
            step pmc_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$PWD/$OUT/pmc_write" -o run -- python3 "$PWD/bench.py" --no-cpu-baseline --steps 3 --warmup 2 ;;
     custom) step custom 600 bash -c "$CUSTOM" ;;
