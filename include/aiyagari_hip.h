@@ -137,6 +137,17 @@ int ks_vfi_solve(double* value, double* k_opt, const double* k_grid, const doubl
                  int64_t nK, int64_t howard_steps, double tol, int64_t max_vfi,
                  int n_devices, int64_t* iters, double* rel_diff);
 
+/* A8: the EGM policy iteration of Krusell_Smith_EGM.m:129-209 for the current B (replaces the
+ * `for egm_iter = 1:max_egm` loop, :130-209).  k_opt: k_size x K_size x 4, in/out (:96 start).
+ * Gauss-Seidel over (s_i outer, K_i inner) exactly as the script: each (s, K) column is
+ * overwritten as soon as it is computed (:199).  Stops when max|k_opt - k_opt_old| < tol
+ * (:204-207) or after max_iter sweeps; iters = sweeps run, diff = the last max change.
+ * AIY_NON_FINITE if some (s, K) pair has fewer than 2 EGM points inside [k_min, k_max]
+ * (MATLAB's griddedInterpolant would raise there). */
+int ks_egm_solve(double* k_opt, const double* k_grid, const double* K_grid, const double* B,
+                 const double* P, const double* params, int64_t nk, int64_t nK, double tol,
+                 int64_t max_iter, int64_t* iters, double* diff);
+
 /* ======================================================================================
  * Device tier: [N][Na] (z-major) arrays in HBM, async on `stream` (hipStream_t).
  * A workspace holds the per-shape scratch (EV/D tables, init/partial buffers, events).

@@ -631,3 +631,150 @@ int orc_ks_howard(const orc_ks_params* p, int64_t nk, int64_t nK, const double* 
     free(Vn);
     return 0;
 }
+
+/* ------------------------------------------------------------------ A8 (KS EGM) */
+/* Per (s_i, K_i) scalars, Krusell_Smith_EGM.m:101-112, :139-175 (libm pow/exp/log).
+ * s_grid = [Z(:), Eps(:)] of meshgrid(z_grid, eps_grid): s = (z1,e1), (z1,e2), (z2,e1), (z2,e2). */
+void orc_ks_egm_pairs(const orc_ks_params* p, int64_t nK, const double* K_grid, const double* B,
+                      orc_ks_egm_pair* out) {
+    const double* zg = p->z_grid;
+    const double* eg = p->eps_grid;
+    const double a = p->alpha, dl = p->delta, lb = p->l_bar;
+    for (int64_t s_i = 0; s_i < 4; ++s_i) {
+        double z = zg[s_i < 2 ? 0 : 1], e = eg[s_i % 2];
+        for (int64_t K_i = 0; K_i < nK; ++K_i) {
+            orc_ks_egm_pair* q = out + s_i * nK + K_i;
+            double K = K_grid[K_i];
+            double L = lb * (1 - p->ug * (double)(z == zg[0]) - p->ub * (double)(z == zg[1]));
+            double r = a * z * pow(K, a - 1) * pow(L, 1 - a);
+            double w = (1 - a) * z * pow(K, a) * pow(L, -a);
+            double Kp = (z == zg[0]) ? exp(B[0] + B[1] * log(K)) : exp(B[2] + B[3] * log(K));
+            for (int s_j = 0; s_j < 4; ++s_j) {
+                double zn = zg[s_j < 2 ? 0 : 1], en = eg[s_j % 2];
+                double Kd = (zn == zg[0]) ? exp(B[0] + B[1] * log(Kp)) : exp(B[2] + B[3] * log(Kp));
+                int64_t idx = 0;
+                double bd = fabs(K_grid[0] - Kd);
+                for (int64_t m = 1; m < nK; ++m) {
+                    double dd = fabs(K_grid[m] - Kd);
+                    if (dd < bd) { bd = dd; idx = m; }
+                }
+                double Ln = lb * (1 - p->ug * (double)(zn == zg[0]) - p->ub * (double)(zn == zg[1]));
+                double rn = a * zn * pow(Kd, a - 1) * pow(Ln, 1 - a);
+                double wn = (1 - a) * zn * pow(Kd, a) * pow(Ln, -a);
+                q->kd[s_j] = (int32_t)idx;
+                q->Rn[s_j] = (1 + rn) - dl;
+                q->Wn[s_j] = (wn * en) * lb;
+            }
+            q->R = (1 + r) - dl;
+            q->We = (w * e) * lb;
+        }
+    }
+}
+
+/* pchip slopes for n >= 2 (pchip.m: n == 2 is linear) */
+static void pchip_slopes_n(int64_t n, const double* x, const double* y, double* d) {
+    if (n == 2) {
+        d[0] = d[1] = (y[1] - y[0]) / (x[1] - x[0]);
+        return;
+    }
+    orc_pchip_slopes(n, x, y, d);
+}
+
+/* One Gauss-Seidel sweep (Krusell_Smith_EGM.m:133-200); k_opt k x K x S column-major. */
+int orc_ks_egm_sweep(const orc_ks_params* p, int64_t nk, int64_t nK, const double* k_grid,
+                     const orc_ks_egm_pair* pairs, const double* P, double* k_opt) {
+    double* d4 = (double*)malloc(sizeof(double) * 4 * nk);
+    double* kc = (double*)malloc(sizeof(double) * nk);
+    int64_t* ord = (int64_t*)malloc(sizeof(int64_t) * nk);
+    double* xs = (double*)malloc(sizeof(double) * nk);
+    double* ys = (double*)malloc(sizeof(double) * nk);
+    double* dd = (double*)malloc(sizeof(double) * nk);
+    int rc = 0;
+    for (int64_t s_i = 0; s_i < 4 && rc == 0; ++s_i)
+        for (int64_t K_i = 0; K_i < nK && rc == 0; ++K_i) {
+            const orc_ks_egm_pair* q = pairs + s_i * nK + K_i;
+            const double* col[4];
+            for (int s_j = 0; s_j < 4; ++s_j) {
+                col[s_j] = k_opt + ((int64_t)s_j * nK + q->kd[s_j]) * nk;
+                orc_pchip_slopes(nk, k_grid, col[s_j], d4 + s_j * nk);
+            }
+            for (int64_t t = 0; t < nk; ++t) {
+                double kp = k_grid[t], em = 0.0;
+                for (int s_j = 0; s_j < 4; ++s_j) {
+                    double kpn = orc_pchip_eval(nk, k_grid, col[s_j], d4 + s_j * nk, kp);
+                    double cn = (q->Rn[s_j] * kp + q->Wn[s_j]) - kpn;
+                    cn = fmax(cn, 1e-8); /* MATLAB max ignores NaN, as fmax */
+                    em = em + (P[s_i * 4 + s_j] * q->Rn[s_j]) / cn;
+                }
+                double c = 1 / (p->beta * em);
+                kc[t] = ((c + kp) - q->We) / q->R;
+            }
+            /* stable ascending sort, NaN last (MATLAB sort) */
+            for (int64_t t = 0; t < nk; ++t) ord[t] = t;
+            for (int64_t t = 1; t < nk; ++t) {
+                int64_t v = ord[t];
+                int64_t u = t;
+                while (u > 0) {
+                    double a0 = kc[ord[u - 1]], b0 = kc[v];
+                    int gt = (a0 != a0) ? (b0 == b0) : (b0 == b0 && a0 > b0);
+                    if (!gt) break;
+                    ord[u] = ord[u - 1];
+                    --u;
+                }
+                ord[u] = v;
+            }
+            int64_t nv = 0;
+            for (int64_t t = 0; t < nk; ++t) {
+                double x = kc[ord[t]];
+                if (x >= p->k_min && x <= p->k_max) {
+                    xs[nv] = x;
+                    ys[nv] = k_grid[ord[t]];
+                    ++nv;
+                }
+            }
+            if (nv < 2) {
+                rc = -2;
+                break;
+            }
+            pchip_slopes_n(nv, xs, ys, dd);
+            double* out = k_opt + (s_i * nK + K_i) * nk;
+            for (int64_t t = 0; t < nk; ++t) {
+                double kq = k_grid[t], v;
+                if (kq < xs[0]) v = ys[0];
+                else if (kq > xs[nv - 1]) v = ys[nv - 1];
+                else v = orc_pchip_eval(nv, xs, ys, dd, kq);
+                v = fmin(v, p->k_max);
+                out[t] = fmax(v, p->k_min);
+            }
+        }
+    free(d4); free(kc); free(ord); free(xs); free(ys); free(dd);
+    return rc;
+}
+
+int orc_ks_egm_solve(const orc_ks_params* p, int64_t nk, int64_t nK, const double* k_grid,
+                     const double* K_grid, const double* B, const double* P, double tol,
+                     int64_t max_iter, double* k_opt, int64_t* iters, double* diff) {
+    orc_ks_egm_pair* pairs = (orc_ks_egm_pair*)malloc(sizeof(orc_ks_egm_pair) * 4 * nK);
+    double* old = (double*)malloc(sizeof(double) * nk * nK * 4);
+    orc_ks_egm_pairs(p, nK, K_grid, B, pairs);
+    int rc = 0;
+    int64_t it;
+    double dmax = NAN;
+    for (it = 1; it <= max_iter; ++it) {
+        memcpy(old, k_opt, sizeof(double) * nk * nK * 4);
+        rc = orc_ks_egm_sweep(p, nk, nK, k_grid, pairs, P, k_opt);
+        if (rc) break;
+        dmax = NAN;
+        for (int64_t n = 0; n < nk * nK * 4; ++n) {
+            double d = fabs(k_opt[n] - old[n]);
+            if (d == d && !(dmax >= d)) dmax = d;
+        }
+        if (dmax < tol) break;
+    }
+    if (it > max_iter) it = max_iter;
+    *iters = it;
+    *diff = dmax;
+    free(pairs);
+    free(old);
+    return rc;
+}

@@ -111,6 +111,24 @@ int orc_ks_howard(const orc_ks_params* p, int64_t nk, int64_t nK, const double* 
                   const double* K_grid, double* V, const double* k_opt, const double* B,
                   const double* P, int64_t steps);
 
+/* A8 Krusell-Smith EGM (Krusell_Smith_EGM.m:101-112, :129-209).  P row-major [s_i*4 + s_j]
+ * (as orc_ks_*); k_opt k x K x S column-major, updated Gauss-Seidel in (s_i outer, K_i inner)
+ * order.  Returns 0, or -2 when an (s, K) pair has fewer than 2 valid EGM points. */
+typedef struct {
+    int32_t kd[4];  /* K''_idx per s_j */
+    double Rn[4];   /* (1 + r_next) - delta */
+    double Wn[4];   /* w_next * eps_next * l_bar */
+    double R;       /* (1 + r) - delta */
+    double We;      /* w * eps * l_bar */
+} orc_ks_egm_pair;
+void orc_ks_egm_pairs(const orc_ks_params* p, int64_t nK, const double* K_grid, const double* B,
+                      orc_ks_egm_pair* out);
+int orc_ks_egm_sweep(const orc_ks_params* p, int64_t nk, int64_t nK, const double* k_grid,
+                     const orc_ks_egm_pair* pairs, const double* P, double* k_opt);
+int orc_ks_egm_solve(const orc_ks_params* p, int64_t nk, int64_t nK, const double* k_grid,
+                     const double* K_grid, const double* B, const double* P, double tol,
+                     int64_t max_iter, double* k_opt, int64_t* iters, double* diff);
+
 #ifdef __cplusplus
 }
 #endif

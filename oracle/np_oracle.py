@@ -786,3 +786,119 @@ def ks_howard(p, k_grid, K_grid, V, k_opt, B, P, steps):
                                                    k_opt[k_i, K_i, s_i], k_i, K_i, s_i)
         V = Vn
     return V
+
+
+# ----------------------------------------------------------------------------------------
+# A8  Krusell-Smith EGM (Krusell_Smith_EGM.m:101-112, :129-209)
+# ----------------------------------------------------------------------------------------
+
+
+def ks_egm_pairs(p, K_grid, B):
+    """Per (s_i, K_i) scalars of the EGM step, in the script's operation order (libm
+    pow/exp/log via math.*).  s_grid = [Z(:), Eps(:)] of meshgrid(z_grid, eps_grid)
+    (:18-19): s = (z1,e1), (z1,e2), (z2,e1), (z2,e2).  Returns a list indexed s_i*nK + K_i of
+    dicts {kd: [K''_idx per s_j], Rn: [(1 + r_next) - delta], Wn: [w_next*eps_next*l_bar],
+    R: (1 + r) - delta, We: w*eps*l_bar}."""
+    zg, eg = p["z_grid"], p["eps_grid"]
+    a, dl, lb = p["alpha"], p["delta"], p["l_bar"]
+    s_grid = [(zg[0], eg[0]), (zg[0], eg[1]), (zg[1], eg[0]), (zg[1], eg[1])]
+
+    def labour(z):  # L = l_bar*(1 - ug*(z==z_grid(1)) - ub*(z==z_grid(2)))  (:108, :149)
+        return lb * (1 - p["ug"] * float(z == zg[0]) - p["ub"] * float(z == zg[1]))
+
+    def alm(z, K):  # :140-145 / :164-169 (no clamp, no floor in the EGM script)
+        if z == zg[0]:
+            return math.exp(B[0] + B[1] * math.log(K))
+        return math.exp(B[2] + B[3] * math.log(K))
+
+    out = []
+    nK = len(K_grid)
+    for s_i in range(4):
+        z, e = s_grid[s_i]
+        for K_i in range(nK):
+            K = float(K_grid[K_i])
+            L = labour(z)
+            r = a * z * math.pow(K, a - 1) * math.pow(L, 1 - a)          # r_table  (:110)
+            w = (1 - a) * z * math.pow(K, a) * math.pow(L, -a)          # w_table  (:109)
+            Kp = alm(z, K)
+            kd, Rn, Wn = [], [], []
+            for s_j in range(4):
+                zn, en = s_grid[s_j]
+                Kdp = alm(zn, Kp)
+                kd.append(int(np.argmin(np.abs(np.asarray(K_grid) - Kdp))))  # first on ties
+                Ln = labour(zn)
+                rn = a * zn * math.pow(Kdp, a - 1) * math.pow(Ln, 1 - a)   # :174
+                wn = (1 - a) * zn * math.pow(Kdp, a) * math.pow(Ln, -a)    # :175
+                Rn.append((1 + rn) - dl)
+                Wn.append((wn * en) * lb)
+            out.append(dict(kd=kd, Rn=Rn, Wn=Wn, R=(1 + r) - dl, We=(w * e) * lb))
+    return out
+
+
+def _pchip_slopes_n(x, y):
+    """pchip.m slopes for n >= 2 (n == 2: the secant, i.e. linear interpolation)."""
+    if len(x) == 2:
+        s = (y[1] - y[0]) / (x[1] - x[0])
+        return np.array([s, s])
+    return pchip_slopes(x, y)
+
+
+def ks_egm_sweep(p, k_grid, K_grid, B, P, k_opt, pairs=None):
+    """One Gauss-Seidel sweep of Krusell_Smith_EGM.m:133-200: k_opt(:,K_i,s_i) is overwritten
+    as soon as it is computed and read by later (s, K) pairs.  k_opt is [k, K, s] (modified in
+    place and returned)."""
+    nk, nK, _ = k_opt.shape
+    pairs = pairs or ks_egm_pairs(p, K_grid, B)
+    k_min, k_max, beta = p["k_min"], p["k_max"], p["beta"]
+    for s_i in range(4):
+        for K_i in range(nK):
+            q = pairs[s_i * nK + K_i]
+            cols = [k_opt[:, q["kd"][s_j], s_j].copy() for s_j in range(4)]
+            slopes = [pchip_slopes(k_grid, c) for c in cols]
+            kc = np.empty(nk)
+            for kp_i in range(nk):
+                kp = float(k_grid[kp_i])
+                em = 0.0
+                for s_j in range(4):
+                    kpn = pchip_eval(k_grid, cols[s_j], slopes[s_j], kp)        # :179
+                    c_next = (q["Rn"][s_j] * kp + q["Wn"][s_j]) - kpn            # :178, :180
+                    c_next = c_next if c_next > 1e-8 else 1e-8                   # :181 (NaN → 1e-8)
+                    em = em + (P[s_i, s_j] * q["Rn"][s_j]) / c_next              # :183
+                c = 1 / (beta * em)                                              # :187
+                kc[kp_i] = ((c + kp) - q["We"]) / q["R"]                         # :188
+            order = np.argsort(kc, kind="stable")                                 # :193 (NaN last)
+            xs, ys = kc[order], k_grid[order]
+            valid = (xs >= k_min) & (xs <= k_max)                                 # :195
+            xs, ys = xs[valid], ys[valid]
+            if len(xs) < 2:
+                raise ValueError("fewer than 2 valid EGM points (griddedInterpolant would fail)")
+            d = _pchip_slopes_n(xs, ys)
+            new = np.empty(nk)
+            for t in range(nk):                                                   # :196-197
+                kq = float(k_grid[t])
+                if kq < xs[0]:
+                    v = ys[0]                                                     # 'nearest'
+                elif kq > xs[-1]:
+                    v = ys[-1]
+                else:
+                    v = pchip_eval(xs, ys, d, kq)
+                v = k_max if not (v <= k_max) else v                              # min(v, k_max)
+                new[t] = k_min if not (v >= k_min) else v                         # max(., k_min)
+            k_opt[:, K_i, s_i] = new                                              # :199
+    return k_opt
+
+
+def ks_egm_solve(p, k_grid, K_grid, B, P, k_opt, tol=1e-6, max_iter=10000):
+    """Krusell_Smith_EGM.m:130-209 for one B: sweeps until max|Δk_opt| < tol."""
+    k_opt = np.array(k_opt, dtype=np.float64, copy=True)
+    pairs = ks_egm_pairs(p, K_grid, B)
+    diff = float("nan")
+    it = 0
+    for it in range(1, max_iter + 1):
+        old = k_opt.copy()
+        ks_egm_sweep(p, k_grid, K_grid, B, P, k_opt, pairs)
+        dd = np.abs(k_opt - old)
+        diff = float(np.nanmax(dd)) if not np.all(np.isnan(dd)) else float("nan")
+        if diff < tol:
+            break
+    return dict(k_opt=k_opt, iters=it, diff=diff)

@@ -102,7 +102,30 @@ def main():
          V_howard2=V2, beta=p["beta"], alpha=p["alpha"], delta=p["delta"], k_min=p["k_min"],
          k_max=p["k_max"], ug=p["ug"], ub=p["ub"], l_bar=p["l_bar"], mu=p["mu"])
     print(f"  KS done {time.time()-t0:.1f}s")
+    make_ks_egm()
+
+
+def make_ks_egm():
+    """A8: Krusell_Smith_EGM.m:129-209 at the reference defaults (k=100, K=4, S=4), from the
+    script's initial k_opt = 0.9*k_grid (:96): 1 and 3 Gauss-Seidel sweeps, and the full solve
+    to tol_egm = 1e-6 (numpy restatement, ~75 s)."""
+    t0 = time.time()
+    p, kg, Kg, Pk, _, B = no.ks_setup()
+    k0 = 0.9 * np.repeat(np.repeat(kg[:, None, None], len(Kg), 1), 4, 2)
+    s1 = no.ks_egm_solve(p, kg, Kg, B, Pk, k0, max_iter=1)
+    s3 = no.ks_egm_solve(p, kg, Kg, B, Pk, k0, max_iter=3)
+    full = no.ks_egm_solve(p, kg, Kg, B, Pk, k0, tol=1e-6, max_iter=10000)
+    save("ks_egm_defaults", k_grid=kg, K_grid=Kg, P=Pk, B=B, k_opt0=k0, k_opt1=s1["k_opt"],
+         k_opt3=s3["k_opt"], diff3=s3["diff"], k_opt_final=full["k_opt"], iters=full["iters"],
+         diff_final=full["diff"], beta=p["beta"], alpha=p["alpha"], delta=p["delta"],
+         k_min=p["k_min"], k_max=p["k_max"], ug=p["ug"], ub=p["ub"], l_bar=p["l_bar"],
+         mu=p["mu"])
+    print(f"  KS EGM done {time.time()-t0:.1f}s ({full['iters']} sweeps)")
 
 
 if __name__ == "__main__":
-    main()
+    import sys as _sys
+    if len(_sys.argv) > 1 and _sys.argv[1] == "ks_egm":
+        make_ks_egm()
+    else:
+        main()

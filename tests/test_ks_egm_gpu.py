@@ -1,0 +1,66 @@
+"""GPU parity for A8 (Krusell_Smith_EGM.m:129-209): the one-workgroup Gauss-Seidel EGM solve
+against the golden fixtures (numpy restatement) and the C restatement.  Every operation is
+the restatement's, in the same order (-ffp-contract=off), so results are bit-exact."""
+import numpy as np
+import pytest
+
+from oracle import corc
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(golden):
+    g = golden("ks_egm_defaults")
+    prm = np.array([g["beta"], g["alpha"], g["delta"], g["k_min"], g["k_max"], g["ug"], g["ub"],
+                    g["l_bar"], g["mu"], 1.01, 0.99, 1.0, 0.0])
+    return g, prm
+
+
+def _cparams(prm):
+    return corc.ks_params(beta=prm[0], alpha=prm[1], delta=prm[2], k_min=prm[3], k_max=prm[4],
+                          ug=prm[5], ub=prm[6], l_bar=prm[7], mu=prm[8], z_grid=(prm[9], prm[10]),
+                          eps_grid=(prm[11], prm[12]))
+
+
+def test_sweeps_match_golden(pkg, gpu, golden):
+    g, prm = _setup(golden)
+    args = (g["k_grid"], g["K_grid"], g["B"], g["P"], prm)
+    r1 = pkg.ks_egm_solve(g["k_opt0"], *args, max_iter=1)
+    assert r1["iters"] == 1 and np.array_equal(r1["k_opt"], g["k_opt1"])
+    r3 = pkg.ks_egm_solve(g["k_opt0"], *args, max_iter=3)
+    assert np.array_equal(r3["k_opt"], g["k_opt3"]) and r3["diff"] == float(g["diff3"])
+
+
+def test_solve_to_tol_matches_golden(pkg, gpu, golden):
+    g, prm = _setup(golden)
+    R = pkg.ks_egm_solve(g["k_opt0"], g["k_grid"], g["K_grid"], g["B"], g["P"], prm, tol=1e-6,
+                         max_iter=10000)
+    assert R["iters"] == int(g["iters"]) == 994
+    assert np.array_equal(R["k_opt"], g["k_opt_final"])
+    assert R["diff"] == float(g["diff_final"])
+
+
+@pytest.mark.parametrize("B,nK,nk", [((0.1, 0.97, 0.08, 0.975), 4, 100),
+                                     ((0.05, 0.985, 0.03, 0.99), 6, 60),
+                                     ((0.0, 1.0, 0.0, 1.0), 3, 150)])
+def test_other_alm_and_sizes_match_oracle(pkg, gpu, golden, B, nK, nk):
+    """Non-identity ALM (K''_idx != K_i, Gauss-Seidel reads of columns updated earlier in the
+    sweep) and other grid sizes, vs the C restatement, 40 sweeps."""
+    from oracle import np_oracle as no
+    g, prm = _setup(golden)
+    p, kg, Kg, P, _, _ = no.ks_setup(k_size=nk, K_size=nK)
+    B = np.array(B)
+    k0 = 0.9 * np.repeat(np.repeat(kg[:, None, None], nK, 1), 4, 2)
+    R = pkg.ks_egm_solve(k0, kg, Kg, B, P, prm, tol=1e-12, max_iter=40)
+    Ro = corc.ks_egm_solve(_cparams(prm), kg, Kg, B, P, k0, tol=1e-12, max_iter=40)
+    assert R["iters"] == Ro["iters"]
+    assert np.array_equal(R["k_opt"], Ro["k_opt"])
+    assert R["diff"] == Ro["diff"] or (np.isnan(R["diff"]) and np.isnan(Ro["diff"]))
+
+
+def test_bad_inputs(pkg, gpu, golden):
+    g, prm = _setup(golden)
+    with pytest.raises(pkg.AiyError):
+        pkg.ks_egm_solve(g["k_opt0"], g["k_grid"][::-1].copy(), g["K_grid"], g["B"], g["P"], prm)
+    with pytest.raises(pkg.AiyError):
+        pkg.ks_egm_solve(g["k_opt0"], g["k_grid"], -g["K_grid"], g["B"], g["P"], prm)

@@ -63,3 +63,14 @@ def test_ks_gateway(pkg, gpu, golden):
                          howard_steps=5, tol=1e-6, max_vfi=3)
     assert int(it[0, 0]) == R["iters"]
     assert np.array_equal(V.reshape(R["value"].shape, order="F"), R["value"])
+
+
+def test_ks_egm_gateway(pkg, gpu, golden):
+    """ks_egm_solve_mex (Krusell_Smith_EGM.m:129-209) returns the golden policy after 3 sweeps."""
+    g = golden("ks_egm_defaults")
+    prm = pkg.ks_params()
+    ko, it, diff = mexstub.call("ks_egm_solve_mex", 3, g["k_opt0"], g["k_grid"], g["K_grid"],
+                                g["B"], g["P"], prm, 1e-6, 3.0)
+    assert int(it[0, 0]) == 3
+    assert np.array_equal(ko.reshape(g["k_opt3"].shape, order="F"), g["k_opt3"])
+    assert float(diff[0, 0]) == float(g["diff3"])

@@ -112,3 +112,28 @@ def test_portable_log_close_to_libm():
     for x in xs:
         y = no.fdlibm_log(float(x))
         assert abs(y - math.log(x)) <= math.ulp(math.log(x))
+
+
+def _ks_cparams(g):
+    return corc.ks_params(beta=float(g["beta"]), alpha=float(g["alpha"]), delta=float(g["delta"]),
+                          k_min=float(g["k_min"]), k_max=float(g["k_max"]), ug=float(g["ug"]),
+                          ub=float(g["ub"]), l_bar=float(g["l_bar"]), mu=float(g["mu"]),
+                          z_grid=(1.01, 0.99), eps_grid=(1.0, 0.0))
+
+
+def test_ks_egm_bitwise(golden):
+    """A8 (Krusell_Smith_EGM.m:129-209): the C restatement equals the numpy restatement bit for
+    bit after 1 and 3 Gauss-Seidel sweeps and over the whole solve (994 sweeps to 1e-6)."""
+    g = golden("ks_egm_defaults")
+    p = _ks_cparams(g)
+    args = (p, g["k_grid"], g["K_grid"], g["B"], g["P"], g["k_opt0"])
+    r1 = corc.ks_egm_solve(*args, max_iter=1)
+    assert np.array_equal(r1["k_opt"], g["k_opt1"])
+    r3 = corc.ks_egm_solve(*args, max_iter=3)
+    assert np.array_equal(r3["k_opt"], g["k_opt3"]) and r3["diff"] == float(g["diff3"])
+    rf = corc.ks_egm_solve(*args, tol=1e-6, max_iter=10000)
+    assert rf["iters"] == int(g["iters"]) == 994
+    assert np.array_equal(rf["k_opt"], g["k_opt_final"]) and rf["diff"] == float(g["diff_final"])
+    # properties of the converged policy: inside [k_min, k_max], nondecreasing in k
+    assert (rf["k_opt"] >= float(g["k_min"])).all() and (rf["k_opt"] <= float(g["k_max"])).all()
+    assert (np.diff(rf["k_opt"], axis=0) >= 0).all()
