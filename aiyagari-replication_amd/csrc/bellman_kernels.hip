@@ -600,7 +600,6 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A, int ntile
     const double y = A.w * A.s[i];
     const int jbase = tile * (64 * R);
     __shared__ double2 s_cand[W][512];  // each wave's current superblock: (a_k, D_k)
-    __shared__ double s_ev[W][512];     // ... and EV_k for the exact values
     __shared__ double s_xb[W][64 * R];  // best exchange
     __shared__ int s_xi[W][64 * R];
 
@@ -697,28 +696,43 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A, int ntile
         };
         set_B();
 
-        auto bound_pass = [&](double dmax, double a0) __attribute__((always_inline)) {
-            double tm = -__builtin_inf();
+        // eight block bounds at once (independent dependency chains, so their latencies
+        // overlap): lanes l0 + stride*u of (dv, av) hold (Dmax, a at the block start); bit u
+        // of the result is set when some sub-state passes bound u (u < cnt)
+        auto mask8 = [&](double dv, double av, int l0, int stride, int cnt)
+                         __attribute__((always_inline)) {
+            double tmax[8];
 #pragma unroll
-            for (int r = 0; r < R; ++r)
+            for (int u = 0; u < 8; ++u) {
+                const int ln = min(l0 + stride * u, 63);
+                const double dmax = readlane_d(dv, ln), a0 = readlane_d(av, ln);
+                double tm = -__builtin_inf();
 #pragma unroll
-                for (int q = 0; q < LB; ++q)
-                    tm = fmax(tm, (dmax - B[r][q]) * aiy_ipow(fmax(coh[r][q] - a0, 0.0), NP));
-            return __any(tm >= kThr);
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int q = 0; q < LB; ++q)
+                        tm = fmax(tm, (dmax - B[r][q]) * aiy_ipow(fmax(coh[r][q] - a0, 0.0), NP));
+                tmax[u] = tm;
+            }
+            unsigned m = 0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) m |= (__any(tmax[u] >= kThr) ? 1u : 0u) << u;
+            return m & ((1u << cnt) - 1u);
         };
-        // candidates [k0, k1), k1 - k0 <= 8, of superblock sbase staged in LDS.  First the
-        // exact screen test on all of them without a branch (the current argmax itself is
-        // masked: its value is known); only when some lane passes, the branchy exact path:
-        // re-test, exact value in the literal MATLAB order, (max value, first index) merge
+        // candidates [k0, k1), k1 - k0 <= 8, of superblock sbase staged in LDS.  The exact
+        // screen test on all of them without a branch (the current argmax itself is masked:
+        // its value is known) gives one vote per candidate; only voted candidates take the
+        // exact path: re-test per lane, exact value in the literal MATLAB order, merge
         auto fine = [&](int sbase, int k0, int k1) __attribute__((always_inline)) {
             if (A.hitcount || A.trace) nfine += k1 - k0;
             double2 tk[8];
 #pragma unroll
             for (int kk = 0; kk < 8; ++kk)  // broadcast reads, all in flight together
                 tk[kk] = s_cand[wave][min(k0 + kk, k1 - 1) - sbase];
-            double tm = -__builtin_inf();
+            double tmax[8];
 #pragma unroll
             for (int kk = 0; kk < 8; ++kk) {
+                double tm = -__builtin_inf();
 #pragma unroll
                 for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -728,23 +742,30 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A, int ntile
                         const int lin = (l0 + q) + Nl * (k0 + kk);
                         tm = (lin == idx[r]) ? tm : fmax(tm, t);
                     }
+                tmax[kk] = tm;
             }
-            if (!__any(tm >= kThr)) return;
+            unsigned vote = 0;
+#pragma unroll
+            for (int kk = 0; kk < 8; ++kk) vote |= (__any(tmax[kk] >= kThr) ? 1u : 0u) << kk;
+            vote &= (1u << (k1 - k0)) - 1u;
+            if (!vote) return;
             stamp(2);
-            for (int kk = 0; kk < 8; ++kk) {
+            while (vote) {
+                const int kk = __builtin_ctz(vote);
+                vote &= vote - 1;
                 const int k = k0 + kk;
-                if (k >= k1) break;
+                const double2 tkk = s_cand[wave][k - sbase];
 #pragma unroll
                 for (int r = 0; r < R; ++r)
 #pragma unroll
                     for (int q = 0; q < LB; ++q) {
-                        const double c = coh[r][q] - tk[kk].x;
+                        const double c = coh[r][q] - tkk.x;
                         const int lin = (l0 + q) + Nl * k;
                         if (lin != idx[r] && c > 0 &&
-                            (tk[kk].y - B[r][q]) * aiy_ipow(c, NP) >= kThr) {
+                            (tkk.y - B[r][q]) * aiy_ipow(c, NP) >= kThr) {
                             ++nhits;
                             const double val =
-                                bell_val<NP, LAB>(c, s_ev[wave][k - sbase], A.sigma, dis[q]);
+                                bell_val<NP, LAB>(c, ev[k], A.sigma, dis[q]);
                             if (lexi_take(val, lin, best[r], idx[r])) {
 #pragma unroll
                                 for (int q2 = 0; q2 < LB; ++q2)
@@ -770,18 +791,18 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A, int ntile
             dm64 = fmax(dm64, __shfl_xor(dm64, 1));
             dm64 = fmax(dm64, __shfl_xor(dm64, 2));
             dm64 = fmax(dm64, __shfl_xor(dm64, 4));
+            // blocks inside the feasible range and owned by this wave
+            const int nblock = min(8, (kg - sbase + 63) >> 6);
+            unsigned own = 0;
+            for (int b = bsel; b < nblock; b += bstep) own |= 1u << b;
+            if (A.hitcount || A.trace) nblk += __builtin_popcount(own);
+            const unsigned bpass = mask8(dm64, a8, 0, 8, nblock) & own;
             unsigned long long pass = 0;  // bit 8b+u: sub-block u of block b passes
-            for (int b = bsel; b < 8; b += bstep) {
-                const int bbase = sbase + (b << 6);
-                if (bbase >= kg) break;
-                ++nblk;
-                if (!bound_pass(readlane_d(dm64, 8 * b), readlane_d(a8, 8 * b))) continue;
-                for (int u = 0; u < 8; ++u) {
-                    if (bbase + (u << 3) >= kg) break;
-                    ++nblk;
-                    if (bound_pass(readlane_d(dm8, 8 * b + u), readlane_d(a8, 8 * b + u)))
-                        pass |= 1ull << (8 * b + u);
-                }
+            for (unsigned bm = bpass; bm; bm &= bm - 1) {
+                const int b = __builtin_ctz(bm);
+                const int nsub = min(8, (kg - (sbase + (b << 6)) + 7) >> 3);
+                if (A.hitcount || A.trace) nblk += nsub;
+                pass |= (unsigned long long)mask8(dm8, a8, 8 * b, 1, nsub) << (8 * b);
             }
             if (!pass) {
                 stamp(1);
@@ -792,20 +813,14 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A, int ntile
                 if ((pass >> (8 * b)) & 0xffull) {
                     const int k = min(sbase + (b << 6) + lane, Na - 1);
                     s_cand[wave][(b << 6) + lane] = make_double2(a[k], Drow[k]);
-                    s_ev[wave][(b << 6) + lane] = ev[k];
                 }
             __builtin_amdgcn_wave_barrier();  // a wave reads only its own slice
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             stamp(1);
-            for (int b = 0; b < 8; ++b) {
-                const unsigned pb = (unsigned)(pass >> (8 * b)) & 0xffu;
-                if (!pb) continue;
-                const int bbase = sbase + (b << 6);
-                for (int u = 0; u < 8; ++u)
-                    if (pb & (1u << u)) {
-                        const int k0 = bbase + (u << 3);
-                        fine(sbase, k0, min(k0 + 8, kg));
-                    }
+            for (unsigned long long pm = pass; pm; pm &= pm - 1) {
+                const int bit = __builtin_ctzll(pm);
+                const int k0 = sbase + (bit << 3);
+                fine(sbase, k0, min(k0 + 8, kg));
             }
             stamp(2);
             __builtin_amdgcn_wave_barrier();  // reads done before the next superblock's writes
@@ -835,14 +850,21 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A, int ntile
             const double dm0 = oks ? A.Dm512[(size_t)i * A.nb512 + sbl] : -__builtin_inf();
             const double a0 = oks ? a[sbl << 9] : 0.0;
             const int ns = min(64, nsb - g);
-            for (int sq = 0; sq < ns; ++sq) {
-                if (g + sq == sfirst || (g + sq) % W != wave) continue;
-                ++nsup;
-                if (!bound_pass(readlane_d(dm0, sq), readlane_d(a0, sq))) continue;
-                superblock(g + sq, 0, 1);
+            for (int s8 = 0; s8 < ns; s8 += 8) {  // superblock bounds eight at a time
+                const int cnt = min(8, ns - s8);
+                unsigned own = 0;
+                for (int u = 0; u < cnt; ++u) {
+                    const int sb = g + s8 + u;
+                    if (sb != sfirst && sb % W == wave) own |= 1u << u;
+                }
+                if (!own) continue;
+                nsup += __builtin_popcount(own);
+                for (unsigned sm = mask8(dm0, a0, s8, 1, cnt) & own; sm; sm &= sm - 1)
+                    superblock(g + s8 + __builtin_ctz(sm), 0, 1);
             }
         }
     }
+
     exchange();
 
     // final outputs, wave 0 (the merge kernel's rules: Aiyagari_VFI.m:79-81,
