@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 
+#include <vector>
+
 namespace aiy {
 struct KsSlice {   // per (K_i, s_i), computed on the host with libm (Krusell_Smith_VFI.m)
     int kp_idx;    // nearest K_grid index of the ALM forecast K' (:335-343)
@@ -20,6 +22,11 @@ struct KsArgs {
     double beta, k_min, k_max, tol;
     int howard, max_vfi;
 };
+struct KsParams {  // the 13-double parameter block, in order
+    double beta, alpha, delta, k_min, k_max, ug, ub, l_bar, mu, z1, z2, e1, e2;
+};
+void ks_slices(const KsParams& p, const double* B, const double* K_grid, int nK,
+               std::vector<KsSlice>& out);
 struct KsOut {
     int iters;
     double rel;

@@ -1,0 +1,143 @@
+// Device tier of the Krusell-Smith VFI (A6/A7) for one process per GPU: a handle owns one
+// shard — the K range [K0, K1) of all four s — and runs the improvement, Howard and
+// relative-difference kernels on it, reading full k x K x S arrays already in HBM.  The
+// caller (aiyagari-replication_amd/ks_dist.py) exchanges the owned value slices between
+// ranks with an RCCL all-gather after every Howard sweep.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "aiy_common.hpp"
+#include "host_ctx.hpp"
+#include "ks.hpp"
+#include "ws.hpp"
+
+struct ks_dev {
+    int dev = 0;
+    int nk = 0, nK = 0, K0 = 0, K1 = 0;
+    double beta = 0, k_min = 0, k_max = 0;
+    double* kg = nullptr;
+    double* P = nullptr;
+    aiy::KsSlice* sl = nullptr;
+    double* dV = nullptr;
+    int* cols = nullptr;   // value columns (s*nK + K) this shard reads: own and K'_idx targets
+    int ncols = 0;
+    unsigned long long* slots = nullptr;
+};
+
+namespace aiy {
+static KsArgs shard_args(const ks_dev* h, int s) {
+    KsArgs A{};
+    A.nk = h->nk;
+    A.nK = h->nK;
+    A.node0 = (s * h->nK + h->K0) * h->nk;
+    A.n_local = (h->K1 - h->K0) * h->nk;
+    A.k_grid = h->kg;
+    A.P = h->P;
+    A.slice = h->sl;
+    A.beta = h->beta;
+    A.k_min = h->k_min;
+    A.k_max = h->k_max;
+    return A;
+}
+}  // namespace aiy
+
+using namespace aiy;
+
+extern "C" {
+
+int ks_dev_destroy(ks_dev* h) {
+    if (!h) return AIY_OK;
+    void* ps[] = {h->kg, h->P, h->sl, h->dV, h->cols, h->slots};
+    for (void* q : ps)
+        if (q) (void)hipFree(q);
+    delete h;
+    return AIY_OK;
+}
+
+int ks_dev_create(const double* k_grid, const double* K_grid, const double* B, const double* P,
+                  const double* params, int64_t nk, int64_t nK, int64_t K0, int64_t K1,
+                  ks_dev** out) {
+    if (!out || !k_grid || !K_grid || !B || !P || !params) return fail(AIY_BAD_ARG, "NULL argument");
+    if (nk < 3 || nK < 1 || nk * nK * 4 > (1ll << 30))
+        return fail(AIY_BAD_SHAPE, "need k_size >= 3, K_size >= 1");
+    if (K0 < 0 || K1 > nK || K0 >= K1) return fail(AIY_BAD_ARG, "shard [K0, K1) must be inside [0, K_size)");
+    AIY_TRY(check_grid(k_grid, nk));
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return fail(AIY_NO_DEVICE, "no HIP device visible");
+    KsParams p;
+    memcpy(&p, params, sizeof p);
+    std::vector<KsSlice> sl;
+    ks_slices(p, B, K_grid, (int)nK, sl);
+    std::vector<char> need(4 * nK, 0);
+    for (int s = 0; s < 4; ++s)
+        for (int64_t K = K0; K < K1; ++K) {
+            need[s * nK + K] = 1;
+            const int kp = sl[s * nK + K].kp_idx;
+            for (int sn = 0; sn < 4; ++sn) need[sn * nK + kp] = 1;
+        }
+    std::vector<int> cols;
+    for (int c = 0; c < 4 * nK; ++c)
+        if (need[c]) cols.push_back(c);
+    double Pr[16];
+    for (int i = 0; i < 4; ++i)
+        for (int m = 0; m < 4; ++m) Pr[i * 4 + m] = P[i + m * 4];
+    ks_dev* h = new ks_dev();
+    (void)hipGetDevice(&h->dev);
+    h->nk = (int)nk; h->nK = (int)nK; h->K0 = (int)K0; h->K1 = (int)K1;
+    h->beta = p.beta; h->k_min = p.k_min; h->k_max = p.k_max;
+    h->ncols = (int)cols.size();
+    const size_t n = (size_t)nk * nK * 4;
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = hipMalloc((void**)&h->kg, nk * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc((void**)&h->P, sizeof Pr);
+    if (e == hipSuccess) e = hipMalloc((void**)&h->sl, sl.size() * sizeof(KsSlice));
+    if (e == hipSuccess) e = hipMalloc((void**)&h->dV, n * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc((void**)&h->cols, cols.size() * sizeof(int));
+    if (e == hipSuccess) e = hipMalloc((void**)&h->slots, 2 * kDiffSlots * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemcpy(h->kg, k_grid, nk * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(h->P, Pr, sizeof Pr, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(h->sl, sl.data(), sl.size() * sizeof(KsSlice), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(h->cols, cols.data(), cols.size() * sizeof(int), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        ks_dev_destroy(h);
+        return fail(AIY_HIP_ERROR, "ks_dev_create: %s", hipGetErrorString(e));
+    }
+    *out = h;
+    return AIY_OK;
+}
+
+// Krusell_Smith_VFI.m:148-168 on the shard's nodes: slopes of the columns it reads, then
+// fminbnd per node.  V: full k x K x S (device); kopt: full array, owned nodes written.
+int ks_dev_improve(ks_dev* h, const double* V, double* kopt, void* stream) {
+    if (!h || !V || !kopt) return fail(AIY_BAD_ARG, "NULL argument");
+    hipStream_t st = (hipStream_t)stream;
+    AIY_TRY(launch_ks_slopes_cols(shard_args(h, 0), h->cols, h->ncols, V, h->dV, st));
+    for (int s = 0; s < 4; ++s) AIY_TRY(launch_ks_improve(shard_args(h, s), V, h->dV, kopt, nullptr, st));
+    return AIY_OK;
+}
+
+// one Jacobi Howard sweep (:173-191) on the shard's nodes: slopes from V, owned nodes of Vout
+int ks_dev_howard(ks_dev* h, const double* V, const double* kopt, double* Vout, void* stream) {
+    if (!h || !V || !kopt || !Vout) return fail(AIY_BAD_ARG, "NULL argument");
+    if (V == Vout) return fail(AIY_BAD_ARG, "Howard sweeps are Jacobi: V and Vout must differ");
+    hipStream_t st = (hipStream_t)stream;
+    AIY_TRY(launch_ks_slopes_cols(shard_args(h, 0), h->cols, h->ncols, V, h->dV, st));
+    for (int s = 0; s < 4; ++s) AIY_TRY(launch_ks_howard(shard_args(h, s), V, h->dV, kopt, Vout, st));
+    return AIY_OK;
+}
+
+// max over the shard's nodes of |V - Vold| / (|Vold| + 1e-10), NaN ignored (:195).
+// out (device, 2 x uint64): {IEEE bits of the max, nonzero if any node was not NaN}
+int ks_dev_reldiff(ks_dev* h, const double* V, const double* Vold, void* out, void* stream) {
+    if (!h || !V || !Vold || !out) return fail(AIY_BAD_ARG, "NULL argument");
+    hipStream_t st = (hipStream_t)stream;
+    AIY_HIP(hipMemsetAsync(h->slots, 0, 2 * kDiffSlots * sizeof(unsigned long long), st));
+    for (int s = 0; s < 4; ++s) AIY_TRY(launch_ks_reldiff(shard_args(h, s), V, Vold, h->slots, st));
+    AIY_TRY(launch_reduce_slots(h->slots, out, st));
+    return AIY_OK;
+}
+
+}  // extern "C"

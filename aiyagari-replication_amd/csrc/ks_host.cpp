@@ -15,12 +15,8 @@
 
 namespace aiy {
 
-struct KsParams {
-    double beta, alpha, delta, k_min, k_max, ug, ub, l_bar, mu, z1, z2, e1, e2;
-};
-
 // per-slice constants, in the script's own operation order (libm pow/exp/log on the host)
-static void ks_slices(const KsParams& p, const double* B, const double* K_grid, int nK,
+void ks_slices(const KsParams& p, const double* B, const double* K_grid, int nK,
                       std::vector<KsSlice>& out) {
     out.resize(4 * nK);
     const double zg[2] = {p.z1, p.z2}, eg[2] = {p.e1, p.e2};

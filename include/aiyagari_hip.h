@@ -225,6 +225,25 @@ int aiy_dist_update_dev(aiy_ws* ws, const double* lambda, const int32_t* policy_
                         const double* policy_k, const double* a_grid, const double* P,
                         double* lambda_out, double* diff, void* stream);
 
+/* ---- A6/A7 device tier for one process per GPU.  A handle owns the shard
+ * K in [K0, K1) of all four s; V / Vold / Vout / kopt are full k x K x S column-major device
+ * arrays (the layout of Krusell_Smith_VFI.m's `value`).  Each call writes only the shard's
+ * nodes; the caller exchanges the owned value slices between ranks (an RCCL all-gather,
+ * aiyagari-replication_amd/ks_dist.py) after every Howard sweep.  Same kernels as
+ * ks_vfi_solve, so any sharding gives the single-device result bit for bit. */
+typedef struct ks_dev ks_dev;
+int ks_dev_create(const double* k_grid, const double* K_grid, const double* B, const double* P,
+                  const double* params, int64_t nk, int64_t nK, int64_t K0, int64_t K1,
+                  ks_dev** out);
+int ks_dev_destroy(ks_dev* h);
+/* :148-168 policy improvement (pchip slopes + fminbnd) on the shard */
+int ks_dev_improve(ks_dev* h, const double* V, double* kopt, void* stream);
+/* :173-191 one Jacobi Howard sweep on the shard: Vout (!= V) gets the shard's new values */
+int ks_dev_howard(ks_dev* h, const double* V, const double* kopt, double* Vout, void* stream);
+/* :195 max relative change over the shard, NaN ignored; out = device uint64[2]
+ * {IEEE bits of the max, nonzero if any node was not NaN} */
+int ks_dev_reldiff(ks_dev* h, const double* V, const double* Vold, void* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

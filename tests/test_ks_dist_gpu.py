@@ -1,0 +1,80 @@
+"""GPU: the sharded Krusell-Smith VFI (ks_dist.py + ks_dev_* device tier) equals the
+single-device solve (ks_vfi_solve) bit for bit — one rank, and two ranks sharing the card over
+gloo (the RCCL path needs one GPU per rank; the exchange logic is the same)."""
+import json
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+B_ALM = np.array([0.1, 0.97, 0.08, 0.975])
+
+
+def _pkg():
+    sys.path.insert(0, str(ROOT))
+    from tests.conftest import load_pkg
+    return load_pkg()
+
+
+def _setup(nK):
+    from oracle import np_oracle as no
+    p, kg, Kg, P, V0, B = no.ks_setup(k_size=100, K_size=nK)
+    return kg, Kg, P, V0
+
+
+def _run(rank, world, nK, steps=8, vfi=7):
+    import torch
+    pkg = _pkg()
+    kg, Kg, P, V0 = _setup(nK)
+    prm = pkg.ks_params()
+    K0, K1 = pkg.ks_dist.shard_range(nK, rank, world)
+    sh = pkg.ks_dist.HipShard(kg, Kg, B_ALM, P, prm, K0, K1)
+    V = torch.as_tensor(np.ascontiguousarray(V0.transpose(2, 1, 0)), device="cuda:0")
+    ko = torch.ones_like(V)
+    it, rel = pkg.ks_dist.ks_vfi_solve_dist(V, ko, sh, nK, howard_steps=steps, tol=1e-6,
+                                            max_vfi=vfi, rank=rank, world=world)
+    torch.cuda.synchronize()
+    return V.cpu().numpy(), ko.cpu().numpy(), it, rel
+
+
+def _reference(nK, steps=8, vfi=7):
+    pkg = _pkg()
+    kg, Kg, P, V0 = _setup(nK)
+    R = pkg.ks_vfi_solve(V0, np.ones_like(V0), kg, Kg, B_ALM, P, pkg.ks_params(),
+                         howard_steps=steps, tol=1e-6, max_vfi=vfi)
+    return (np.ascontiguousarray(R["value"].transpose(2, 1, 0)),
+            np.ascontiguousarray(R["k_opt"].transpose(2, 1, 0)), R["iters"], R["rel_diff"])
+
+
+def test_one_rank_equals_single_device(pkg, gpu):
+    V, ko, it, rel = _run(0, 1, 4)
+    Vr, kr, itr, relr = _reference(4)
+    assert it == itr and np.array_equal(V, Vr) and np.array_equal(ko, kr) and rel == relr
+
+
+def _worker(rank, world, port, outdir, nK):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    V, ko, it, rel = _run(rank, world, nK)
+    np.save(Path(outdir, f"V{rank}.npy"), V)
+    np.save(Path(outdir, f"k{rank}.npy"), ko)
+    Path(outdir, f"m{rank}.json").write_text(json.dumps(dict(it=it, rel=rel)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("nK", [4, 6])
+def test_two_ranks_gloo_equal_single_device(pkg, gpu, tmp_path, nK):
+    import torch.multiprocessing as mp
+    port = 29800 + (os.getpid() % 1000) + nK
+    mp.spawn(_worker, args=(2, port, str(tmp_path), nK), nprocs=2, join=True)
+    Vr, kr, itr, relr = _reference(nK)
+    for rank in range(2):
+        assert np.array_equal(np.load(Path(tmp_path, f"V{rank}.npy")), Vr)
+        assert np.array_equal(np.load(Path(tmp_path, f"k{rank}.npy")), kr)
+        assert json.loads(Path(tmp_path, f"m{rank}.json").read_text())["it"] == itr
