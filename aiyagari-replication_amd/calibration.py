@@ -104,3 +104,33 @@ def aiyagari(Na=400, rho=0.75, sigma_e=0.75, beta=0.96, sigma=5.0, alpha=0.36, d
     a_grid, amin = asset_grid(Na, alpha, beta, delta, b, s[0])
     return dict(P=P, s=s, labor=float(s @ pi), a_grid=a_grid, amin=amin, beta=beta,
                 sigma=sigma, alpha=alpha, delta=delta, N=len(s), Na=Na)
+
+
+def krusell_smith(k_size=100, K_size=4, K_min=30.0, K_max=50.0, beta=0.99, k_min=0.0001,
+                  k_max=1000.0, ug=0.04, ub=0.10):
+    """Krusell_Smith_VFI.m:5-55 and :97-98: the individual grid k_grid = x^7 scaling with
+    pinned endpoints (:16-17), the aggregate grid K_grid (linspace, :20), the 4x4 transition
+    matrix over s = (z, eps) built from the unemployment durations (:33-55), and the initial
+    value log(0.1/0.9 k_opt0)/(1-beta) with k_opt0 = 0.9 k (:97-98).  Returns
+    (k_grid, K_grid, P, V0) with V0 of shape (k, K, 4) (MATLAB's k x K x S)."""
+    x = linspace01(k_size)
+    k_grid = (x ** 7) * (k_max - k_min) + k_min
+    k_grid[0], k_grid[-1] = k_min, k_max
+    K_grid = K_min + (K_max - K_min) * linspace01(K_size)
+    pgg = pbb = 1 - 1 / 8
+    pgb, pbg = 1 - pgg, 1 - pbb
+    p00_gg, p00_bb = 1 - 1 / 1.5, 1 - 1 / 2.5
+    p00_gb, p00_bg = 1.25 * p00_bb, 0.75 * p00_gg
+    p01_gg, p01_bb, p01_gb, p01_bg = 1 - p00_gg, 1 - p00_bb, 1 - p00_gb, 1 - p00_bg
+    p10_gg = (ug - ug * p00_gg) / (1 - ug)
+    p10_bb = (ub - ub * p00_bb) / (1 - ub)
+    p10_gb = (ub - ug * p00_gb) / (1 - ug)
+    p10_bg = (ug - ub * p00_bg) / (1 - ub)
+    p11_gg, p11_bb, p11_gb, p11_bg = 1 - p10_gg, 1 - p10_bb, 1 - p10_gb, 1 - p10_bg
+    P = np.array([[pgg * p11_gg, pgb * p11_gb, pgg * p10_gg, pgb * p10_gb],
+                  [pbg * p11_bg, pbb * p11_bb, pbg * p10_bg, pbb * p10_bb],
+                  [pgg * p01_gg, pgb * p01_gb, pgg * p00_gg, pgb * p00_gb],
+                  [pbg * p01_bg, pbb * p01_bb, pbg * p00_bg, pbb * p00_bb]])
+    k_opt0 = 0.9 * np.repeat(np.repeat(k_grid[:, None, None], K_size, 1), 4, 2)
+    V0 = np.log(0.1 / 0.9 * k_opt0) / (1 - beta)
+    return k_grid, K_grid, P, V0

@@ -140,4 +140,16 @@ int ks_dev_reldiff(ks_dev* h, const double* V, const double* Vold, void* out, vo
     return AIY_OK;
 }
 
+int ks_forecast_index(const double* K_grid, const double* B, const double* params, int64_t nK,
+                      int32_t* out) {
+    if (!K_grid || !B || !params || !out) return fail(AIY_BAD_ARG, "NULL argument");
+    if (nK < 1 || nK > (1 << 24)) return fail(AIY_BAD_SHAPE, "need 1 <= K_size");
+    KsParams p;
+    memcpy(&p, params, sizeof p);
+    std::vector<KsSlice> sl;
+    ks_slices(p, B, K_grid, (int)nK, sl);
+    for (size_t c = 0; c < sl.size(); ++c) out[c] = sl[c].kp_idx;
+    return AIY_OK;
+}
+
 }  // extern "C"

@@ -7,7 +7,10 @@ Aiyagari VFI, Na = 20,000, Nz = 7 Rouwenhorst, one exhaustive Bellman sweep per 
 
 Multi-GPU: the general-equilibrium loop's candidate interest rates are independent units
 (SURVEY §8(e) E2), so each rank solves its own r (weak scaling, no collective on the data
-path); the timing is max over ranks.  Rank 0 prints one JSON line.
+path); the timing is max over ranks.  Rank 0 prints one JSON line.  The line also carries
+`ks_sharded` (BASELINE configs[4]): one VFI iteration of the Krusell-Smith solve at k = 32,768,
+K = 64 sharded over the same N ranks (strong scaling, halo exchange per Howard sweep), so the
+driver's N = 1, 2, 4, 8 runs give its speed-up directly.
 """
 from __future__ import annotations
 
@@ -122,6 +125,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ge", action="store_true", help="skip the GE wall-time leg")
     ap.add_argument("--no-solve", action="store_true", help="skip the solve-to-tol leg")
+    ap.add_argument("--no-ks", action="store_true", help="skip the sharded Krusell-Smith leg")
     args = ap.parse_args()
 
     import torch
@@ -191,6 +195,11 @@ def main():
     else:
         kern_avg_ms = kern_ms / max(launches, 1)
 
+    ks = None
+    if not args.no_ks:   # BASELINE configs[4]: KS VFI sharded over the same ranks (strong)
+        import bench_ks
+        ks = bench_ks.ks_leg(pkg, world, rank, dev)
+
     if rank == 0:
         evals_per_sweep = N * Na * Na
         value = world * evals_per_sweep * args.steps / dt
@@ -246,6 +255,8 @@ def main():
                                             f"{evals_per_sweep} candidates per launch, the exhaustive "
                                             f"scan this kernel reproduces bit for bit"},
         }
+        if ks is not None:
+            out["ks_sharded"] = ks
         if not args.no_solve:
             out["solve_to_tol"] = solve_wall(pkg, ws, cal, r, w, a_t, s_t, P_t, dev)
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count())

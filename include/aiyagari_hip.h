@@ -243,6 +243,12 @@ int ks_dev_howard(ks_dev* h, const double* V, const double* kopt, double* Vout, 
 /* :195 max relative change over the shard, NaN ignored; out = device uint64[2]
  * {IEEE bits of the max, nonzero if any node was not NaN} */
 int ks_dev_reldiff(ks_dev* h, const double* V, const double* Vold, void* out, void* stream);
+/* Host-only (no device): the forecast column K'_idx(s, K) that bellman_value reads for every
+ * node of slice (K, s) (Krusell_Smith_VFI.m:335-343, clamp + nearest index), 0-based,
+ * out[s * nK + K].  The sharded driver builds its halo exchange from it: a rank needs, besides
+ * its own slices, exactly the columns K'_idx of its nodes, for all four s'. */
+int ks_forecast_index(const double* K_grid, const double* B, const double* params, int64_t nK,
+                      int32_t* out);
 
 #ifdef __cplusplus
 }

@@ -62,7 +62,7 @@ def _setup(nK=4):
     return cp, kg, Kg, P, V0, B
 
 
-def _worker(rank, world, port, outdir, nK):
+def _worker(rank, world, port, outdir, nK, exchange="halo"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     from oracle import corc
     corc.num_threads(1)
@@ -74,20 +74,26 @@ def _worker(rank, world, port, outdir, nK):
     K0, K1 = kd.shard_range(len(Kg), rank, world)
     V = torch.from_numpy(np.ascontiguousarray(V0.transpose(2, 1, 0)))
     ko = torch.ones_like(V)
-    it, rel = kd.ks_vfi_solve_dist(V, ko, OracleShard(cp, kg, Kg, B, P, K0, K1), len(Kg),
-                                   howard_steps=3, tol=1e-6, max_vfi=6, rank=rank, world=world)
+    sh = OracleShard(cp, kg, Kg, B, P, K0, K1)
+    sh.kp_idx = kd.forecast_index(Kg, B, _pkg().ks_params())  # host-only C ABI call
+    it, rel = kd.ks_vfi_solve_dist(V, ko, sh, len(Kg), howard_steps=3, tol=1e-6, max_vfi=6,
+                                   rank=rank, world=world, exchange=exchange,
+                                   poison=(exchange == "halo"))
     np.save(Path(outdir, f"V{rank}.npy"), V.numpy())
     np.save(Path(outdir, f"k{rank}.npy"), ko.numpy())
     Path(outdir, f"m{rank}.json").write_text(json.dumps(dict(it=it, rel=rel)))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,nK", [(2, 4), (3, 5)])
-def test_gloo_sharded_equals_unsharded(tmp_path, world, nK):
+@pytest.mark.parametrize("world,nK,exchange", [(2, 4, "halo"), (3, 5, "halo"), (3, 8, "halo"),
+                                               (2, 4, "allgather")])
+def test_gloo_sharded_equals_unsharded(tmp_path, world, nK, exchange):
+    """Halo runs poison every column a rank neither owns nor reads with NaN: equality with the
+    unsharded solve then proves the halo plan covers every read."""
     import torch.multiprocessing as mp
     from oracle import corc
-    port = 29600 + (os.getpid() % 1500) + 7 * world
-    mp.spawn(_worker, args=(world, port, str(tmp_path), nK), nprocs=world, join=True)
+    port = 29600 + (os.getpid() % 1500) + 7 * world + 3 * nK + (exchange == "halo")
+    mp.spawn(_worker, args=(world, port, str(tmp_path), nK, exchange), nprocs=world, join=True)
     cp, kg, Kg, P, V0, B = _setup(nK)
     R = corc.ks_vfi_solve(cp, kg, Kg, V0, np.ones_like(V0), B, P, howard=3, tol=1e-6, max_vfi=6)
     Vr = np.ascontiguousarray(R["value"].transpose(2, 1, 0))
@@ -108,3 +114,46 @@ def test_shard_ranges_cover():
             rs = [kd.shard_range(nK, r, world) for r in range(world)]
             assert rs[0][0] == 0 and rs[-1][1] == nK
             assert all(rs[i][1] == rs[i + 1][0] and rs[i][0] < rs[i][1] for i in range(world - 1))
+
+
+def test_forecast_index_and_halo_plan():
+    """ks_forecast_index (host-only) is the clamp + nearest-index rule of bellman_value
+    (Krusell_Smith_VFI.m:335-343); halo_plan lists exactly the foreign columns a rank reads."""
+    kd = _pkg().ks_dist
+    prm = _pkg().ks_params()
+    Kg = np.linspace(30.0, 50.0, 64)
+    for B in ([0.1, 0.97, 0.08, 0.975], [0.0, 1.0, 0.0, 1.0], [0.5, 0.8, -0.3, 1.1]):
+        B = np.array(B)
+        kp = kd.forecast_index(Kg, B, prm)
+        z1, z2 = prm[9], prm[10]
+        for s in range(4):
+            z = z2 if s + 1 <= 2 else z1            # flipped current_z (:332)
+            b0, b1 = (B[0], B[1]) if z == z1 else (B[2], B[3])
+            Kp = np.clip(np.exp(b0 + b1 * np.log(Kg)), Kg[0], Kg[-1])
+            want = np.argmin(np.abs(Kg[None, :] - Kp[:, None]), axis=1)
+            assert np.array_equal(kp[s], want)
+        for world in (2, 3, 8):
+            plan = kd.halo_plan(kp, 64, world)
+            for q in range(world):
+                a, b = kd.shard_range(64, q, world)
+                need = set(np.unique(kp[:, a:b]).tolist()) - set(range(a, b))
+                got = [c for p in range(world) for c in plan[q][p]]
+                assert sorted(got) == sorted(need) and not plan[q][q]
+                for p in range(world):
+                    pa, pb = kd.shard_range(64, p, world)
+                    assert all(pa <= c < pb for c in plan[q][p])
+    # identity ALM: every node forecasts its own K, so no halo at all
+    kp = kd.forecast_index(Kg, np.array([0.0, 1.0, 0.0, 1.0]), prm)
+    assert np.array_equal(kp, np.tile(np.arange(64), (4, 1)))
+    assert all(not c for row in kd.halo_plan(kp, 64, 8) for c in row)
+
+
+def test_calibration_matches_oracle_setup():
+    """The package's KS calibration (used by the benches) equals the oracle's restatement."""
+    from oracle import np_oracle as no
+    cal = _pkg().calibration
+    for k, K in ((100, 4), (1000, 64)):
+        p, kg, Kg, P, V0, B = no.ks_setup(k_size=k, K_size=K)
+        kg2, Kg2, P2, V02 = cal.krusell_smith(k_size=k, K_size=K)
+        for a, b in ((kg, kg2), (Kg, Kg2), (P, P2), (V0, V02)):
+            assert np.array_equal(a, b)

@@ -26,7 +26,7 @@ def _setup(nK):
     return kg, Kg, P, V0
 
 
-def _run(rank, world, nK, steps=8, vfi=7):
+def _run(rank, world, nK, steps=8, vfi=7, exchange="halo"):
     import torch
     pkg = _pkg()
     kg, Kg, P, V0 = _setup(nK)
@@ -36,7 +36,8 @@ def _run(rank, world, nK, steps=8, vfi=7):
     V = torch.as_tensor(np.ascontiguousarray(V0.transpose(2, 1, 0)), device="cuda:0")
     ko = torch.ones_like(V)
     it, rel = pkg.ks_dist.ks_vfi_solve_dist(V, ko, sh, nK, howard_steps=steps, tol=1e-6,
-                                            max_vfi=vfi, rank=rank, world=world)
+                                            max_vfi=vfi, rank=rank, world=world,
+                                            exchange=exchange, poison=(exchange == "halo"))
     torch.cuda.synchronize()
     return V.cpu().numpy(), ko.cpu().numpy(), it, rel
 
@@ -56,23 +57,24 @@ def test_one_rank_equals_single_device(pkg, gpu):
     assert it == itr and np.array_equal(V, Vr) and np.array_equal(ko, kr) and rel == relr
 
 
-def _worker(rank, world, port, outdir, nK):
+def _worker(rank, world, port, outdir, nK, exchange="halo"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                       HSA_ENABLE_IPC_MODE_LEGACY="0")
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    V, ko, it, rel = _run(rank, world, nK)
+    V, ko, it, rel = _run(rank, world, nK, exchange=exchange)
     np.save(Path(outdir, f"V{rank}.npy"), V)
     np.save(Path(outdir, f"k{rank}.npy"), ko)
     Path(outdir, f"m{rank}.json").write_text(json.dumps(dict(it=it, rel=rel)))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("nK", [4, 6])
-def test_two_ranks_gloo_equal_single_device(pkg, gpu, tmp_path, nK):
+@pytest.mark.parametrize("nK,exchange", [(4, "halo"), (6, "halo"), (6, "allgather")])
+def test_two_ranks_gloo_equal_single_device(pkg, gpu, tmp_path, nK, exchange):
+    """Halo runs NaN-poison every column a rank neither owns nor reads (ks_dist poison)."""
     import torch.multiprocessing as mp
-    port = 29800 + (os.getpid() % 1000) + nK
-    mp.spawn(_worker, args=(2, port, str(tmp_path), nK), nprocs=2, join=True)
+    port = 29800 + (os.getpid() % 1000) + nK + 20 * (exchange == "halo")
+    mp.spawn(_worker, args=(2, port, str(tmp_path), nK, exchange), nprocs=2, join=True)
     Vr, kr, itr, relr = _reference(nK)
     for rank in range(2):
         assert np.array_equal(np.load(Path(tmp_path, f"V{rank}.npy")), Vr)

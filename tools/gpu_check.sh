@@ -24,8 +24,10 @@ for s in ${STEPS:-tests smoke bench prof}; do
     smoke) step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python -u bench.py ${BENCH_ARGS} ;;
     prof)  step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/prof" -o run -- python3 "$PWD/bench.py" --no-cpu-baseline --no-ge --no-solve ${BENCH_ARGS} ;;
-    pmc)   step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$PWD/$OUT/pmc_fetch" -o run -- python3 "$PWD/bench.py" --no-cpu-baseline --steps 3 --warmup 2
-           step pmc_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$PWD/$OUT/pmc_write" -o run -- python3 "$PWD/bench.py" --no-cpu-baseline --steps 3 --warmup 2 ;;
+    pmc)   PMC_ARGS="--no-cpu-baseline --no-ge --no-solve --no-ks --steps 20 --warmup 5"
+           step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$PWD/$OUT/pmc/fetch" -o run -- python3 "$PWD/bench.py" $PMC_ARGS
+           step pmc_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$PWD/$OUT/pmc/write" -o run -- python3 "$PWD/bench.py" $PMC_ARGS
+           python3 tools/pmc_traffic.py "$OUT/pmc" bell_tree_kernel "$OUT/traffic_vfi_tree.json" ;;
     custom) step custom 600 bash -c "$CUSTOM" ;;
   esac
 done
