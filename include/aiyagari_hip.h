@@ -148,6 +148,27 @@ int ks_egm_solve(double* k_opt, const double* k_grid, const double* K_grid, cons
                  const double* P, const double* params, int64_t nk, int64_t nK, double tol,
                  int64_t max_iter, int64_t* iters, double* diff);
 
+/* F3 — replaces the shock simulation Krusell_Smith_VFI.m:57-94 (also Krusell_Smith_EGM.m).
+ * uniforms: the script's `rand` stream, ks_shock_draws(T, population) values in its draw order
+ * (T-1 aggregate draws :63/:65, `population` draws :71, then (T-1)*population draws with t
+ * outer and i inner :89/:91).  params: the 13 KS doubles (ug = params[5], ub = params[6]).
+ * out: zi_shock T (0 good / 1 bad: the value after `zi_shock - 1`, :68) and epsi_shock
+ * T x population column-major (1 employed / 2 unemployed). */
+int64_t ks_shock_draws(int64_t T, int64_t population);
+int ks_shocks(int64_t T, int64_t population, const double* uniforms, const double* params,
+              double* zi_shock, double* epsi_shock);
+
+/* F2 — replaces the capital path simulation Krusell_Smith_VFI.m:206-248 (Krusell_Smith_EGM.m
+ * :211-253).  k_opt k x K x 4; zi_shock T; epsi_shock T x population (as ks_shocks returns);
+ * k_population in/out (it persists across ALM iterations in the script, :101); K_ts out (T).
+ * Every agent moves to griddedInterpolant({k_grid, K_grid}, k_opt(:,:,s))(k, K_ts(t)) (2-D
+ * linear, linear extrapolation), s from (z_t, eps_t,i) in s_grid order; K_ts(t+1) =
+ * mean(k_population) summed in the fixed order documented in DESIGN.md (MATLAB's is unpinned). */
+int ks_simulate_capital(const double* k_opt, const double* k_grid, const double* K_grid,
+                        int64_t nk, int64_t nK, const double* zi_shock,
+                        const double* epsi_shock, int64_t T, int64_t population,
+                        double* k_population, double* K_ts);
+
 /* ======================================================================================
  * Device tier: [N][Na] (z-major) arrays in HBM, async on `stream` (hipStream_t).
  * A workspace holds the per-shape scratch (EV/D tables, init/partial buffers, events).
@@ -249,6 +270,18 @@ int ks_dev_reldiff(ks_dev* h, const double* V, const double* Vold, void* out, vo
  * its own slices, exactly the columns K'_idx of its nodes, for all four s'. */
 int ks_forecast_index(const double* K_grid, const double* B, const double* params, int64_t nK,
                       int32_t* out);
+
+/* ---- F3 / F2 device tier.  uniforms, zi (int8 [T], 0 good / 1 bad) and eps (int8
+ * [T][population] row-major, 0 employed / 1 unemployed: t-major so each period is one
+ * contiguous row) in HBM; k_opt k x K x 4 column-major; k_population in/out; K_ts out [T];
+ * scratch: ks_panel_scratch_bytes(population) bytes of device memory. */
+int ks_shocks_dev(int64_t T, int64_t population, const double* uniforms, const double* params,
+                  int8_t* zi, int8_t* eps, void* stream);
+int64_t ks_panel_scratch_bytes(int64_t population);
+int ks_simulate_capital_dev(int64_t nk, int64_t nK, const double* k_grid, const double* K_grid,
+                            const double* k_opt, int64_t T, int64_t population,
+                            const int8_t* zi, const int8_t* eps, double* k_population,
+                            double* K_ts, void* scratch, void* stream);
 
 #ifdef __cplusplus
 }

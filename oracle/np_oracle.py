@@ -902,3 +902,143 @@ def ks_egm_solve(p, k_grid, K_grid, B, P, k_opt, tol=1e-6, max_iter=10000):
         if diff < tol:
             break
     return dict(k_opt=k_opt, iters=it, diff=diff)
+
+
+# ----------------------------------------------------------------------------------------
+# F3  Krusell-Smith shock panel (Krusell_Smith_VFI.m:57-94) and F2 panel simulation
+#     (:206-248).  Vectorised over agents; every operation is an IEEE basic operation or a
+#     comparison, so the results are exact restatements (no libm).
+# ----------------------------------------------------------------------------------------
+
+
+def ks_eps_probs(p):
+    """The idiosyncratic transition probabilities of Krusell_Smith_VFI.m:24-45, returned as
+    thr[cur_z, prev_z, prev_e] = Peps(prev_e, 1) of :78-92 (z: 0 good / 1 bad after the
+    `zi_shock - 1` of :68; e: 0 employed / 1 unemployed = epsi_shock - 1)."""
+    pgg = 1 - 1 / 8; pbb = 1 - 1 / 8
+    p00_gg = 1 - 1 / 1.5; p00_bb = 1 - 1 / 2.5
+    p00_gb = 1.25 * p00_bb; p00_bg = 0.75 * p00_gg
+    p01_gg = 1 - p00_gg; p01_bb = 1 - p00_bb; p01_gb = 1 - p00_gb; p01_bg = 1 - p00_bg
+    ug, ub = p["ug"], p["ub"]
+    p10_gg = (ug - ug * p00_gg) / (1 - ug); p10_bb = (ub - ub * p00_bb) / (1 - ub)
+    p10_gb = (ub - ug * p00_gb) / (1 - ug); p10_bg = (ug - ub * p00_bg) / (1 - ub)
+    p11_gg = 1 - p10_gg; p11_bb = 1 - p10_bb; p11_gb = 1 - p10_gb; p11_bg = 1 - p10_bg
+    thr = np.zeros((2, 2, 2))
+    # (cur, prev) -> matrix: (0,0) gg, (0,1) bg, (1,0) gb, else bb  (:78-86)
+    for cz, pz, (p11, p01) in ((0, 0, (p11_gg, p01_gg)), (0, 1, (p11_bg, p01_bg)),
+                               (1, 0, (p11_gb, p01_gb)), (1, 1, (p11_bb, p01_bb))):
+        thr[cz, pz, 0] = p11   # prev_eps == 1 -> Peps(1,1)  (:88-89)
+        thr[cz, pz, 1] = p01   # else          -> Peps(2,1)  (:90-91)
+    return dict(pgg=pgg, pbb=pbb, thr=thr)
+
+
+def ks_shock_draws(T, population):
+    """Number of `rand` draws :57-94 consumes: T-1 aggregate, `population` initial, then
+    (T-1)*population idiosyncratic (t outer, i inner)."""
+    return (T - 1) + population + (T - 1) * population
+
+
+def ks_shocks(p, T, population, U):
+    """Krusell_Smith_VFI.m:59-94.  U = the MATLAB rand stream (ks_shock_draws(T, pop) values).
+    Returns zi (T,) int8 in {0 good, 1 bad} (= zi_shock after :68) and e (T, population) int8 in
+    {0, 1} (= epsi_shock - 1: 0 employed, 1 unemployed)."""
+    pr = ks_eps_probs(p)
+    U = np.asarray(U, dtype=np.float64)
+    zi = np.zeros(T, np.int8)
+    z = 1                                                     # :60 zi_shock(1) = 1
+    for t in range(1, T):                                     # :61-67
+        u = U[t - 1]
+        z = 1 + int(u > (pr["pgg"] if z == 1 else pr["pbb"]))
+        zi[t] = z - 1
+    pos = T - 1
+    e = np.zeros((T, population), np.int8)
+    e[0] = (U[pos:pos + population] > p["ug"]).astype(np.int8)   # :71 ((rand>ug)+1) - 1
+    pos += population
+    thr = pr["thr"]
+    for t in range(1, T):                                     # :72-94
+        th = thr[zi[t], zi[t - 1]][e[t - 1]]
+        e[t] = (U[pos:pos + population] > th).astype(np.int8)
+        pos += population
+    return zi, e
+
+
+def ks_panel_blocks(population, block=256, max_blocks=1024):
+    """Reduction geometry of mean(k_population) shared with the HIP kernel (MATLAB's own sum
+    order is unpinned): G blocks of `block` lanes; lane g of the grid sums agents g, g + G*block,
+    ... in order; each block folds its lanes pairwise (h = block/2 ... 1); the G block sums are
+    added in block order and divided by the population."""
+    return max(1, min(max_blocks, -(-population // block)))
+
+
+def ks_mean_blocked(x, G, block=256):
+    n = x.size
+    L = G * block
+    lanes = np.zeros(L)
+    for m in range(0, n, L):
+        seg = x[m:m + L]
+        lanes[:seg.size] = lanes[:seg.size] + seg
+    s = lanes.reshape(G, block)
+    h = block // 2
+    while h >= 1:
+        s = s.copy()
+        s[:, :h] = s[:, :h] + s[:, h:2 * h]
+        h //= 2
+    acc = 0.0
+    for b in range(G):
+        acc = acc + s[b, 0]
+    return acc / n
+
+
+def _bilin_seg(x, q):
+    i = np.searchsorted(x, q, side="right") - 1
+    return np.clip(i, 0, x.size - 2)
+
+
+def ks_panel_simulate(k_grid, K_grid, k_opt, zi, e, k_pop, block=256, max_blocks=1024):
+    """Krusell_Smith_VFI.m:206-248: K_ts(1) = mean(k_population); per period t the agents in
+    state s = (z_t, eps_t,i) (s_grid order (g,e),(g,u),(b,e),(b,u), :19-20) move to
+    griddedInterpolant({k_grid, K_grid}, k_opt(:,:,s)) at (k, K_ts(t)) — bilinear, linear
+    extrapolation from the edge cells: segment = largest i with x_i <= q clamped to
+    [0, n-2]; f0 = f(ik,iK) + tk*(f(ik+1,iK) - f(ik,iK)), f1 likewise at iK+1,
+    value = f0 + tK*(f1 - f0).  k_opt indexed [k, K, s].  Returns (K_ts, k_pop)."""
+    k_pop = np.array(k_pop, dtype=np.float64, copy=True)
+    T = zi.size
+    n = k_pop.size
+    G = ks_panel_blocks(n, block, max_blocks)
+    K_ts = np.zeros(T)
+    K_ts[0] = ks_mean_blocked(k_pop, G, block)                     # :208
+    for t in range(T - 1):                                         # :222
+        K = K_ts[t]
+        iK = int(_bilin_seg(K_grid, np.array([K]))[0])
+        tK = (K - K_grid[iK]) / (K_grid[iK + 1] - K_grid[iK])
+        s = 2 * int(zi[t]) + e[t].astype(np.int64)                 # :227-232
+        ik = _bilin_seg(k_grid, k_pop)
+        tk = (k_pop - k_grid[ik]) / (k_grid[ik + 1] - k_grid[ik])
+        f00 = k_opt[ik, iK, s]; f10 = k_opt[ik + 1, iK, s]
+        f01 = k_opt[ik, iK + 1, s]; f11 = k_opt[ik + 1, iK + 1, s]
+        f0 = f00 + tk * (f10 - f00)
+        f1 = f01 + tk * (f11 - f01)
+        k_pop = f0 + tK * (f1 - f0)                                # :241-246
+        K_ts[t + 1] = ks_mean_blocked(k_pop, G, block)             # :247
+    return K_ts, k_pop
+
+
+def ks_alm_regress(K_ts, zi, T_discard=100):
+    """Krusell_Smith_VFI.m:252-285: OLS of log K(t+1) on [1, log K(t)] per aggregate state over
+    t = T_discard..T-1 (MATLAB 1-based t).  Returns (B_new (4,), R2_g, R2_b).  MATLAB's `\\`
+    is a QR solve; numpy's lstsq (SVD) agrees to rounding (ulp-level; not bit-pinned)."""
+    T = K_ts.size
+    ts = np.arange(T_discard - 1, T - 1)                           # 0-based t
+    B = np.zeros(4)
+    R2 = [0.0, 0.0]
+    for g, zsel in ((0, 0), (1, 1)):
+        sel = ts[zi[ts] == zsel]
+        if sel.size == 0:
+            continue
+        X = np.stack([np.ones(sel.size), np.log(K_ts[sel])], 1)
+        Y = np.log(K_ts[sel + 1])
+        b = np.linalg.lstsq(X, Y, rcond=None)[0]
+        B[2 * g:2 * g + 2] = b
+        res = Y - X @ b
+        R2[g] = 1 - np.sum(res ** 2) / np.sum((Y - Y.mean()) ** 2)
+    return B, R2[0], R2[1]

@@ -123,9 +123,28 @@ def make_ks_egm():
     print(f"  KS EGM done {time.time()-t0:.1f}s ({full['iters']} sweeps)")
 
 
+def make_ks_panel():
+    """F3/F2: Krusell_Smith_VFI.m:57-94 shock panel and :206-248 capital simulation at a
+    reduced panel (T = 120 periods, 700 agents: three reduction blocks, the last one ragged),
+    MATLAB's fresh-session rand stream, the policy k_opt of ks_defaults (one improvement) and
+    the script's initial population k = K_grid(1) (:101)."""
+    p, kg, Kg, Pk, _, B = no.ks_setup()
+    g = np.load(Path(__file__).resolve().parent / "ks_defaults.npz")
+    T, pop = 120, 700
+    U = no.matlab_rand_stream(no.ks_shock_draws(T, pop))
+    zi, e = no.ks_shocks(p, T, pop, U)
+    k0 = np.full(pop, Kg[0])
+    K_ts, k_fin = no.ks_panel_simulate(kg, Kg, g["k_opt"], zi, e, k0)
+    save("ks_panel_small", T=T, population=pop, zi=zi, eps=e, k_opt=g["k_opt"], k_grid=kg,
+         K_grid=Kg, K_ts=K_ts, k_final=k_fin, ug=p["ug"], ub=p["ub"])
+    print("  KS panel done")
+
+
 if __name__ == "__main__":
     import sys as _sys
     if len(_sys.argv) > 1 and _sys.argv[1] == "ks_egm":
         make_ks_egm()
+    elif len(_sys.argv) > 1 and _sys.argv[1] == "ks_panel":
+        make_ks_panel()
     else:
         main()

@@ -67,3 +67,24 @@ def test_ks_egm_shape_and_usage(cal):
     with pytest.raises(mexstub.MexError) as e:
         mexstub.call("ks_egm_solve_mex", 1, np.zeros((10, 4, 4)))
     assert e.value.id == "aiy:usage"
+
+
+def test_ks_panel_gateways_validate(cal):
+    """F3/F2 gateways: argument counts and shapes are checked before the library is called."""
+    with pytest.raises(mexstub.MexError) as e:
+        mexstub.call("ks_shocks_mex", 2, 10.0, 5.0, np.zeros(3), np.zeros(13))
+    assert e.value.id == "aiy:shape"   # uniforms must hold (T-1) + pop + (T-1)*pop draws
+    with pytest.raises(mexstub.MexError) as e:
+        mexstub.call("ks_shocks_mex", 2, 10.5, 5.0, np.zeros(3), np.zeros(13))
+    assert e.value.id == "aiy:shape"
+    with pytest.raises(mexstub.MexError) as e:
+        mexstub.call("ks_simulate_capital_mex", 2, np.zeros((10, 4, 4)), np.linspace(0, 1, 10),
+                     np.linspace(30, 50, 4), np.zeros(5), np.ones((5, 3)), np.ones(4))
+    assert e.value.id == "aiy:shape"   # epsi_shock columns != numel(k_population)
+    with pytest.raises(mexstub.MexError) as e:
+        mexstub.call("ks_simulate_capital_mex", 2, np.zeros((10, 4, 4)))
+    assert e.value.id == "aiy:usage"
+    with pytest.raises(mexstub.MexError) as e:   # zi_shock codes other than 0/1: BAD_ARG
+        mexstub.call("ks_simulate_capital_mex", 2, np.zeros((10, 4, 4)), np.linspace(0, 1, 10),
+                     np.linspace(30, 50, 4), np.full(5, 3.0), np.ones((5, 3)), np.ones(3))
+    assert e.value.id == "aiy:BAD_ARG"

@@ -74,3 +74,17 @@ def test_ks_egm_gateway(pkg, gpu, golden):
     assert int(it[0, 0]) == 3
     assert np.array_equal(ko.reshape(g["k_opt3"].shape, order="F"), g["k_opt3"])
     assert float(diff[0, 0]) == float(g["diff3"])
+
+
+def test_ks_panel_gateways(pkg, gpu, golden):
+    """ks_shocks_mex / ks_simulate_capital_mex (Krusell_Smith_VFI.m:57-94, :206-248) reproduce
+    the committed panel fixture."""
+    from oracle import np_oracle as no
+    g = golden("ks_panel_small")
+    T, pop = int(g["T"]), int(g["population"])
+    U = no.matlab_rand_stream(no.ks_shock_draws(T, pop))
+    zi, ep = mexstub.call("ks_shocks_mex", 2, float(T), float(pop), U, pkg.ks_params())
+    assert np.array_equal(zi.ravel(), g["zi"]) and np.array_equal(ep, g["eps"] + 1)
+    K_ts, kf = mexstub.call("ks_simulate_capital_mex", 2, g["k_opt"], g["k_grid"], g["K_grid"],
+                            zi, ep, np.full(pop, g["K_grid"][0]))
+    assert np.array_equal(K_ts.ravel(), g["K_ts"]) and np.array_equal(kf.ravel(), g["k_final"])
