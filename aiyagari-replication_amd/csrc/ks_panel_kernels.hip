@@ -10,10 +10,10 @@
 // Panel simulation: per period every agent moves by a 2-D linear interpolation of k_opt(:,:,s)
 // at (k, K_ts(t)) (griddedInterpolant default 'linear', linear extrapolation), and
 // K_ts(t+1) = mean(k_population) couples all agents.  One launch per period: the launch for
-// period t first folds the previous launch's block partials in block order (every block, the
+// period t first folds the previous launch's block partials pairwise (every block, the
 // same sequence of additions, so every block holds the same K_ts(t) — no grid barrier, no
 // atomics), then moves its agents and writes its own partial.  The order of the mean is fixed
-// (lane-strided sums, pairwise fold per block, block order) and restated by
+// (lane-strided sums, pairwise fold per block, pairwise fold of the zero-padded block sums) and restated by
 // np_oracle.ks_panel_simulate; MATLAB's own summation order is unpinned.
 #include "aiy_common.hpp"
 #include "ks_panel.hpp"
@@ -22,14 +22,25 @@ namespace aiy {
 
 constexpr int kPanelLdsGrid = 8192;  // k_grid staged in LDS up to this many points
 
+// The aggregate chain on one wave: 64 draws per round are loaded in parallel, compared with
+// both thresholds (two ballots), then the wave walks the 64 steps on the masks with scalar bit
+// logic — the serial part is register work, the loads are not on the dependency chain.
 __global__ __launch_bounds__(64) void ks_zi_kernel(ShockArgs A) {
-    if (threadIdx.x != 0) return;
-    int z = 1;                                   // :60 zi_shock(1) = 1 (1-based good)
-    A.zi[0] = 0;
-    for (int t = 1; t < A.T; ++t) {              // :61-67
-        const double u = A.U[t - 1];
-        z = 1 + (u > (z == 1 ? A.pgg : A.pbb) ? 1 : 0);
-        A.zi[t] = (int8_t)(z - 1);               // :68
+    const int lane = threadIdx.x;
+    int z = 0;                                   // :60 zi_shock(1) = 1 (0 after :68)
+    if (lane == 0) A.zi[0] = 0;
+    for (int t0 = 1; t0 < A.T; t0 += 64) {       // :61-67
+        const int t = t0 + lane;
+        const double u = t < A.T ? A.U[t - 1] : 0.0;
+        const unsigned long long g = __ballot(u > A.pgg);   // next bad if now good
+        const unsigned long long b = __ballot(u > A.pbb);   // next bad if now bad
+        unsigned long long zm = 0;
+        const int n = min(64, A.T - t0);
+        for (int q = 0; q < n; ++q) {
+            z = (int)(((z ? b : g) >> q) & 1ull);
+            zm |= (unsigned long long)z << q;
+        }
+        if (t < A.T) A.zi[t] = (int8_t)((zm >> lane) & 1ull);
     }
 }
 
@@ -43,7 +54,7 @@ __global__ __launch_bounds__(256) void ks_eps_kernel(ShockArgs A) {
     U += pop;
     const int8_t* __restrict__ zi = A.zi;
     int zp = zi[0];
-    constexpr int UN = 8;
+    constexpr int UN = 32;
     int t = 1;
     for (; t + UN <= A.T; t += UN) {
         double u[UN];
@@ -95,11 +106,42 @@ __device__ __forceinline__ double block_fold(double acc, double* red) {
     return x;
 }
 
-// sum of the G block partials in block order, divided by the population (thread 0)
+// mean of the population from the G block partials (wave 0; every lane returns it): the
+// partials, zero-padded to G' = next power of two, are folded pairwise (h = G'/2 ... 1:
+// s[l] + s[l+h]), then divided by the population.  Lane l holds s[l + 64m]: the folds with
+// h >= 64 stay in registers, h < 64 are shuffles — one parallel load, no barrier, no serial
+// chain of G dependent additions.  Split in a load and a fold phase so the loads can be in
+// flight together with the block's other prefetches.
+constexpr int kFoldPer = kPanelMaxBlocks / 64;   // 16 partials per lane at most
+__device__ __forceinline__ void fold_load(const double* __restrict__ part, int G, double* v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int m = 0; m < kFoldPer; ++m) {
+        const int i = lane + 64 * m;
+        v[m] = i < G ? part[i] : 0.0;
+    }
+}
+__device__ __forceinline__ double fold_sum(double* v, int G, int pop) {
+    int Gp = 1;
+    while (Gp < G) Gp <<= 1;
+#pragma unroll
+    for (int hm = kFoldPer / 2; hm >= 1; hm >>= 1)   // h = 64*hm
+        if (64 * hm < Gp)
+#pragma unroll
+            for (int m = 0; m < hm; ++m) v[m] = v[m] + v[m + hm];
+    double x = v[0];
+#pragma unroll
+    for (int h = 32; h >= 1; h >>= 1) {
+        const double o = __shfl_down(x, h);
+        if (h < Gp) x = x + o;
+    }
+    x = __shfl(x, 0);
+    return x / (double)pop;
+}
 __device__ __forceinline__ double fold_partials(const double* __restrict__ part, int G, int pop) {
-    double acc = 0.0;
-    for (int b = 0; b < G; ++b) acc = acc + part[b];
-    return acc / (double)pop;
+    double v[kFoldPer];
+    fold_load(part, G, v);
+    return fold_sum(v, G, pop);
 }
 
 __device__ __forceinline__ int seg_lds(const double* x, int n, double q) {
@@ -125,59 +167,82 @@ __global__ __launch_bounds__(256) void ks_panel_sum_kernel(PanelArgs A) {
     if (threadIdx.x == 0) A.part[blockIdx.x] = s;
 }
 
+// One period.  Dependent global round trips: one (the previous partials, the grids, this
+// thread's first agent and its state are all loaded together before the first barrier) plus
+// the k_opt gathers, which need K.
 template <bool LDS>
 __global__ __launch_bounds__(256) void ks_panel_step_kernel(PanelArgs A, int t) {
     __shared__ double red[256];
     __shared__ double sK;
-    extern __shared__ double kg_lds[];
+    extern __shared__ double grid_lds[];
+    const int nk = A.nk, nK = A.nK;
     const double* kg = A.k_grid;
+    const double* Kg = A.K_grid;
     if constexpr (LDS) {
-        for (int q = threadIdx.x; q < A.nk; q += 256) kg_lds[q] = A.k_grid[q];
-        kg = kg_lds;
+        for (int q = threadIdx.x; q < nk; q += 256) grid_lds[q] = A.k_grid[q];
+        for (int q = threadIdx.x; q < nK; q += 256) grid_lds[nk + q] = A.K_grid[q];
+        kg = grid_lds;
+        Kg = grid_lds + nk;
     }
-    const double* part_in = A.part + (t & 1) * A.G;
-    double* part_out = A.part + ((t + 1) & 1) * A.G;
-    if (threadIdx.x == 0) {
-        const double K = fold_partials(part_in, A.G, A.pop);
-        sK = K;
-        if (blockIdx.x == 0) A.K_ts[t] = K;   // :208 / :247 of the previous period
+    const int64_t L = (int64_t)A.G * 256;
+    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int zt = A.zi[t];
+    const int8_t* __restrict__ erow = A.eps + (int64_t)t * A.ts;
+    double k = 0.0;
+    int e = 0;
+    if (i < A.pop) {           // first agent: prefetched before the partials are folded
+        k = A.k_pop[i];
+        e = erow[i * A.is];
     }
+    double v[kFoldPer];
+    if (threadIdx.x < 64) fold_load(A.part + (t & 1) * A.G, A.G, v);
+    __syncthreads();           // grids staged; every prefetch has landed
+    if (threadIdx.x < 64) {
+        const double K = fold_sum(v, A.G, A.pop);
+        if (threadIdx.x == 0) {
+            sK = K;
+            if (blockIdx.x == 0) A.K_ts[t] = K;   // :208 / :247 of the previous period
+        }
+    }
+    // k-segment of the first agent does not depend on K
+    int ik = seg_lds(kg, nk, k);
+    double tk = (k - kg[ik]) / (kg[ik + 1] - kg[ik]);
     __syncthreads();
     const double K = sK;
-    const int nk = A.nk, nK = A.nK;
-    const int iK = seg_of_dev(A.K_grid, nK, K);
-    const double K0 = A.K_grid[iK], K1 = A.K_grid[iK + 1];
-    const double tK = (K - K0) / (K1 - K0);
-    const int zt = A.zi[t];
-    const int64_t L = (int64_t)A.G * 256;
+    const int iK = seg_lds(Kg, nK, K);
+    const double tK = (K - Kg[iK]) / (Kg[iK + 1] - Kg[iK]);
     double acc = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < A.pop; i += L) {
-        const double k = A.k_pop[i];
-        const int s = 2 * zt + A.eps[(int64_t)t * A.ts + i * A.is];   // :227-232
-        const int ik = seg_lds(kg, nk, k);
-        const double x0 = kg[ik], x1 = kg[ik + 1];
-        const double tk = (k - x0) / (x1 - x0);
-        const double* f = A.k_opt + ((size_t)s * nK + iK) * nk + ik;   // column (iK, s)
+    while (i < A.pop) {
+        const int s = 2 * zt + e;                                        // :227-232
+        const double* f = A.k_opt + ((size_t)s * nK + iK) * nk + ik;     // column (iK, s)
         const double f00 = f[0], f10 = f[1], f01 = f[nk], f11 = f[nk + 1];
         const double f0 = f00 + tk * (f10 - f00);
         const double f1 = f01 + tk * (f11 - f01);
         const double kn = f0 + tK * (f1 - f0);   // :241-245
         A.k_pop[i] = kn;                         // :246
         acc = acc + kn;
+        i += L;
+        if (i < A.pop) {
+            k = A.k_pop[i];
+            e = erow[i * A.is];
+            ik = seg_lds(kg, nk, k);
+            tk = (k - kg[ik]) / (kg[ik + 1] - kg[ik]);
+        }
     }
     const double sb = block_fold(acc, red);
-    if (threadIdx.x == 0) part_out[blockIdx.x] = sb;
+    if (threadIdx.x == 0) A.part[((t + 1) & 1) * A.G + blockIdx.x] = sb;
 }
 
 __global__ __launch_bounds__(64) void ks_panel_final_kernel(PanelArgs A, int t) {
-    if (threadIdx.x == 0) A.K_ts[t] = fold_partials(A.part + (t & 1) * A.G, A.G, A.pop);
+    const double K = fold_partials(A.part + (t & 1) * A.G, A.G, A.pop);
+    if (threadIdx.x == 0) A.K_ts[t] = K;
 }
 
 int launch_ks_panel(const PanelArgs& A, hipStream_t st) {
     ks_panel_sum_kernel<<<A.G, 256, 0, st>>>(A);
     AIY_HIP(hipGetLastError());
-    const bool lds = A.nk <= kPanelLdsGrid;
-    const size_t sh = lds ? sizeof(double) * A.nk : 0;
+    const bool lds = A.nk + A.nK <= kPanelLdsGrid;
+    const size_t sh = lds ? sizeof(double) * (A.nk + A.nK) : 0;
     for (int t = 0; t + 1 < A.T; ++t) {
         if (lds) ks_panel_step_kernel<true><<<A.G, 256, sh, st>>>(A, t);
         else ks_panel_step_kernel<false><<<A.G, 256, 0, st>>>(A, t);

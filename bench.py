@@ -126,6 +126,7 @@ def main():
     ap.add_argument("--no-ge", action="store_true", help="skip the GE wall-time leg")
     ap.add_argument("--no-solve", action="store_true", help="skip the solve-to-tol leg")
     ap.add_argument("--no-ks", action="store_true", help="skip the sharded Krusell-Smith leg")
+    ap.add_argument("--no-panel", action="store_true", help="skip the KS panel (F2/F3) leg")
     args = ap.parse_args()
 
     import torch
@@ -257,6 +258,9 @@ def main():
         }
         if ks is not None:
             out["ks_sharded"] = ks
+        if not args.no_panel and world == 1:   # F3/F2: KS shock panel + agent simulation
+            import bench_panel
+            out["ks_panel"] = bench_panel.panel_leg(pkg, dev)
         if not args.no_solve:
             out["solve_to_tol"] = solve_wall(pkg, ws, cal, r, w, a_t, s_t, P_t, dev)
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count())

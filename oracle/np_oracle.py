@@ -965,8 +965,9 @@ def ks_shocks(p, T, population, U):
 def ks_panel_blocks(population, block=256, max_blocks=1024):
     """Reduction geometry of mean(k_population) shared with the HIP kernel (MATLAB's own sum
     order is unpinned): G blocks of `block` lanes; lane g of the grid sums agents g, g + G*block,
-    ... in order; each block folds its lanes pairwise (h = block/2 ... 1); the G block sums are
-    added in block order and divided by the population."""
+    ... in order; each block folds its lanes pairwise (h = block/2 ... 1); the G block sums,
+    zero-padded to the next power of two, are folded pairwise the same way and the total is
+    divided by the population."""
     return max(1, min(max_blocks, -(-population // block)))
 
 
@@ -983,10 +984,17 @@ def ks_mean_blocked(x, G, block=256):
         s = s.copy()
         s[:, :h] = s[:, :h] + s[:, h:2 * h]
         h //= 2
-    acc = 0.0
-    for b in range(G):
-        acc = acc + s[b, 0]
-    return acc / n
+    Gp = 1
+    while Gp < G:
+        Gp *= 2
+    q = np.zeros(Gp)
+    q[:G] = s[:, 0]
+    h = Gp // 2
+    while h >= 1:
+        q = q.copy()
+        q[:h] = q[:h] + q[h:2 * h]
+        h //= 2
+    return q[0] / n
 
 
 def _bilin_seg(x, q):
