@@ -167,6 +167,18 @@ __global__ __launch_bounds__(256) void ks_panel_sum_kernel(PanelArgs A) {
     if (threadIdx.x == 0) A.part[blockIdx.x] = s;
 }
 
+// griddedInterpolant({k_grid, K_grid}, k_opt(:,:,s)) at (k, K): column (iK, s) of k_opt,
+// segments ik / iK with weights tk / tK (:241-245)
+__device__ __forceinline__ double move_agent(const PanelArgs& A, int iK, double tK, int s, int ik,
+                                             double tk) {
+    const int nk = A.nk;
+    const double* f = A.k_opt + ((size_t)s * A.nK + iK) * nk + ik;
+    const double f00 = f[0], f10 = f[1], f01 = f[nk], f11 = f[nk + 1];
+    const double f0 = f00 + tk * (f10 - f00);
+    const double f1 = f01 + tk * (f11 - f01);
+    return f0 + tK * (f1 - f0);
+}
+
 // One period.  Dependent global round trips: one (the previous partials, the grids, this
 // thread's first agent and its state are all loaded together before the first barrier) plus
 // the k_opt gathers, which need K.
@@ -212,21 +224,37 @@ __global__ __launch_bounds__(256) void ks_panel_step_kernel(PanelArgs A, int t) 
     const int iK = seg_lds(Kg, nK, K);
     const double tK = (K - Kg[iK]) / (Kg[iK + 1] - Kg[iK]);
     double acc = 0.0;
-    while (i < A.pop) {
-        const int s = 2 * zt + e;                                        // :227-232
-        const double* f = A.k_opt + ((size_t)s * nK + iK) * nk + ik;     // column (iK, s)
-        const double f00 = f[0], f10 = f[1], f01 = f[nk], f11 = f[nk + 1];
-        const double f0 = f00 + tk * (f10 - f00);
-        const double f1 = f01 + tk * (f11 - f01);
-        const double kn = f0 + tK * (f1 - f0);   // :241-245
-        A.k_pop[i] = kn;                         // :246
+    // first agent (prefetched); the lane's sum keeps agent order
+    if (i < A.pop) {
+        const double kn = move_agent(A, iK, tK, 2 * zt + e, ik, tk);   // :227-245
+        A.k_pop[i] = kn;                                                 // :246
         acc = acc + kn;
         i += L;
-        if (i < A.pop) {
-            k = A.k_pop[i];
-            e = erow[i * A.is];
-            ik = seg_lds(kg, nk, k);
-            tk = (k - kg[ik]) / (kg[ik + 1] - kg[ik]);
+    }
+    // further agents (more than G*256 agents), four at a time: loads, searches and gathers
+    // of the four are independent, only the lane sum is ordered
+    for (; i < A.pop; i += 4 * L) {
+        double kk[4], kn[4];
+        int ee[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t j = i + q * L;
+            kk[q] = j < A.pop ? A.k_pop[j] : kg[0];
+            ee[q] = j < A.pop ? erow[j * A.is] : 0;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int jk = seg_lds(kg, nk, kk[q]);
+            const double tq = (kk[q] - kg[jk]) / (kg[jk + 1] - kg[jk]);
+            kn[q] = move_agent(A, iK, tK, 2 * zt + ee[q], jk, tq);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t j = i + q * L;
+            if (j < A.pop) {
+                A.k_pop[j] = kn[q];
+                acc = acc + kn[q];
+            }
         }
     }
     const double sb = block_fold(acc, red);

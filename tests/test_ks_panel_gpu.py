@@ -30,7 +30,8 @@ def test_simulate_fixture(pkg, gpu, golden):
     assert np.array_equal(K_ts, g["K_ts"]) and np.array_equal(kf, g["k_final"])
 
 
-@pytest.mark.parametrize("T,pop", [(1100, 10000), (2, 1), (7, 255), (9, 257), (33, 300001)])
+@pytest.mark.parametrize("T,pop", [(1100, 10000), (2, 1), (7, 255), (9, 257), (33, 300001),
+                                   (3, 5 * 262144 + 7)])
 def test_reference_size_and_ragged(pkg, gpu, golden, T, pop):
     """The script's panel (T = 1100, 10,000 agents) and ragged/edge populations (one agent,
     one block short/over, > 1024 blocks so lanes hold several agents)."""
