@@ -222,9 +222,103 @@ int ws_read_diff(aiy_ws* ws, hipStream_t st, double* d) {
     return AIY_OK;
 }
 
+// A2 with speculative batches.  The one-sweep-at-a-time loop pays a stream synchronisation per
+// sweep to read max|Δv| (at the script's Na = 400 that round trip costs more than the sweep).
+// Here sweeps are enqueued m at a time: sweep g reads ring slot (g−1) mod R and writes slot
+// g mod R (R = spec_max + 1 value buffers), its policies go to set g mod spec_max, its folded
+// diff to its own slot, and one D2H read per batch finds the first sweep below tol.  Sweeps
+// are deterministic and each depends only on its predecessor, so sweeps 1..g* are exactly the
+// ones the plain loop runs; later sweeps of the batch are discarded and the ring still holds
+// v_new(g*), v_old = v(g*−1) and the policies of g*.  m follows the observed geometric decay
+// of the diff (sweeps still needed to reach tol), capped at spec_max.
+static int bell_solve_spec(aiy_ws* ws, BellCall c, double* v_a, double* v_b, double tol,
+                           int64_t max_iter, int64_t* iters, int* out_new, hipStream_t st) {
+    const int R = ws->spec_max + 1, Rp = ws->spec_max;
+    const size_t n = (size_t)ws->N * ws->Na;
+    if (ws->spec_n != n) {
+        ws->free_spec();
+        AIY_TRY(dalloc(&ws->spec_v, (size_t)R * n));
+        AIY_TRY(dalloc(&ws->spec_idx, (size_t)Rp * n));
+        AIY_TRY(dalloc(&ws->spec_pol, (size_t)Rp * 3 * n));
+        AIY_TRY(dalloc(&ws->spec_diff, 2 * (size_t)Rp));
+        AIY_HIP(hipHostMalloc((void**)&ws->spec_hdiff, 2 * (size_t)Rp * sizeof(unsigned long long)));
+        ws->spec_n = n;
+    }
+    auto vslot = [&](int64_t g) { return ws->spec_v + (size_t)(g % R) * n; };
+    auto islot = [&](int64_t g) { return ws->spec_idx + (size_t)(g % Rp) * n; };
+    auto pslot = [&](int64_t g, int q) { return ws->spec_pol + ((size_t)(g % Rp) * 3 + q) * n; };
+    const size_t vb = n * sizeof(double);
+    // slot 0 = v_old of sweep 1; slot 1 = the incoming v_new buffer (the labour sweep's
+    // keep-incoming rule reads it on sweep 1)
+    AIY_HIP(hipMemcpyAsync(vslot(0), v_a, vb, hipMemcpyDeviceToDevice, st));
+    AIY_HIP(hipMemcpyAsync(vslot(1), v_b, vb, hipMemcpyDeviceToDevice, st));
+    const int* first_hint = c.hint;
+    double* const upk = c.pk;
+    double* const upc = c.pc;
+    double* const upl = c.pl;
+    int* const uidx = c.idx;
+    int64_t done = 0, stop = 0;
+    double d_prev = NAN, d_last = NAN;
+    while (!stop && done < max_iter) {
+        int64_t m = ws->spec_max;
+        if (d_last == d_last && d_prev == d_prev && d_last < d_prev && d_last > 0) {
+            double need = std::ceil(std::log(tol / d_last) / std::log(d_last / d_prev));
+            if (need >= 1 && need < (double)m) m = (int64_t)need;
+        }
+        m = std::min<int64_t>(std::max<int64_t>(m, 1), max_iter - done);
+        for (int64_t t = 0; t < m; ++t) {
+            const int64_t g = done + 1 + t;
+            c.hint = (g == 1) ? first_hint : islot(g - 1);
+            c.keep_incoming = (g == 1);
+            c.v_old = vslot(g - 1);
+            c.v_new = vslot(g);
+            c.idx = islot(g);
+            c.pk = upk ? pslot(g, 0) : nullptr;
+            c.pc = upc ? pslot(g, 1) : nullptr;
+            c.pl = upl ? pslot(g, 2) : nullptr;
+            c.diff_out = reinterpret_cast<double*>(ws->spec_diff + 2 * t);  // {bits, any}
+            AIY_TRY(bell_sweep_dev(ws, c, st));
+        }
+        AIY_HIP(hipMemcpyAsync(ws->spec_hdiff, ws->spec_diff,
+                               2 * (size_t)m * sizeof(unsigned long long),
+                               hipMemcpyDeviceToHost, st));
+        AIY_HIP(hipStreamSynchronize(st));
+        for (int64_t t = 0; t < m; ++t) {
+            const unsigned long long* h = ws->spec_hdiff + 2 * t;
+            double d = NAN;  // {max|Δ| bits, any non-NaN} (reduce_slots_kernel)
+            if (h[1]) std::memcpy(&d, &h[0], sizeof d);
+            d_prev = d_last;
+            d_last = d;
+            if (d < tol) {  // Aiyagari_VFI.m:85-86
+                stop = done + 1 + t;
+                break;
+            }
+        }
+        if (!stop) done += m;
+    }
+    const int64_t g = stop ? stop : max_iter;
+    // the plain loop leaves v_new in v_b after odd sweep counts (ping-pong from v_a)
+    const int nw = (g & 1) ? 1 : 0;
+    double* vnew = nw ? v_b : v_a;
+    double* vold = nw ? v_a : v_b;
+    AIY_HIP(hipMemcpyAsync(vnew, vslot(g), vb, hipMemcpyDeviceToDevice, st));
+    // exhausted: v_old = v_new after the last sweep (:88); else the previous iterate
+    AIY_HIP(hipMemcpyAsync(vold, stop ? vslot(g - 1) : vslot(g), vb, hipMemcpyDeviceToDevice, st));
+    AIY_HIP(hipMemcpyAsync(uidx, islot(g), n * sizeof(int), hipMemcpyDeviceToDevice, st));
+    if (upk) AIY_HIP(hipMemcpyAsync(upk, pslot(g, 0), vb, hipMemcpyDeviceToDevice, st));
+    if (upc) AIY_HIP(hipMemcpyAsync(upc, pslot(g, 1), vb, hipMemcpyDeviceToDevice, st));
+    if (upl) AIY_HIP(hipMemcpyAsync(upl, pslot(g, 2), vb, hipMemcpyDeviceToDevice, st));
+    *iters = g;
+    *out_new = nw;
+    return AIY_OK;
+}
+
 int bell_solve_dev(aiy_ws* ws, BellCall c, double* v_a, double* v_b, double tol,
                    int64_t max_iter, int64_t* iters, int* out_new, hipStream_t st) {
     if (max_iter < 1) return fail(AIY_BAD_ARG, "max_iter must be >= 1");
+    if (!c.idx) return fail(AIY_BAD_ARG, "NULL device pointer");
+    if (ws && ws->spec_max > 1 && !c.diff_out)
+        return bell_solve_spec(ws, c, v_a, v_b, tol, max_iter, iters, out_new, st);
     double* cur = v_a;
     double* nxt = v_b;
     const int* first_hint = c.hint;
@@ -362,6 +456,14 @@ int aiy_ws_set_variant(aiy_ws* ws, int variant) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
     if (variant < 0 || variant > 31) return fail(AIY_BAD_ARG, "variant in [0, 31]");
     ws->variant = variant;
+    return AIY_OK;
+}
+
+int aiy_ws_set_speculation(aiy_ws* ws, int max_batch) {
+    if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
+    if (max_batch < 0 || max_batch > 256) return fail(AIY_BAD_ARG, "max_batch in [0, 256]");
+    if (max_batch != ws->spec_max) ws->free_spec();
+    ws->spec_max = max_batch;
     return AIY_OK;
 }
 

@@ -105,12 +105,179 @@ __global__ __launch_bounds__(64) void sim_capital_kernel(SimArgs A) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Chain kernel (N <= 15).  The state chain z_t does not depend on k, so it leaves the critical
+// path: for a chunk of steps the whole block tabulates each step's transition map
+//   F_t = { z -> find(u_t < cumsum(P(z,:)), 1) }   (4 bits per z, 15 = find() empty)
+// into LDS, and the serial step becomes z_t = (F_t >> 4 z_{t-1}) & 15 on scalars.  The k step
+// reads a 64-point window of a_grid and of the policy row around the previous segment in one
+// LDS round; every lane evaluates interp1's formula for its own segment while the ballot
+// locates k, and the segment's lane is read back (v_readlane) — the division runs in parallel
+// with the search instead of after it.  A window that misses k falls back to the 64-ary search.
+// Same operations in the same order as sim_capital_kernel, so the path is bit-identical.
+constexpr int kSimChunk = 2048;
+constexpr int kSimChainLdsMax = 16384;  // doubles for a_grid + policy rows (+16 KB F, 2 KB cs)
+
+__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int l) {
+    unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
+    unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+template <bool LDS>
+__global__ __launch_bounds__(256) void sim_chain_kernel(SimArgs A) {
+    extern __shared__ double lds[];
+    __shared__ unsigned long long F[kSimChunk];
+    __shared__ double cs[16 * 16];
+    __shared__ int stop_flag;
+    const int tid = threadIdx.x, lane = tid & 63;
+    // wave-uniform for the compiler too: the chain's control flow and indices stay scalar
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int N = A.N, Na = A.Na;
+    const double* a = A.a;
+    const double* pol = A.pol;
+    size_t zs = A.zs, as = A.as;
+    if constexpr (LDS) {
+        for (int k = tid; k < Na; k += 256) lds[k] = A.a[k];
+        for (int q = tid; q < N * Na; q += 256) {
+            int zz = q / Na, kk = q - zz * Na;
+            lds[Na + q] = A.pol[(size_t)zz * A.zs + (size_t)kk * A.as];
+        }
+        a = lds;
+        pol = lds + Na;
+        zs = Na;
+        as = 1;
+    }
+    if (tid == 0) {  // cumulative transition rows, sequential sums as cumsum does
+        for (int z = 0; z < N; ++z) {
+            double acc = 0.0;
+            for (int m = 0; m < N; ++m) {
+                acc = acc + A.P[z * N + m];
+                cs[z * N + m] = acc;
+            }
+        }
+        stop_flag = 0;
+    }
+    __syncthreads();
+    const int wmax = Na > 64 ? Na - 64 : 0;
+    int z = A.z1;
+    double k = A.k1;
+    double sum = k;
+    int w0 = 0;
+    int status = 0;
+    double kbuf = k;  // lane (t & 63) holds sim_k(t) until its block of 64 is stored
+    int zbuf = z;
+    int t_last = 0;
+    auto flush = [&](int t) {
+        const int base = t & ~63;
+        if (base + lane <= t) {
+            if (A.sim_k) A.sim_k[base + lane] = kbuf;
+            if (A.sim_z) A.sim_z[base + lane] = zbuf;
+        }
+    };
+    for (int c0 = 1; c0 < A.T; c0 += kSimChunk) {
+        const int cn = min(kSimChunk, A.T - c0);
+        for (int q = tid; q < cn; q += 256) {
+            const double u = A.U[c0 + q - 1];
+            unsigned long long f = 0;
+            for (int zz = 0; zz < N; ++zz) {
+                int m = 15;
+                for (int mm = N - 1; mm >= 0; --mm)
+                    if (u < cs[zz * N + mm]) m = mm;
+                f |= (unsigned long long)m << (4 * zz);
+            }
+            F[q] = f;
+        }
+        __syncthreads();
+        if (wave == 0) {
+            unsigned long long Fv = 0;
+            for (int i = 0; i < cn; ++i) {
+                const int t = c0 + i;
+                if ((i & 63) == 0) Fv = (i + lane < cn) ? F[i + lane] : 0ull;
+                const unsigned long long f = readlane_u64(Fv, i & 63);
+                const int zn = (int)((f >> (4 * z)) & 15ull);
+                if (zn == 15) {  // the reference's find() would return empty and error
+                    status = 1;
+                    break;
+                }
+                z = zn;
+                const double* y = pol + (size_t)z * zs;
+                // ---- window round: every lane evaluates its own segment (indices clamped so
+                // the loads need no exec masking; lanes past the grid are never selected)
+                const int p = w0 + lane;
+                const int p0 = min(p, Na - 1), p1 = min(p + 1, Na - 1);
+                const double x0 = a[p0], x1 = a[p1];
+                const double y0 = y[(size_t)p0 * as], y1 = y[(size_t)p1 * as];
+                const int cnt = __popcll(__ballot(p < Na && x0 <= k));
+                const double tt = (k - x0) / (x1 - x0);
+                const double kn = y0 + tt * (y1 - y0);
+                const int wend = min(w0 + 64, Na);
+                int seg = w0 + cnt - 1;
+                seg = seg < 0 ? 0 : (seg > Na - 2 ? Na - 2 : seg);
+                const int sl = min(max(seg - w0, 0), 63);
+                const double kw = readlane_d(kn, sl);  // issued before the rare fallback test
+                if ((cnt > 0 || w0 == 0) && (w0 + cnt < wend || wend == Na)) {
+                    k = kw;
+                } else {  // window missed: largest i with a[i] <= k by 64-ary search
+                    int lo = 0, hi = Na;
+                    while (hi - lo > 64) {
+                        int step = (hi - lo + 63) / 64;
+                        int pp = lo + lane * step;
+                        bool le = pp < hi && a[pp] <= k;
+                        int c = __popcll(__ballot(le));
+                        if (c == 0) {
+                            hi = lo;
+                            break;
+                        }
+                        lo = lo + (c - 1) * step;
+                        hi = min(lo + step, hi);
+                    }
+                    int pp = lo + lane;
+                    int c = __popcll(__ballot(pp < hi && a[pp] <= k));
+                    seg = lo + c - 1;
+                    seg = seg < 0 ? 0 : (seg > Na - 2 ? Na - 2 : seg);
+                    double X0 = a[seg], X1 = a[seg + 1];
+                    double Y0 = y[(size_t)seg * as], Y1 = y[(size_t)(seg + 1) * as];
+                    double T0 = (k - X0) / (X1 - X0);
+                    k = Y0 + T0 * (Y1 - Y0);
+                }
+                w0 = seg - 31;
+                w0 = w0 < 0 ? 0 : (w0 > wmax ? wmax : w0);
+                sum += k;
+                if (lane == (t & 63)) {
+                    kbuf = k;
+                    zbuf = z;
+                }
+                t_last = t;
+                if ((t & 63) == 63) flush(t);
+            }
+            if (status && lane == 0) stop_flag = 1;
+        }
+        __syncthreads();
+        if (stop_flag) break;
+    }
+    if (wave == 0) {
+        if ((t_last & 63) != 63) flush(t_last);
+        if (lane == 0) {
+            A.out[0] = sum / (double)A.T;  // mean(sim_k)
+            A.status[0] = status;
+        }
+    }
+}
+
 int launch_sim_capital(const SimArgs& A, hipStream_t st) {
     if (A.N > 16 || A.N < 1) return fail(AIY_BAD_SHAPE, "simulation supports 1 <= N <= 16");
-    if ((long long)A.Na * (A.N + 1) <= kSimLdsMax)
-        sim_capital_kernel<true><<<1, 64, sizeof(double) * A.Na * (A.N + 1), st>>>(A);
-    else
+    const long long need = (long long)A.Na * (A.N + 1);
+    if (A.N <= 15) {
+        if (need <= kSimChainLdsMax)
+            sim_chain_kernel<true><<<1, 256, sizeof(double) * need, st>>>(A);
+        else
+            sim_chain_kernel<false><<<1, 256, 0, st>>>(A);
+    } else if (need <= kSimLdsMax) {
+        sim_capital_kernel<true><<<1, 64, sizeof(double) * need, st>>>(A);
+    } else {
         sim_capital_kernel<false><<<1, 64, 0, st>>>(A);
+    }
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }

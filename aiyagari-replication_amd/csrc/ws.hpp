@@ -55,6 +55,15 @@ struct aiy_ws {
     double* g1 = nullptr;
     double* g2 = nullptr;
     int* gi = nullptr;
+    // speculative solve (aiy_ws_set_speculation): ring of spec_max + 1 value buffers, spec_max
+    // policy sets and one folded-diff slot per sweep of a batch
+    int spec_max = 16;
+    size_t spec_n = 0;  // states per buffer the rings were sized for (0 = not allocated)
+    double* spec_v = nullptr;
+    int* spec_idx = nullptr;
+    double* spec_pol = nullptr;                 // [spec_max][3][N*Na] (k, c, l)
+    unsigned long long* spec_diff = nullptr;    // device [2*spec_max]
+    unsigned long long* spec_hdiff = nullptr;   // pinned host [2*spec_max]
     // timing of the dominant kernel
     bool timing = false, count_hits = false;
     std::vector<hipEvent_t> ev_start, ev_stop;
@@ -62,11 +71,20 @@ struct aiy_ws {
     double tot_ms = 0;
     int64_t launches = 0;
 
+    void free_spec() {
+        void* ps[] = {spec_v, spec_idx, spec_pol, spec_diff};
+        for (void* p : ps)
+            if (p) (void)hipFree(p);
+        if (spec_hdiff) (void)hipHostFree(spec_hdiff);
+        spec_v = nullptr; spec_idx = nullptr; spec_pol = nullptr; spec_diff = nullptr;
+        spec_hdiff = nullptr; spec_n = 0;
+    }
     void free_all() {
         void* ps[] = {EV, T, T32, Dm, Dm8, Dt, Dm512, touched, best0, idx0, dis, kf, partial, diff, hitcount, trace, g0, g1, g2, gi,
                       d_key, d_head, d_wr, d_mass, d_part};
         for (void* p : ps)
             if (p) (void)hipFree(p);
+        free_spec();
         if (hdiff) (void)hipHostFree(hdiff);
         EV = nullptr; T = nullptr; T32 = nullptr; Dm = nullptr; Dm8 = nullptr; Dt = nullptr; Dm512 = nullptr; touched = nullptr; best0 = nullptr; dis = nullptr; kf = nullptr; kf_cap = 0;
         kf_ok = false;

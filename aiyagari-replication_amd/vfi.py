@@ -108,6 +108,11 @@ class Workspace:
         """Screen-kernel geometry (tuning; results identical), see aiy_ws_set_variant."""
         check(lib().aiy_ws_set_variant(self._h, ip(variant)))
 
+    def set_speculation(self, max_batch: int):
+        """Sweeps a solve enqueues between reads of max|dv| (0/1 = one sync per sweep);
+        results do not depend on it, see aiy_ws_set_speculation."""
+        check(lib().aiy_ws_set_speculation(self._h, ip(max_batch)))
+
     def set_search(self, coarse_stride=0, k_chunk=1024):
         check(lib().aiy_ws_set_search(self._h, ip(coarse_stride), ip(k_chunk)))
 

@@ -199,6 +199,11 @@ int aiy_ws_invalidate(aiy_ws* ws);
 /* search knobs (defaults tuned for gfx950): coarse stride for cold starts, k-chunk (a multiple
  * of 64: candidates a' per screen work item). */
 int aiy_ws_set_search(aiy_ws* ws, int coarse_stride, int k_chunk);
+/* VFI solves (A2, all tiers) enqueue up to max_batch sweeps between reads of max|v_new-v_old|
+ * (default 16; 0 or 1 = one synchronisation per sweep).  Sweeps past the stopping sweep are
+ * discarded, so iteration count, v_new, v_old and policies do not depend on it; memory:
+ * max_batch + 1 value buffers and max_batch policy sets per workspace. */
+int aiy_ws_set_speculation(aiy_ws* ws, int max_batch);
 /* screen-kernel shape (tuning only; results are identical).  bit 3 clear (default): the bound
  * tree screen, bit 0 = 2 states per lane (else 1), bits 1-2 = 1, 2, 4 or 8 cooperating waves
  * per tile, bit 4 = XCD-aware tile order.  bit 3 set: the chunked screen + merge, with

@@ -44,3 +44,30 @@ def test_sim_find_empty_is_an_error(pkg, gpu):
         pkg.sim_capital(np.zeros((2, 3)), np.array([0.0, 1.0, 2.0]), P, 1, 0.0,
                         np.array([0.99995]))
     assert e.value.status == "AIY_FIND_EMPTY"
+
+
+@pytest.mark.parametrize("N,Na,T", [(7, 400, 1), (7, 400, 2), (7, 400, 65), (7, 400, 4097),
+                                    (1, 50, 300), (3, 2, 300), (5, 37, 1000), (16, 300, 3000),
+                                    (15, 1100, 3000), (7, 3000, 2049)])
+def test_sim_chain_shapes_and_jumps(pkg, gpu, N, Na, T):
+    """Chain kernel edge cases vs the C restatement: T = 1, block/chunk boundaries (64, 2048),
+    tiny grids (Na < 64 window), N = 1 and the N = 16 wide-state path, and policies that jump
+    across the grid every step (the 64-point window misses, the full search runs)."""
+    rng = np.random.default_rng(N * 1000 + Na)
+    a = np.sort(rng.uniform(0, 50, Na))
+    a[0] = 0.0
+    P = rng.random((N, N)) + 0.05
+    P /= P.sum(axis=1, keepdims=True)
+    P[:, -1] += 1e-9  # rows sum above 1: find() never empty
+    for jumpy in (False, True):
+        if jumpy:
+            pol = rng.uniform(-5, 60, (N, Na))
+        else:
+            pol = np.sort(rng.uniform(0, a[-1], (N, Na)), axis=1)
+        U = rng.random(T - 1)
+        k1 = float(a[Na // 2])
+        Ks, path, zp = pkg.sim_capital(pol, a, P, N, k1, U, return_path=True)
+        Ko, po = corc.sim_capital(pol, a, P, N - 1, k1, U, return_path=True)
+        assert np.array_equal(path, po, equal_nan=True)
+        assert Ks == Ko or (np.isnan(Ks) and np.isnan(Ko))
+        assert zp.shape == (T,) and zp[0] == N and zp.min() >= 1 and zp.max() <= N
