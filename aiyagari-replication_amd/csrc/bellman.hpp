@@ -46,6 +46,7 @@ struct BellArgs {
     double* pl;  // A3 only (nullable)
     double* pc;
     unsigned long long* diff;  // nullable, [2]
+    unsigned long long* fold;  // nullable [2]: the table kernel folds the previous sweep's diff slots here
 };
 
 int launch_bell_table(const BellArgs& A, hipStream_t st);

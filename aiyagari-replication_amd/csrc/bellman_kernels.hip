@@ -121,19 +121,36 @@ __device__ __forceinline__ double table_D(double ev, int np) {
 // 2-D grid (x: 512 candidates of a row, y: row i).  Besides EV and the (a_k, D_k) pairs the
 // kernel writes the screening bounds: the maxima of D over aligned 8-, 64- and 512-candidate
 // blocks of the row (lane butterflies, then LDS across the block's 8 waves).  Block (0, 0)
-// clears the diff slots of the coming sweep.
+// clears the diff slots of the coming sweep — after folding the previous sweep's slots into
+// fold[0..1] when asked (the speculative solve's per-sweep diff, without a reduce launch).
 constexpr int kTableBlock = 512;
 __global__ __launch_bounds__(kTableBlock) void bell_table_kernel(
     int N, int Na, const double* __restrict__ P, const double* __restrict__ V, double beta,
     int np, const double* __restrict__ a, double* __restrict__ EV, double2* __restrict__ T,
     float* __restrict__ T32, int CK, double* __restrict__ Dm, double* __restrict__ Dm8,
     double* __restrict__ Dm512, int nb, int nb8, int nb512,
-    unsigned long long* __restrict__ diff, double* __restrict__ Dt) {
+    unsigned long long* __restrict__ diff, double* __restrict__ Dt,
+    unsigned long long* __restrict__ fold) {
     __shared__ double s_max[kTableBlock / 64];
     const int i = blockIdx.y;
     const int k = blockIdx.x * kTableBlock + threadIdx.x;
-    if (diff && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2 * kDiffSlots)
-        diff[threadIdx.x] = 0ull;
+    if (diff && blockIdx.x == 0 && blockIdx.y == 0) {  // block-uniform branch
+        if (fold && threadIdx.x < 64) {  // same fold as reduce_slots_kernel
+            const int l = threadIdx.x;
+            unsigned long long m = diff[2 * l];
+            const int any = __ballot(diff[2 * l + 1] != 0ull) != 0ull;
+            for (int off = 32; off > 0; off >>= 1) {
+                unsigned long long o = __shfl_xor(m, off);
+                m = o > m ? o : m;
+            }
+            if (l == 0) {
+                fold[0] = m;
+                fold[1] = any ? 1ull : 0ull;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < 2 * kDiffSlots) diff[threadIdx.x] = 0ull;
+    }
     const bool ok = k < Na;
     double D = -__builtin_inf();
     if (ok) {
@@ -1027,7 +1044,7 @@ int launch_bell_table(const BellArgs& A, hipStream_t st) {
     bell_table_kernel<<<grid, kTableBlock, 0, st>>>(
         A.N, A.Na, A.P, A.v_old, A.beta, A.np, A.a, A.EV, scr ? A.T : nullptr,
         scr ? A.T32 : nullptr, A.CK, scr ? A.Dm : nullptr, scr ? A.Dm8 : nullptr,
-        scr ? A.Dm512 : nullptr, A.nb, A.nb8, A.nb512, A.diff, scr ? A.Dt : nullptr);
+        scr ? A.Dm512 : nullptr, A.nb, A.nb8, A.nb512, A.diff, scr ? A.Dt : nullptr, A.fold);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }

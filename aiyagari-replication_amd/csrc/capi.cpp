@@ -171,6 +171,7 @@ int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
     A.pl = c.pl;
     A.pc = c.pc;
     A.diff = ws->diff;
+    A.fold = (unsigned long long*)c.prev_diff_out;
     if (c.labor) AIY_TRY(launch_disutility(c.L, (int)c.Nl, c.psi, c.eta, ws->dis, st));
     // feasible prefixes: cached while (r, w, a, s, L) are unchanged (aiy_ws_invalidate resets)
     size_t kf_need = (size_t)A.Nl * A.N * A.Na;
@@ -276,7 +277,10 @@ static int bell_solve_spec(aiy_ws* ws, BellCall c, double* v_a, double* v_b, dou
             c.pk = upk ? pslot(g, 0) : nullptr;
             c.pc = upc ? pslot(g, 1) : nullptr;
             c.pl = upl ? pslot(g, 2) : nullptr;
-            c.diff_out = reinterpret_cast<double*>(ws->spec_diff + 2 * t);  // {bits, any}
+            // sweep t's {max bits, any} lands in slot t: folded by sweep t+1's table kernel,
+            // or by a reduce launch after the batch's last sweep
+            c.prev_diff_out = t ? ws->spec_diff + 2 * (t - 1) : nullptr;
+            c.diff_out = (t == m - 1) ? reinterpret_cast<double*>(ws->spec_diff + 2 * t) : nullptr;
             AIY_TRY(bell_sweep_dev(ws, c, st));
         }
         AIY_HIP(hipMemcpyAsync(ws->spec_hdiff, ws->spec_diff,

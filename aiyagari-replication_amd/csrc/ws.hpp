@@ -115,6 +115,7 @@ struct BellCall {
     double* pl = nullptr;
     double* pc = nullptr;
     double* diff_out = nullptr;
+    void* prev_diff_out = nullptr;  // [2] u64: the previous sweep's folded {max bits, any}
 };
 int ws_ensure_bell(aiy_ws* ws, size_t partial_slots);
 int ws_timing_begin(aiy_ws* ws, hipStream_t st);
