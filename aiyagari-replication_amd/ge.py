@@ -181,3 +181,113 @@ def aiyagari_labor_egm(Na=400, T=10000, tol=1e-5, max_iter=1000, supply="mc", ph
                        theta=1.0):
     """Aiyagari_Endogenous_Labor_EGM.m."""
     return _egm_common(True, Na, T, tol, max_iter, supply, phi, theta)
+
+
+def aiyagari_vfi_overlapped(Na=400, rho=0.75, sigma_e=0.75, shocks="tauchen", T=10000, tol=1e-5,
+                            max_iter=1000, r0=0.04, max_r_iter=10, r_tol=1e-5):
+    """Aiyagari_VFI.m's computation (as `aiyagari_vfi`, supply = MC) with the bisection's
+    serial Monte-Carlo chain taken off the critical path.  Step j needs K_s(r_j) only to pick
+    the next midpoint, and both candidates warm-start from the same v_old(r_j): so while the
+    chain for r_j runs (one CU), the solves at both possible next midpoints run beside it on
+    their own streams and workspaces (device tier, one host thread each; ctypes drops the GIL),
+    and the chain's K_s selects one.  Every solve and chain is the one the sequential loop runs,
+    on the same inputs and uniform block, so r_history / k_supply / iters are identical
+    (tests/test_ge_gpu.py); the discarded solve is spare GPU work."""
+    import concurrent.futures as cf
+
+    import torch
+
+    from .sim import sim_capital_dev
+    from .vfi import Workspace
+
+    t0 = time.perf_counter()
+    cal = cb.aiyagari(Na=Na, rho=rho, sigma_e=sigma_e, shocks=shocks)
+    a, s, P, N = cal["a_grid"], cal["s"], cal["P"], cal["N"]
+    st = _Stream(T, max_r_iter)
+    z1 = int(math.ceil(N * st.take(1)[0]))
+    k1 = float(a[int(math.ceil(Na * st.take(1)[0])) - 1])
+    dev = torch.device("cuda", torch.cuda.current_device())
+    tt = lambda x: torch.as_tensor(np.ascontiguousarray(x, dtype=np.float64), device=dev)
+    a_t, s_t, P_t = tt(a), tt(s), tt(P)
+    U = tt(st.u[st.pos:])  # block j (the j-th chain's T-1 draws) = U[j(T-1) : (j+1)(T-1)]
+
+    class _Slot:
+        def __init__(self):
+            self.ws = Workspace(N, Na)
+            self.stream = torch.cuda.Stream(device=dev)
+            self.va = torch.zeros((N, Na), dtype=torch.float64, device=dev)
+            self.vb = torch.zeros_like(self.va)
+            self.idx = torch.zeros((N, Na), dtype=torch.int32, device=dev)
+            self.pk, self.pc = torch.empty_like(self.va), torch.empty_like(self.va)
+            self.v_old = None
+
+        def solve(self, v_init, r):
+            with torch.cuda.stream(self.stream):
+                self.va.copy_(v_init)
+                self.vb.zero_()
+                it, which = self.ws.vfi_solve(
+                    self.va, self.vb, a_t, s_t, P_t, r, cb.wage(r, cal["alpha"], cal["delta"]),
+                    cal["beta"], cal["sigma"], tol, max_iter, self.idx, self.pk, self.pc,
+                    stream=self.stream)
+                self.stream.synchronize()
+            self.v_old = self.vb if which == 0 else self.va
+            return it
+
+    sim_ws = Workspace(N, Na)
+    sim_stream = torch.cuda.Stream(device=dev)
+    k_out = torch.zeros(1, dtype=torch.float64, device=dev)
+    k_status = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def chain(slot, j):
+        with torch.cuda.stream(sim_stream):
+            sim_capital_dev(sim_ws, slot.pk, a_t, P_t, z1 - 1, k1, U[j * (T - 1):(j + 1) * (T - 1)],
+                            k_out, k_status, stream=sim_stream)
+            sim_stream.synchronize()
+        if int(k_status.item()) != 0:
+            raise RuntimeError("find() empty in the capital-supply chain (Aiyagari_VFI.m:106)")
+        return float(k_out.item())
+
+    slots = [_Slot(), _Slot(), _Slot()]
+    cur = slots[0]
+    out = dict(r_history=[], k_supply=[], k_demand=[], iters=[])
+    r_low, r_high = -0.05, 1 / cal["beta"] - 1
+    with cf.ThreadPoolExecutor(max_workers=3) as pool:
+        it0 = cur.solve(torch.zeros((N, Na), dtype=torch.float64, device=dev), r0)
+        r = (r_low + r_high) / 2
+        # the chain at r0 (its K_s is not used by the bisection) beside the first midpoint
+        f_chain = pool.submit(chain, cur, 0)
+        nxt = slots[1]
+        it = nxt.solve(cur.v_old, r)
+        f_chain.result()
+        cur, spare = nxt, [slots[0], slots[2]]
+        for j in range(1, max_r_iter + 1):
+            last = j == max_r_iter
+            r_lo_next, r_hi_next = (r_low + r) / 2, (r + r_high) / 2  # Ks > Kd : else
+            f_chain = pool.submit(chain, cur, j)
+            if not last:
+                f_lo = pool.submit(spare[0].solve, cur.v_old, r_lo_next)
+                f_hi = pool.submit(spare[1].solve, cur.v_old, r_hi_next)
+            Ks = f_chain.result()
+            Kd = cb.capital_demand(r, cal["labor"], cal["alpha"], cal["delta"])
+            out["r_history"].append(r); out["k_supply"].append(Ks); out["k_demand"].append(Kd)
+            out["iters"].append(it)
+            if not last:
+                it_lo, it_hi = f_lo.result(), f_hi.result()
+            if last or abs(Ks - Kd) < r_tol:
+                break
+            if Ks > Kd:
+                r_high = r
+                r, it, chosen, other = r_lo_next, it_lo, spare[0], spare[1]
+            else:
+                r_low = r
+                r, it, chosen, other = r_hi_next, it_hi, spare[1], spare[0]
+            spare = [cur, other]
+            cur = chosen
+    out["r"] = out["r_history"][-1]
+    out["iters"] = [it0] + out["iters"]
+    out["wall_s"] = time.perf_counter() - t0
+    out["cal"] = cal
+    for sl in slots:
+        sl.ws.close()
+    sim_ws.close()
+    return out

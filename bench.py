@@ -79,8 +79,12 @@ def ge_wall(pkg, threads):
     from oracle import corc
     from oracle import np_oracle as no
     pkg.ge.aiyagari_vfi(max_iter=5)  # warm the library / context (not timed)
+    pkg.ge.aiyagari_vfi_overlapped(max_iter=5)
     t0 = time.perf_counter()
-    out = pkg.ge.aiyagari_vfi()
+    seq = pkg.ge.aiyagari_vfi()
+    seq_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    out = pkg.ge.aiyagari_vfi_overlapped()
     gpu_s = time.perf_counter() - t0
     corc.num_threads(threads)
     cal = no.calib_aiyagari()
@@ -90,6 +94,9 @@ def ge_wall(pkg, threads):
     return {"workload": "Aiyagari_VFI.m defaults (configs[0]): initial VFI + 10-step bisection + MC",
             "r_gpu": out["r"], "r_cpu": H["r_final"], "identical_trace": out["r_history"] == H["r"],
             "sweeps": int(sum(out["iters"])), "wall_s_gpu": gpu_s, "wall_s_cpu": cpu_s,
+            "driver": "ge.aiyagari_vfi_overlapped (MC chain beside both next solves)",
+            "wall_s_gpu_sequential": seq_s, "sequential_trace_equal": seq["r_history"] == out["r_history"]
+            and seq["k_supply"] == out["k_supply"] and seq["iters"] == out["iters"],
             "cpu_cores": threads, "cpu_kind": "port (oracle/aiy_oracle.c)"}
 
 

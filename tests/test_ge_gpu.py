@@ -22,6 +22,23 @@ def test_ge_vfi_matches_golden_trace(pkg, gpu, golden):
     assert out["r"] == float(g["r_final"])
 
 
+def test_ge_vfi_overlapped_matches_golden_trace(pkg, gpu, golden):
+    """The overlapped driver (chain beside both speculative next solves) runs the same solves
+    and chains: the trace equals the golden one and the sequential driver's."""
+    g = golden("a11_ge_vfi_defaults")
+    out = pkg.ge.aiyagari_vfi_overlapped()
+    assert out["r_history"] == list(g["r_history"])
+    assert out["k_supply"] == list(g["k_supply"])
+    assert out["iters"] == list(g["iters"])
+    assert out["r"] == float(g["r_final"])
+    # a shorter bisection and a tighter grid: still identical to the sequential driver
+    kw = dict(Na=300, T=3000)
+    seq = pkg.ge.aiyagari_vfi(**kw)
+    ovl = pkg.ge.aiyagari_vfi_overlapped(**kw)
+    for key in ("r_history", "k_supply", "k_demand", "iters", "r"):
+        assert ovl[key] == seq[key], key
+
+
 def _oracle_ge(cal, solve_at_factory, policy_of, vfi_layout, T=10000):
     U = no.matlab_rand_stream(2 + (T - 1) * 11)
     N, Na, a, P = cal["N"], cal["Na"], cal["a_grid"], cal["P"]
