@@ -124,7 +124,7 @@ __device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v,
     return ((unsigned long long)hi << 32) | lo;
 }
 
-template <bool LDS>
+template <bool LDS, bool PATH>
 __global__ __launch_bounds__(256) void sim_chain_kernel(SimArgs A) {
     extern __shared__ double lds[];
     __shared__ unsigned long long F[kSimChunk];
@@ -138,14 +138,17 @@ __global__ __launch_bounds__(256) void sim_chain_kernel(SimArgs A) {
     const double* pol = A.pol;
     size_t zs = A.zs, as = A.as;
     if constexpr (LDS) {
-        for (int k = tid; k < Na; k += 256) lds[k] = A.a[k];
-        for (int q = tid; q < N * Na; q += 256) {
-            int zz = q / Na, kk = q - zz * Na;
-            lds[Na + q] = A.pol[(size_t)zz * A.zs + (size_t)kk * A.as];
+        // rows padded by 64 so a window [w0, w0 + 64] never needs clamping (w0 <= Na - 64, or
+        // 0 when Na < 64): the pads are read only by lanes that are never selected
+        const int S = Na + 64;
+        for (int k = tid; k < S; k += 256) lds[k] = A.a[min(k, Na - 1)];
+        for (int q = tid; q < N * S; q += 256) {
+            int zz = q / S, kk = q - zz * S;
+            lds[S + q] = kk < Na ? A.pol[(size_t)zz * A.zs + (size_t)kk * A.as] : 0.0;
         }
         a = lds;
-        pol = lds + Na;
-        zs = Na;
+        pol = lds + S;
+        zs = S;
         as = 1;
     }
     if (tid == 0) {  // cumulative transition rows, sequential sums as cumsum does
@@ -170,7 +173,7 @@ __global__ __launch_bounds__(256) void sim_chain_kernel(SimArgs A) {
     int t_last = 0;
     auto flush = [&](int t) {
         const int base = t & ~63;
-        if (base + lane <= t) {
+        if (PATH && base + lane <= t) {
             if (A.sim_k) A.sim_k[base + lane] = kbuf;
             if (A.sim_z) A.sim_z[base + lane] = zbuf;
         }
@@ -205,7 +208,7 @@ __global__ __launch_bounds__(256) void sim_chain_kernel(SimArgs A) {
                 // ---- window round: every lane evaluates its own segment (indices clamped so
                 // the loads need no exec masking; lanes past the grid are never selected)
                 const int p = w0 + lane;
-                const int p0 = min(p, Na - 1), p1 = min(p + 1, Na - 1);
+                const int p0 = LDS ? p : min(p, Na - 1), p1 = LDS ? p + 1 : min(p + 1, Na - 1);
                 const double x0 = a[p0], x1 = a[p1];
                 const double y0 = y[(size_t)p0 * as], y1 = y[(size_t)p1 * as];
                 const int cnt = __popcll(__ballot(p < Na && x0 <= k));
@@ -244,12 +247,14 @@ __global__ __launch_bounds__(256) void sim_chain_kernel(SimArgs A) {
                 w0 = seg - 31;
                 w0 = w0 < 0 ? 0 : (w0 > wmax ? wmax : w0);
                 sum += k;
-                if (lane == (t & 63)) {
-                    kbuf = k;
-                    zbuf = z;
+                if constexpr (PATH) {  // the path is only kept when sim_k / sim_z are asked for
+                    if (lane == (t & 63)) {
+                        kbuf = k;
+                        zbuf = z;
+                    }
+                    t_last = t;
+                    if ((t & 63) == 63) flush(t);
                 }
-                t_last = t;
-                if ((t & 63) == 63) flush(t);
             }
             if (status && lane == 0) stop_flag = 1;
         }
@@ -257,7 +262,7 @@ __global__ __launch_bounds__(256) void sim_chain_kernel(SimArgs A) {
         if (stop_flag) break;
     }
     if (wave == 0) {
-        if ((t_last & 63) != 63) flush(t_last);
+        if (PATH && (t_last & 63) != 63) flush(t_last);
         if (lane == 0) {
             A.out[0] = sum / (double)A.T;  // mean(sim_k)
             A.status[0] = status;
@@ -269,10 +274,15 @@ int launch_sim_capital(const SimArgs& A, hipStream_t st) {
     if (A.N > 16 || A.N < 1) return fail(AIY_BAD_SHAPE, "simulation supports 1 <= N <= 16");
     const long long need = (long long)A.Na * (A.N + 1);
     if (A.N <= 15) {
-        if (need <= kSimChainLdsMax)
-            sim_chain_kernel<true><<<1, 256, sizeof(double) * need, st>>>(A);
-        else
-            sim_chain_kernel<false><<<1, 256, 0, st>>>(A);
+        const long long need_pad = (long long)(A.Na + 64) * (A.N + 1);
+        const bool path = A.sim_k || A.sim_z;
+        if (need_pad <= kSimChainLdsMax) {
+            if (path) sim_chain_kernel<true, true><<<1, 256, sizeof(double) * need_pad, st>>>(A);
+            else sim_chain_kernel<true, false><<<1, 256, sizeof(double) * need_pad, st>>>(A);
+        } else {
+            if (path) sim_chain_kernel<false, true><<<1, 256, 0, st>>>(A);
+            else sim_chain_kernel<false, false><<<1, 256, 0, st>>>(A);
+        }
     } else if (need <= kSimLdsMax) {
         sim_capital_kernel<true><<<1, 64, sizeof(double) * need, st>>>(A);
     } else {

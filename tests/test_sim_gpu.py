@@ -71,3 +71,17 @@ def test_sim_chain_shapes_and_jumps(pkg, gpu, N, Na, T):
         assert np.array_equal(path, po, equal_nan=True)
         assert Ks == Ko or (np.isnan(Ks) and np.isnan(Ko))
         assert zp.shape == (T,) and zp[0] == N and zp.min() >= 1 and zp.max() <= N
+
+
+@pytest.mark.parametrize("Na", [60, 400, 2100, 20000])
+def test_sim_mean_only(pkg, gpu, Na):
+    """K_s without the path (the GE drivers' call: no sim_k/sim_z stores), LDS-padded and L2
+    variants, vs the C restatement."""
+    cal = no.calib_aiyagari(Na=Na, shocks="rouwenhorst")
+    a, P = cal["a_grid"], cal["P"]
+    rng = np.random.default_rng(Na + 1)
+    pol = np.sort(rng.uniform(0, a[-1], (7, Na)), axis=1)
+    U = rng.random(9999)
+    Ks = pkg.sim_capital(pol, a, P, 4, float(a[Na // 3]), U)
+    Ko = corc.sim_capital(pol, a, P, 3, float(a[Na // 3]), U)
+    assert Ks == Ko
