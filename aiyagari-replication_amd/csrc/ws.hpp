@@ -13,7 +13,7 @@ struct aiy_ws {
     // search knobs (aiy_ws_set_search)
     int coarse = 512;
     int CK = 1024;
-    int variant = 0;
+    int variant = -1;  // -1: by size (see bell_sweep_dev)
     // VFI scratch
     double* EV = nullptr;
     double2* T = nullptr;

@@ -208,7 +208,8 @@ int aiy_ws_set_speculation(aiy_ws* ws, int max_batch);
  * tree screen, bit 0 = 2 states per lane (else 1), bits 1-2 = 1, 2, 4 or 8 cooperating waves
  * per tile, bit 4 = XCD-aware tile order.  bit 3 set: the chunked screen + merge, with
  * bit 0 = 4 states per lane (else 2), bit 1 = registers capped for 8 waves per SIMD, bit 2 =
- * fp64-only screen (else the packed fp32 pre-screen with directed-rounding bounds first). */
+ * fp64-only screen (else the packed fp32 pre-screen with directed-rounding bounds first).
+ * -1 (default): chosen by size — 2 cooperating waves per tile for Na <= 4096, else 0. */
 int aiy_ws_set_variant(aiy_ws* ws, int variant);
 
 /* A1 on device.  hint (nullable, [N][Na] int32 0-based) = previous sweep's argmax; the result
