@@ -324,8 +324,16 @@ int bell_solve_dev(aiy_ws* ws, BellCall c, double* v_a, double* v_b, double tol,
                    int64_t max_iter, int64_t* iters, int* out_new, hipStream_t st) {
     if (max_iter < 1) return fail(AIY_BAD_ARG, "max_iter must be >= 1");
     if (!c.idx) return fail(AIY_BAD_ARG, "NULL device pointer");
-    if (ws && ws->spec_max > 1 && !c.diff_out)
-        return bell_solve_spec(ws, c, v_a, v_b, tol, max_iter, iters, out_new, st);
+    if (ws && ws->spec_max > 1 && !c.diff_out) {
+        // rings: (spec_max + 1) value buffers + spec_max sets of idx and 3 policies
+        const size_t n = (size_t)ws->N * ws->Na;
+        const size_t bytes = ((size_t)ws->spec_max * 4 + 1) * n * sizeof(double);
+        if (bytes <= ((size_t)8 << 30)) {
+            int rc = bell_solve_spec(ws, c, v_a, v_b, tol, max_iter, iters, out_new, st);
+            if (rc != AIY_NO_MEMORY) return rc;
+            ws->free_spec();  // no room for the rings: one synchronisation per sweep instead
+        }
+    }
     double* cur = v_a;
     double* nxt = v_b;
     const int* first_hint = c.hint;
