@@ -21,6 +21,7 @@ struct KsArgs {
     const KsSlice* slice;  // [s][K]
     double beta, k_min, k_max, tol;
     int howard, max_vfi;
+    int* seg_hint;  // nullable [node]: k-segment of clamp(k_opt), written by improve, a hint for Howard
 };
 struct KsParams {  // the 13-double parameter block, in order
     double beta, alpha, delta, k_min, k_max, ug, ub, l_bar, mu, z1, z2, e1, e2;

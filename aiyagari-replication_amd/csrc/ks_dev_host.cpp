@@ -25,6 +25,7 @@ struct ks_dev {
     int* cols = nullptr;   // value columns (s*nK + K) this shard reads: own and K'_idx targets
     int ncols = 0;
     unsigned long long* slots = nullptr;
+    int* seg = nullptr;    // [node] segment hints: improve writes them, Howard checks and uses them
 };
 
 namespace aiy {
@@ -40,6 +41,7 @@ static KsArgs shard_args(const ks_dev* h, int s) {
     A.beta = h->beta;
     A.k_min = h->k_min;
     A.k_max = h->k_max;
+    A.seg_hint = h->seg;
     return A;
 }
 }  // namespace aiy
@@ -50,7 +52,7 @@ extern "C" {
 
 int ks_dev_destroy(ks_dev* h) {
     if (!h) return AIY_OK;
-    void* ps[] = {h->kg, h->P, h->sl, h->dV, h->cols, h->slots};
+    void* ps[] = {h->kg, h->P, h->sl, h->dV, h->cols, h->slots, h->seg};
     for (void* q : ps)
         if (q) (void)hipFree(q);
     delete h;
@@ -97,6 +99,8 @@ int ks_dev_create(const double* k_grid, const double* K_grid, const double* B, c
     if (e == hipSuccess) e = hipMalloc((void**)&h->dV, n * sizeof(double));
     if (e == hipSuccess) e = hipMalloc((void**)&h->cols, cols.size() * sizeof(int));
     if (e == hipSuccess) e = hipMalloc((void**)&h->slots, 2 * kDiffSlots * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc((void**)&h->seg, n * sizeof(int));
+    if (e == hipSuccess) e = hipMemset(h->seg, 0, n * sizeof(int));
     if (e == hipSuccess) e = hipMemcpy(h->kg, k_grid, nk * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->P, Pr, sizeof Pr, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->sl, sl.data(), sl.size() * sizeof(KsSlice), hipMemcpyHostToDevice);

@@ -31,11 +31,24 @@ struct KsView {  // where the value/slope columns and the grid live (LDS or glob
     const double* dV;
 };
 
+// seg_of_dev(x, n, q) given a guess g: the guess is accepted only where it is provably the
+// search's answer (largest j <= n-2 with x[j] <= q, else 0; x non-decreasing), so a stale or
+// garbage hint costs a search, never a different result.
+__device__ __forceinline__ int seg_hinted_dev(const double* __restrict__ x, int n, double q,
+                                              int g) {
+    g = g < 0 ? 0 : (g > n - 2 ? n - 2 : g);
+    const bool lo_ok = g == 0 || x[g] <= q;
+    const bool hi_ok = g == n - 2 || q < x[g + 1];
+    if (lo_ok && hi_ok && q == q) return g;
+    return seg_of_dev(x, n, q);
+}
+
 __device__ __forceinline__ double ks_bellman_dev(const KsArgs& A, const KsView& W,
-                                                 const KsSlice& sl, int si, double k, double kp) {
+                                                 const KsSlice& sl, int si, double k, double kp,
+                                                 int hint = -1) {
     const int nk = A.nk;
     double kq = fmax(fmin(kp, W.kg[nk - 1]), W.kg[0]);
-    int seg = seg_of_dev(W.kg, nk, kq);
+    int seg = hint >= 0 ? seg_hinted_dev(W.kg, nk, kq, hint) : seg_of_dev(W.kg, nk, kq);
     double expec = 0;
 #pragma unroll
     for (int sn = 0; sn < 4; ++sn) {
@@ -140,7 +153,7 @@ __device__ __forceinline__ double howard_node(const KsArgs& A, const KsView& W, 
     int ki, Ki, si;
     node_coords(A, n, ki, Ki, si);
     const KsSlice sl = A.slice[si * A.nK + Ki];
-    return ks_bellman_dev(A, W, sl, si, W.kg[ki], kp);
+    return ks_bellman_dev(A, W, sl, si, W.kg[ki], kp, A.seg_hint ? A.seg_hint[n] : -1);
 }
 
 // ------------------------------------------------------------------------------ tiled
@@ -171,8 +184,11 @@ __global__ void ks_improve_kernel(KsArgs A, const double* __restrict__ V,
     int n = A.node0 + t;
     KsView W{A.k_grid, V, dV};
     int nf = 0;
-    k_opt[n] = improve_node(A, W, n, &nf);
+    const double kp = improve_node(A, W, n, &nf);
+    k_opt[n] = kp;
     if (nfev) nfev[n] = nf;
+    if (A.seg_hint)  // the segment Howard's 50 sweeps will evaluate this k_opt in
+        A.seg_hint[n] = seg_of_dev(A.k_grid, A.nk, fmax(fmin(kp, A.k_grid[A.nk - 1]), A.k_grid[0]));
 }
 
 __global__ void ks_howard_kernel(KsArgs A, const double* __restrict__ V,
