@@ -57,6 +57,7 @@ void ks_slices(const KsParams& p, const double* B, const double* K_grid, int nK,
 struct KsDev {
     double *kg, *P, *V, *V2, *dV, *Vold, *kopt;
     int* nfev;
+    int* seg;  // Howard segment hints (verified before use, so never initialised)
     KsSlice* sl;
     KsOut* out;
     unsigned long long* slots;
@@ -82,6 +83,7 @@ static int ks_stage(HostCtx* c, const double* value, const double* k_opt, const 
     AIY_TRY(c->buf("ks_Vold", nb, (void**)&D.Vold));
     AIY_TRY(c->buf("ks_kopt", nb, (void**)&D.kopt));
     AIY_TRY(c->buf("ks_nfev", n * sizeof(int), (void**)&D.nfev));
+    AIY_TRY(c->buf("ks_seg", n * sizeof(int), (void**)&D.seg));
     AIY_TRY(c->buf("ks_sl", sl.size() * sizeof(KsSlice), (void**)&D.sl));
     AIY_TRY(c->buf("ks_out", sizeof(KsOut), (void**)&D.out));
     AIY_TRY(c->buf("ks_slots", 2 * kDiffSlots * sizeof(unsigned long long), (void**)&D.slots));
@@ -98,6 +100,7 @@ static int ks_stage(HostCtx* c, const double* value, const double* k_opt, const 
     A.nk = (int)nk; A.nK = (int)nK; A.node0 = 0; A.n_local = (int)n;
     A.k_grid = D.kg; A.P = D.P; A.slice = D.sl;
     A.beta = p.beta; A.k_min = p.k_min; A.k_max = p.k_max;
+    A.seg_hint = D.seg;
     return AIY_OK;
 }
 
@@ -129,6 +132,7 @@ struct KsShard {
     std::vector<std::pair<int, int>> remote;  // (column, owner shard)
     double *kg = nullptr, *P = nullptr, *V = nullptr, *V2 = nullptr, *dV = nullptr,
            *Vold = nullptr, *kopt = nullptr;
+    int* seg = nullptr;              // Howard segment hints (verified before use)
     int* dcols = nullptr;
     KsSlice* sl = nullptr;
     unsigned long long* slots = nullptr;
@@ -163,7 +167,7 @@ static int ks_vfi_solve_multi_impl(double* value, double* k_opt, const double* k
     auto cleanup = [&]() {
         for (auto& sh : S) {
             (void)hipSetDevice(sh.dev);
-            void* ps[] = {sh.kg, sh.P, sh.V, sh.V2, sh.dV, sh.Vold, sh.kopt, sh.dcols, sh.sl, sh.slots};
+            void* ps[] = {sh.kg, sh.P, sh.V, sh.V2, sh.dV, sh.Vold, sh.kopt, sh.dcols, sh.sl, sh.slots, sh.seg};
             for (void* q : ps)
                 if (q) (void)hipFree(q);
             if (sh.done) (void)hipEventDestroy(sh.done);
@@ -213,6 +217,7 @@ static int ks_vfi_solve_multi_impl(double* value, double* k_opt, const double* k
         KS_CHECK(hipMalloc((void**)&sh.dV, nb));
         KS_CHECK(hipMalloc((void**)&sh.Vold, nb));
         KS_CHECK(hipMalloc((void**)&sh.kopt, nb));
+        KS_CHECK(hipMalloc((void**)&sh.seg, n * sizeof(int)));
         KS_CHECK(hipMalloc((void**)&sh.dcols, sh.cols.size() * sizeof(int) + 4));
         KS_CHECK(hipMalloc((void**)&sh.sl, sl.size() * sizeof(KsSlice)));
         KS_CHECK(hipMalloc((void**)&sh.slots, 2 * kDiffSlots * sizeof(unsigned long long)));
@@ -233,6 +238,7 @@ static int ks_vfi_solve_multi_impl(double* value, double* k_opt, const double* k
         A.n_local = (int)((sh.K1 - sh.K0) * nk);
         A.k_grid = sh.kg; A.P = sh.P; A.slice = sh.sl;
         A.beta = p.beta; A.k_min = p.k_min; A.k_max = p.k_max;
+        A.seg_hint = sh.seg;
         return A;
     };
     // peer copies of the columns each shard reads from others (after all shards finished)

@@ -331,7 +331,9 @@ bool ks_fused_fits(int nk, int nK) {
 
 int launch_ks_fused(const KsArgs& A, double* V, double* kopt, int* nfev, KsOut* out,
                     hipStream_t st) {
-    ks_fused_vfi_kernel<<<1, kFusedThreads, ks_fused_lds_bytes(A.nk, A.nK), st>>>(A, V, kopt,
+    KsArgs F = A;
+    F.seg_hint = nullptr;  // k_opt lives in registers here; the search runs in LDS anyway
+    ks_fused_vfi_kernel<<<1, kFusedThreads, ks_fused_lds_bytes(A.nk, A.nK), st>>>(F, V, kopt,
                                                                                   nfev, out);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
