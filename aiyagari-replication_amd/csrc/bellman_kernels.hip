@@ -643,9 +643,34 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A, int ntile
                     const int hk = min(h / Nl, kf - 1);
                     const double coh = cash<LAB>(x[r], y, LAB ? A.L[hl] : 1.0);
                     const double dis = LAB ? A.dis[hl] : 0.0;
-                    for (int k = max(hk - 1, 0); k <= min(hk + 1, kf - 1); ++k)
-                        lexi_take(bell_val<NP, LAB>(coh - a[k], ev[k], A.sigma, dis), hl + Nl * k,
-                                  best[r], idx[r]);
+                    auto take = [&](int k) __attribute__((always_inline)) {
+                        return lexi_take(bell_val<NP, LAB>(coh - a[k], ev[k], A.sigma, dis),
+                                         hl + Nl * k, best[r], idx[r]);
+                    };
+                    for (int k = max(hk - 1, 0); k <= min(hk + 1, kf - 1); ++k) take(k);
+                    // Climb: when a neighbour of the hint beats it, the optimum has moved (early
+                    // sweeps; the sweep after a cold start moves it by thousands of candidates).
+                    // Doubling steps while the value improves, then halving steps around the
+                    // best point: for a unimodal objective this lands on the maximiser in
+                    // O(log distance) exact evaluations instead of the tree raising the bar
+                    // one passing candidate at a time.  Any candidate is a valid bar, so the
+                    // result does not depend on it (the tree below still proves the maximum).
+                    const int kb = idx[r] >= 0 ? idx[r] / Nl : hk;
+                    const int dir = kb > hk ? 1 : (kb < hk ? -1 : 0);
+                    if (dir != 0 && !(A.variant & 32)) {
+                        int k = kb, step = 2;
+                        for (;;) {
+                            const int kn = min(max(k + dir * step, 0), kf - 1);
+                            if (kn == k || !take(kn)) break;
+                            k = kn;
+                            step <<= 1;
+                        }
+                        for (int s2 = step >> 1; s2 >= 1; s2 >>= 1) {
+                            const int c0 = idx[r] / Nl;
+                            if (c0 + s2 < kf) take(c0 + s2);
+                            if (c0 - s2 >= 0) take(c0 - s2);
+                        }
+                    }
                 }
             }
         } else {

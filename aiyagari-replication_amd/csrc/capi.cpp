@@ -261,6 +261,21 @@ static int bell_solve_spec(aiy_ws* ws, BellCall c, double* v_a, double* v_b, dou
     double* const upc = c.pc;
     double* const upl = c.pl;
     int* const uidx = c.idx;
+    if (c.labor) {
+        // Labor_VFI.m:85: a state with no feasible choice keeps its incoming policies (the
+        // kernels do not write them).  The plain loop reuses the caller's buffers, so those
+        // entries stay the caller's; every ring slot starts as a copy of them to match
+        // (feasibility depends on (r, w, grids) only, so it is fixed within a solve).
+        for (int q = 0; q < Rp; ++q) {
+            AIY_HIP(hipMemcpyAsync(ws->spec_idx + (size_t)q * n, uidx, n * sizeof(int),
+                                   hipMemcpyDeviceToDevice, st));
+            double* const src[3] = {upk, upc, upl};
+            for (int p = 0; p < 3; ++p)
+                if (src[p])
+                    AIY_HIP(hipMemcpyAsync(ws->spec_pol + ((size_t)q * 3 + p) * n, src[p], vb,
+                                           hipMemcpyDeviceToDevice, st));
+        }
+    }
     int64_t done = 0, stop = 0;
     double d_prev = NAN, d_last = NAN;
     while (!stop && done < max_iter) {
@@ -469,7 +484,7 @@ int aiy_ws_invalidate(aiy_ws* ws) {
 
 int aiy_ws_set_variant(aiy_ws* ws, int variant) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
-    if (variant < -1 || variant > 31) return fail(AIY_BAD_ARG, "variant in [-1, 31]");
+    if (variant < -1 || variant > 127) return fail(AIY_BAD_ARG, "variant in [-1, 127]");
     ws->variant = variant;
     return AIY_OK;
 }

@@ -14,9 +14,13 @@ pass() {  # name, counters...
   echo "=== pmc $name rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 "$OUT/$name.log"; exit $rc; fi
 }
-pass sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU
-pass sq2 SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_ANY SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM_RD SQ_WAVES
-pass grbm GRBM_GUI_ACTIVE GRBM_COUNT
-pass fetch FETCH_SIZE
-pass write WRITE_SIZE
+for ps in ${PASSES:-sq sq2 grbm fetch write}; do
+  case $ps in
+    sq)    pass sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU ;;
+    sq2)   pass sq2 SQ_WAVES SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA ;;
+    grbm)  pass grbm GRBM_GUI_ACTIVE GRBM_COUNT ;;
+    fetch) pass fetch FETCH_SIZE ;;
+    write) pass write WRITE_SIZE ;;
+  esac
+done
 echo "=== pmc done"
