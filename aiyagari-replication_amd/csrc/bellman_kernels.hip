@@ -157,9 +157,9 @@ __global__ __launch_bounds__(kTableBlock) void bell_table_kernel(
         const size_t t = (size_t)i * Na + k;
         double acc = table_ev(N, Na, P, V, beta, i, k);
         EV[t] = acc;
-        if (T) {
+        if (T || Dt) {
             D = table_D(acc, np);
-            T[t] = make_double2(a[k], D);
+            if (T) T[t] = make_double2(a[k], D);
             if (Dt) Dt[t] = D;
             if (T32) {  // relative to the chunk origin (a, D at k0): small magnitudes, fine ulps
                 int k0 = k - k % CK;
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(kTableBlock) void bell_table_kernel(
             }
         }
     }
-    if (!T) return;  // uniform per launch
+    if (!T && !Dt) return;  // uniform per launch
     // block maxima (NaN keys drop out of fmax: a NaN candidate is never a maximiser)
     D = fmax(D, __shfl_xor(D, 1));
     D = fmax(D, __shfl_xor(D, 2));
@@ -770,7 +770,7 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A, int ntile
             double2 tk[8];
 #pragma unroll
             for (int kk = 0; kk < 8; ++kk)  // broadcast reads, all in flight together
-                tk[kk] = s_cand[wave][min(k0 + kk, k1 - 1) - sbase];
+                tk[kk] = s_cand[wave][k0 - sbase + kk];  // whole 64-block staged; kk >= k1 - k0 masked below
             double tmax[8];
 #pragma unroll
             for (int kk = 0; kk < 8; ++kk) {
@@ -785,6 +785,12 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A, int ntile
                         tm = (lin == idx[r]) ? tm : fmax(tm, t);
                     }
                 tmax[kk] = tm;
+            }
+            {  // one wave vote first: almost always no candidate passes
+                double tall = tmax[0];
+#pragma unroll
+                for (int kk = 1; kk < 8; ++kk) tall = fmax(tall, tmax[kk]);
+                if (!__any(tall >= kThr)) return;
             }
             unsigned vote = 0;
 #pragma unroll
@@ -822,13 +828,17 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A, int ntile
         // one superblock, blocks b with b % bstep == bsel: one round trip for the 64 sub-block
         // bounds, then all bound tests (v_readlane, no memory), then ONE round trip staging the
         // candidates of every passing block in LDS
-        auto superblock = [&](int sb, int bsel, int bstep) __attribute__((always_inline)) {
+        // the 64 sub-block bounds of superblock sb, one per lane (issued ahead of their use)
+        auto load8 = [&](int sb, double& dm8, double& a8) __attribute__((always_inline)) {
+            const int sub = (sb << 6) + lane;
+            const bool oku = sub < A.nb8;
+            dm8 = oku ? A.Dm8[(size_t)i * A.nb8 + sub] : -__builtin_inf();
+            a8 = oku ? a[sub << 3] : 0.0;
+        };
+        auto superblock = [&](int sb, int bsel, int bstep, double dm8, double a8)
+                              __attribute__((always_inline)) {
             stamp(0);
             const int sbase = sb << 9;  // first candidate of the superblock
-            const int sub = (sbase >> 3) + lane;
-            const bool oku = sub < A.nb8;
-            const double dm8 = oku ? A.Dm8[(size_t)i * A.nb8 + sub] : -__builtin_inf();
-            const double a8 = oku ? a[sub << 3] : 0.0;
             double dm64 = dm8;
             dm64 = fmax(dm64, __shfl_xor(dm64, 1));
             dm64 = fmax(dm64, __shfl_xor(dm64, 2));
@@ -880,17 +890,26 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A, int ntile
             const unsigned long long m = __ballot(hk >= 0);
             if (m) sfirst = min(readlane_i(hk, __builtin_ctzll(m)) >> 9, nsb - 1);
         }
+        // level-0 bounds of the first 64 superblocks, issued before the first superblock's
+        // work so that their latency overlaps it
+        double dm0, a0;
+        auto load512 = [&](int g) __attribute__((always_inline)) {
+            const int sbl = g + lane;
+            const bool oks = sbl < nsb;
+            dm0 = oks ? A.Dm512[(size_t)i * A.nb512 + sbl] : -__builtin_inf();
+            a0 = oks ? a[sbl << 9] : 0.0;
+        };
+        load512(0);
         if (sfirst >= 0) {  // (its bound would pass: it holds the bar's candidate)
             ++nsup;
-            superblock(sfirst, wave, W);
+            double d8, a8;
+            load8(sfirst, d8, a8);
+            superblock(sfirst, wave, W, d8, a8);
             exchange();
             set_B();
         }
         for (int g = 0; g < nsb; g += 64) {
-            const int sbl = g + lane;
-            const bool oks = sbl < nsb;
-            const double dm0 = oks ? A.Dm512[(size_t)i * A.nb512 + sbl] : -__builtin_inf();
-            const double a0 = oks ? a[sbl << 9] : 0.0;
+            if (g > 0) load512(g);
             const int ns = min(64, nsb - g);
             for (int s8 = 0; s8 < ns; s8 += 8) {  // superblock bounds eight at a time
                 const int cnt = min(8, ns - s8);
@@ -901,8 +920,19 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A, int ntile
                 }
                 if (!own) continue;
                 nsup += __builtin_popcount(own);
-                for (unsigned sm = mask8(dm0, a0, s8, 1, cnt) & own; sm; sm &= sm - 1)
-                    superblock(g + s8 + __builtin_ctz(sm), 0, 1);
+                unsigned sm = mask8(dm0, a0, s8, 1, cnt) & own;
+                if (!sm) continue;
+                // software pipeline: the next passing superblock's sub-block bounds load while
+                // this one's candidates are staged and screened
+                double pd, pa;
+                load8(g + s8 + __builtin_ctz(sm), pd, pa);
+                while (sm) {
+                    const int cur = g + s8 + __builtin_ctz(sm);
+                    sm &= sm - 1;
+                    const double d8 = pd, a8 = pa;
+                    if (sm) load8(g + s8 + __builtin_ctz(sm), pd, pa);
+                    superblock(cur, 0, 1, d8, a8);
+                }
             }
         }
     }
@@ -970,6 +1000,247 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A, int ntile
             atomicAdd(hc + 1, nsup * ns);
             atomicAdd(hc + 2, nblk * ns);
             if (nfine) atomicAdd(hc + 3, nfine * ns);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------ 3''. quad
+// The bound tree with four lanes per state (A1; the default for integer sigma).  A wave owns
+// 16 consecutive states of row i; lane = st + 16·q holds state st and is sub-lane q of it.
+// Every level of the tree splits its tests over the four sub-lanes — two of each group of eight
+// bounds (superblocks, 64-blocks, 8-blocks) and two of each eight candidates per sub-lane — so
+// one wave-instruction performs 64 state-tests where the one-lane-per-state tree performs 64
+// with a 4x wider union of argmax ranges over its 64 states.  Per-wave latency drops ~4x and
+// four times as many waves fill the SIMDs.  Candidates that pass are evaluated exactly by the
+// lane that tested them (no wave-uniform exact loop).  Each sub-lane keeps its own running
+// (best, first index); the bars are merged across the four sub-lanes between superblocks and
+// at the end with the same order-independent rule, so the result is the plain exhaustive
+// scan's bit for bit (the same exactness argument as the tree: every bound is an upper bound of
+// t_k over its block in floating point, and a candidate whose exact value reaches a lane's
+// running best passes that lane's test).
+template <int NP>
+__global__ __launch_bounds__(64) void bell_quad_kernel(BellArgs A, int ntile) {
+    const int lane = threadIdx.x & 63;
+    const int st = lane & 15, q4 = lane >> 4;
+    const int item = (A.variant & 16) ? xcd_remap((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+    const int tile = item % ntile;
+    const int i = item / ntile;
+    const int Na = A.Na;
+    const double* __restrict__ a = A.a;
+    const double* __restrict__ Drow = A.Dt + (size_t)i * Na;
+    const double* __restrict__ ev = A.EV + (size_t)i * Na;
+    const double y = A.w * A.s[i];
+    const int j = tile * 16 + st;
+    const bool ok = j < Na;
+    const size_t t = (size_t)i * Na + (ok ? j : 0);
+    __shared__ double2 s_cand[512];  // the current superblock's staged candidates (a_k, D_k)
+
+    const double x = ok ? (1 + A.r) * a[j] : 0.0;
+    const double coh = x + y;  // Aiyagari_VFI.m:72
+    const int kf = ok ? A.kf[t] : 0;
+    double best = __builtin_nan("");
+    int idx = -1;
+    unsigned nhits = 0, nsup = 0, nblk = 0, nfine = 0;
+    const long long t_start = A.trace ? (long long)wall_clock64() : 0;
+
+    // (max value, first index) over the four sub-lanes of each state
+    auto merge4 = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int off = 16; off <= 32; off <<= 1) {
+            const double ob = __shfl_xor(best, off);
+            const int oq = __shfl_xor(idx, off);
+            if (oq >= 0) lexi_take(ob, oq, best, idx);
+        }
+    };
+    auto evalk = [&](int k) __attribute__((always_inline)) {
+        return bell_val<NP, false>(coh - a[k], ev[k], A.sigma, 0.0);
+    };
+    if (A.hint) {
+        const int h = ok ? A.hint[t] : -1;
+        const int hk = (h >= 0 && kf > 0) ? min(h, kf - 1) : -1;
+        if (hk >= 0) {  // sub-lanes 0..2 evaluate hint-1, hint, hint+1
+            const int k = hk - 1 + q4;
+            if (q4 < 3 && k >= 0 && k < kf) lexi_take(evalk(k), k, best, idx);
+        }
+        merge4();
+        if (hk >= 0 && idx >= 0 && idx != hk && !(A.variant & 32)) {
+            // climb (see bell_tree_kernel), redundantly in the four sub-lanes
+            const int dir = idx > hk ? 1 : -1;
+            int k = idx, step = 2;
+            for (;;) {
+                const int kn = min(max(k + dir * step, 0), kf - 1);
+                if (kn == k || !lexi_take(evalk(kn), kn, best, idx)) break;
+                k = kn;
+                step <<= 1;
+            }
+            for (int s2 = step >> 1; s2 >= 1; s2 >>= 1) {
+                const int c0 = idx;
+                if (c0 + s2 < kf) lexi_take(evalk(c0 + s2), c0 + s2, best, idx);
+                if (c0 - s2 >= 0) lexi_take(evalk(c0 - s2), c0 - s2, best, idx);
+            }
+        }
+    } else if (ok) {
+        best = A.best0[t];
+        idx = A.idx0[t] == -2 ? -1 : A.idx0[t];
+    }
+    double B;
+    auto set_B = [&]() __attribute__((always_inline)) {
+        B = ok ? screen_B(best, idx, 0.0, NP) : __builtin_nan("");  // invalid: every test false
+    };
+    set_B();
+
+    int kg = kf;  // the wave's feasible range
+    for (int off = 1; off < 16; off <<= 1) kg = max(kg, __shfl_xor(kg, off));
+    kg = readfirst(kg);
+
+    // Eight bounds per call, two per sub-lane: position u = q4 + 4p (p = 0, 1) reads lane
+    // base + stride·u of (dv, av) = (Dmax, a at the block start).  Bit u of the result is set
+    // when some state passes bound u (u < cnt).
+    auto qmask8 = [&](double dv, double av, int base, int stride, int cnt, unsigned& ctr)
+                      __attribute__((always_inline)) {
+        double tm[2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int u = q4 + 4 * p;
+            const int ln = min(base + stride * u, 63);
+            const double dmax = __shfl(dv, ln), a0 = __shfl(av, ln);
+            const double tt = (dmax - B) * aiy_ipow(fmax(coh - a0, 0.0), NP);
+            tm[p] = u < cnt ? tt : -__builtin_inf();
+        }
+        if (A.hitcount && ok) ctr += (q4 < cnt) + (q4 + 4 < cnt);
+        const unsigned long long b0 = __ballot(tm[0] >= kThr), b1 = __ballot(tm[1] >= kThr);
+        unsigned m = 0;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            m |= ((b0 >> (16 * s)) & 0xffffull) ? 1u << s : 0u;
+            m |= ((b1 >> (16 * s)) & 0xffffull) ? 1u << (s + 4) : 0u;
+        }
+        return m;
+    };
+    // candidates [k0, k1), k1 - k0 <= 8, staged in LDS: sub-lane q4 tests k0 + 2·q4 + {0, 1};
+    // a candidate that passes is evaluated exactly by its own lane (MATLAB order) and merged
+    auto fine = [&](int sbase, int k0, int k1) __attribute__((always_inline)) {
+        double tm[2], cc[2];
+        int kk[2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            kk[p] = k0 + 2 * q4 + p;
+            const double2 tk = s_cand[min(kk[p], k1 - 1) - sbase];
+            cc[p] = coh - tk.x;
+            const double tt = (tk.y - B) * aiy_ipow(fmax(cc[p], 0.0), NP);
+            tm[p] = (kk[p] >= k1 || kk[p] == idx) ? -__builtin_inf() : tt;
+        }
+        if (A.hitcount && ok) nfine += (kk[0] < k1) + (kk[1] < k1);
+        if (!__any(tm[0] >= kThr || tm[1] >= kThr)) return;
+        bool upd = false;
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+            if (tm[p] >= kThr && cc[p] > 0) {
+                ++nhits;
+                upd |= lexi_take(bell_val<NP, false>(cc[p], ev[kk[p]], A.sigma, 0.0), kk[p], best, idx);
+            }
+        if (upd) set_B();
+    };
+    auto superblock = [&](int sb) __attribute__((always_inline)) {
+        const int sbase = sb << 9;
+        const int sub = (sbase >> 3) + lane;
+        const bool oku = sub < A.nb8;
+        const double dm8 = oku ? A.Dm8[(size_t)i * A.nb8 + sub] : -__builtin_inf();
+        const double a8 = oku ? a[sub << 3] : 0.0;
+        double dm64 = dm8;
+        dm64 = fmax(dm64, __shfl_xor(dm64, 1));
+        dm64 = fmax(dm64, __shfl_xor(dm64, 2));
+        dm64 = fmax(dm64, __shfl_xor(dm64, 4));
+        const int nblock = min(8, (kg - sbase + 63) >> 6);
+        const unsigned bpass = qmask8(dm64, a8, 0, 8, nblock, nblk);
+        unsigned long long pass = 0;  // bit 8b+u: sub-block u of block b passes
+        for (unsigned bm = bpass; bm; bm &= bm - 1) {
+            const int b = __builtin_ctz(bm);
+            const int nsub = min(8, (kg - (sbase + (b << 6)) + 7) >> 3);
+            pass |= (unsigned long long)qmask8(dm8, a8, 8 * b, 1, nsub, nblk) << (8 * b);
+        }
+        if (!pass) return;
+#pragma unroll
+        for (int b = 0; b < 8; ++b)  // all loads issued before any is used
+            if ((pass >> (8 * b)) & 0xffull) {
+                const int k = min(sbase + (b << 6) + lane, Na - 1);
+                s_cand[(b << 6) + lane] = make_double2(a[k], Drow[k]);
+            }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        for (unsigned long long pm = pass; pm; pm &= pm - 1) {
+            const int k0 = sbase + (__builtin_ctzll(pm) << 3);
+            fine(sbase, k0, min(k0 + 8, kg));
+        }
+        __builtin_amdgcn_wave_barrier();  // reads done before the next superblock's writes
+        merge4();
+        set_B();
+    };
+
+    if (kg > 0) {
+        const int nsb = (kg + 511) >> 9;
+        int sfirst = -1;  // best first: the superblock holding the first state's current argmax
+        {
+            const unsigned long long m = __ballot(idx >= 0);
+            if (m) sfirst = min(readlane_i(idx, __builtin_ctzll(m)) >> 9, nsb - 1);
+        }
+        if (sfirst >= 0) superblock(sfirst);
+        for (int g = 0; g < nsb; g += 64) {
+            const int sbl = g + lane;
+            const bool oks = sbl < nsb;
+            const double dm0 = oks ? A.Dm512[(size_t)i * A.nb512 + sbl] : -__builtin_inf();
+            const double a0 = oks ? a[sbl << 9] : 0.0;
+            const int ns = min(64, nsb - g);
+            for (int s8 = 0; s8 < ns; s8 += 8) {
+                const int cnt = min(8, ns - s8);
+                unsigned m = qmask8(dm0, a0, s8, 1, cnt, nsup);
+                if (sfirst >= g + s8 && sfirst < g + s8 + 8) m &= ~(1u << (sfirst - g - s8));
+                for (; m; m &= m - 1) superblock(g + s8 + __builtin_ctz(m));
+            }
+        }
+    }
+    merge4();
+
+    // outputs (sub-lane 0): Aiyagari_VFI.m:79-81
+    bool okd = false;
+    double dmax = 0.0;
+    if (ok && q4 == 0) {
+        double b = best;
+        int qq = idx;
+        if (qq < 0) {  // all candidates NaN: max returns NaN at index 1
+            qq = 0;
+            b = __builtin_nan("");
+        }
+        const double kp = a[qq];
+        A.idx[t] = qq;
+        if (A.pk) A.pk[t] = kp;
+        if (A.pc) A.pc[t] = coh - kp;
+        A.v_new[t] = b;
+        const double d = fabs(b - A.v_old[t]);
+        if (d == d) {
+            dmax = d;
+            okd = true;
+        }
+    }
+    block_max_to_slots(okd, dmax, A.diff);
+    if (A.hitcount || A.trace) {  // instrumentation: per-state test counts, summed over the wave
+        unsigned c4[4] = {nhits, nsup, nblk, nfine};
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            for (int off = 32; off > 0; off >>= 1) c4[c] += __shfl_xor(c4[c], off);
+        if (A.hitcount && lane == 0) {
+            unsigned long long* hc = A.hitcount + 4 * (blockIdx.x % kDiffSlots);
+            for (int c = 0; c < 4; ++c)
+                if (c4[c]) atomicAdd(hc + c, (unsigned long long)c4[c]);
+        }
+        if (A.trace && lane == 0) {
+            long long* tr = A.trace + 16 * (size_t)item;
+            tr[0] = t_start;
+            tr[1] = (long long)wall_clock64();
+            tr[2] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));  // HW_REG_XCC_ID
+            for (int c = 0; c < 4; ++c) tr[3 + c] = c4[(c + 1) & 3];
+            tr[7] = blockIdx.x;
+            for (int c = 8; c < 16; ++c) tr[c] = 0;
         }
     }
 }
@@ -1067,7 +1338,7 @@ int launch_bell_table(const BellArgs& A, hipStream_t st) {
     dim3 grid(cdiv(A.Na, kTableBlock), A.N);
     const bool scr = A.np > 0;
     bell_table_kernel<<<grid, kTableBlock, 0, st>>>(
-        A.N, A.Na, A.P, A.v_old, A.beta, A.np, A.a, A.EV, scr ? A.T : nullptr,
+        A.N, A.Na, A.P, A.v_old, A.beta, A.np, A.a, A.EV, (scr && !A.tree) ? A.T : nullptr,
         scr ? A.T32 : nullptr, A.CK, scr ? A.Dm : nullptr, scr ? A.Dm8 : nullptr,
         scr ? A.Dm512 : nullptr, A.nb, A.nb8, A.nb512, A.diff, scr ? A.Dt : nullptr, A.fold);
     AIY_HIP(hipGetLastError());
@@ -1136,6 +1407,13 @@ static void tree_w(const BellArgs& A, hipStream_t st) {
 }
 template <int NP, bool LAB>
 static void run_tree(const BellArgs& A, hipStream_t st) {
+    if constexpr (NP > 0 && !LAB) {
+        if (A.variant & 64) {  // four lanes per state, 16 states per wave
+            const int ntile = cdiv(A.Na, 16);
+            bell_quad_kernel<NP><<<A.N * ntile, 64, 0, st>>>(A, ntile);
+            return;
+        }
+    }
     if constexpr (NP > 0) {
         // the tuning geometries are instantiated for the reference sigma = 5 (NP = 4) only
         if constexpr (!LAB && NP == 4) {

@@ -127,8 +127,8 @@ int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
     A.coarse = ws->coarse;
     A.CK = ws->CK;
     // default geometry by size (measured at Na = 400: 2 cooperating waves per tile 10 % faster;
-    // at Na = 20,000 one wave per tile)
-    const int var = ws->variant >= 0 ? ws->variant : (ws->Na <= 4096 ? 2 : 0);
+    // at Na = 20,000 one wave per tile, XCD-aware tile order: 44.3 vs 45.9 us)
+    const int var = ws->variant >= 0 ? ws->variant : (ws->Na <= 4096 ? 2 : 16);
     A.variant = var;
     A.r = c.r;
     A.w = c.w;
@@ -160,10 +160,11 @@ int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
     A.hitcount = ws->count_hits ? ws->hitcount : nullptr;
     A.trace = nullptr;
     if (ws->tracing) {
-        const int64_t cap = (int64_t)ws->N * ((ws->Na + 63) / 64);
+        const int64_t cap = (int64_t)ws->N * ((ws->Na + 15) / 16);  // quad tiles: 16 states
         if (ws->trace_cap < cap) {
             dfree(ws->trace);
             AIY_TRY(dalloc(&ws->trace, 16 * (size_t)cap));
+            AIY_HIP(hipMemset(ws->trace, 0, 16 * (size_t)cap * sizeof(long long)));
             ws->trace_cap = cap;
         }
         A.trace = ws->trace;
@@ -436,6 +437,8 @@ int aiy_ws_set_timing(aiy_ws* ws, int enable) {
     ws->tot_ms = 0;
     ws->launches = 0;
     if (ws->hitcount) AIY_HIP(hipMemset(ws->hitcount, 0, 4 * kDiffSlots * sizeof(unsigned long long)));
+    if (ws->tracing && ws->trace)  // records of an earlier geometry must not linger
+        AIY_HIP(hipMemset(ws->trace, 0, 16 * (size_t)ws->trace_cap * sizeof(long long)));
     return AIY_OK;
 }
 

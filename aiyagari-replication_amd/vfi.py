@@ -82,11 +82,12 @@ class Workspace:
         """Records of the last tree sweep: int64 array (items, 16) = start, end (100 MHz clock),
         XCD id, superblock tests, block tests, candidates, exact evaluations, block id, then
         wave-0 shader cycles in startup+superblock tests, block tests, fine screens, exact."""
-        cap = self.N * ((self.Na + 63) // 64)
+        cap = self.N * ((self.Na + 15) // 16)
         out = np.zeros((cap, 16), np.int64)
         n = C.c_int64(0)
         check(lib().aiy_ws_trace(self._h, out.ctypes.data_as(C.c_void_p), i64(cap), C.byref(n)))
-        return out[:n.value]
+        out = out[:n.value]
+        return out[out[:, 1] > 0]  # items the last sweep's geometry wrote
 
     def timing(self):
         ms, n, hits = C.c_double(0), C.c_int64(0), C.c_int64(0)

@@ -9,7 +9,7 @@ from oracle import corc
 pytestmark = pytest.mark.gpu
 
 
-def test_multisection_matches_sequential_and_oracle(pkg, gpu):
+def test_multisection_matches_sequential_and_oracle(pkg, gpu, golden):
     gb = pkg.ge_batch
     cb = pkg.calibration
     A = gb.aiyagari_vfi_multisection(levels=6)
@@ -21,6 +21,13 @@ def test_multisection_matches_sequential_and_oracle(pkg, gpu):
     S = gb.bisection(ev, -0.05, 1 / cal["beta"] - 1)
     assert A.r_history == S.r_history and A.k_supply == S.k_supply and A.iters == S.iters
     assert A.rounds == 2 and A.candidates == 63 + 15
+    # Aiyagari_VFI.m:142-206's own trace (golden, chained warm start): warm-starting every
+    # candidate from the r0 solution moves K_s by ~1e-3 but takes every bracket decision the
+    # same way, so the r sequence and the equilibrium r are identical
+    g = golden("a11_ge_vfi_defaults")
+    assert A.r_history == [float(x) for x in g["r_history"]]
+    assert A.r == float(g["r_final"])
+    assert np.max(np.abs(np.array(A.k_supply) - g["k_supply"])) < 1e-2
 
     def solve(v, r, w):
         return corc.vfi_solve(v, cal["a_grid"], cal["s"], cal["P"], r, w, cal["beta"], cal["sigma"])

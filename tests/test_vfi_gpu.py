@@ -57,7 +57,8 @@ def _device_sweep(pkg, torch, V, a, s, P, r, w, beta, sigma, mode, hint=None, ws
 
 
 @pytest.mark.parametrize("variant,k_chunk", [(0, 1024), (1, 1024), (2, 1024), (6, 1024), (16, 1024),
-                                             (8, 1024), (9, 512), (11, 256), (12, 1024), (13, 256)])
+                                             (8, 1024), (9, 512), (11, 256), (12, 1024), (13, 256),
+                                             (32, 1024), (64, 1024), (80, 1024), (96, 1024)])
 @pytest.mark.parametrize("Na,shocks", [(1500, "rouwenhorst"), (777, "tauchen")])
 def test_screened_equals_plain_and_oracle(pkg, gpu, Na, shocks, variant, k_chunk):
     import torch
@@ -75,16 +76,19 @@ def test_screened_equals_plain_and_oracle(pkg, gpu, Na, shocks, variant, k_chunk
     assert np.array_equal(pks, pko) and np.array_equal(pcs, pco)
 
 
-def test_hint_does_not_change_result(pkg, gpu):
+@pytest.mark.parametrize("variant", [0, 64])
+def test_hint_does_not_change_result(pkg, gpu, variant):
     import torch
     cal = no.calib_aiyagari(Na=900)
     a, s, P = cal["a_grid"], cal["s"], cal["P"]
     w = no.wage(0.04, 0.36, 0.08)
     V = corc.vfi_solve(np.zeros((7, 900)), a, s, P, 0.04, w, 0.96, 5.0, 1e-5, 40)["v_new"]
-    ref = _device_sweep(pkg, torch, V, a, s, P, 0.04, w, 0.96, 5.0, mode=1)
+    ref = _device_sweep(pkg, torch, V, a, s, P, 0.04, w, 0.96, 5.0, mode=1, variant=variant)
     rng = np.random.default_rng(0)
-    for hint in (np.zeros((7, 900)), rng.integers(0, 900, (7, 900)), np.full((7, 900), 10**6)):
-        out = _device_sweep(pkg, torch, V, a, s, P, 0.04, w, 0.96, 5.0, mode=1, hint=hint)
+    for hint in (np.zeros((7, 900)), rng.integers(0, 900, (7, 900)), np.full((7, 900), 10**6),
+                 np.full((7, 900), -1)):
+        out = _device_sweep(pkg, torch, V, a, s, P, 0.04, w, 0.96, 5.0, mode=1, hint=hint,
+                            variant=variant)
         for x, y in zip(out, ref):
             assert np.array_equal(x, y)
 
@@ -142,7 +146,7 @@ def test_full_size_bitwise_vs_oracle(pkg, gpu):
     assert (pcs > 0).all()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 6, 8, 12])
+@pytest.mark.parametrize("variant", [0, 1, 2, 6, 8, 12, 64, 96])
 def test_screen_stress_noisy_value(pkg, gpu, variant):
     """Rough value functions put many candidates within rounding distance of the running best
     (near-ties everywhere, multi-modal objectives): the fp32 pre-screen, the fp64 screen and

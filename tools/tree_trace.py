@@ -27,13 +27,13 @@ def main():
         ws = pkg.Workspace(N, Na)
         ws.set_variant(var)
         cur = 0
-        for q in range(40):
-            if q in (10, 25, 39):
+        for q in range(101):
+            if q in (10, 25, 100):
                 ws.set_timing(True, trace=True)
             ws.vfi_sweep(v[cur], a_t, s_t, P_t, r, w, cal["beta"], cal["sigma"], v[1 - cur], idx,
                          hint=None if q == 0 else idx, mode=1)
             cur = 1 - cur
-            if q in (10, 25, 39):
+            if q in (10, 25, 100):
                 torch.cuda.synchronize()
                 ms, _, _ = ws.timing()
                 ws.set_timing(False)
