@@ -17,7 +17,8 @@ from . import ks_panel
 from . import stats
 from .ks import ks_egm_solve, ks_howard, ks_params, ks_policy_improve, ks_vfi_solve
 from .sim import sim_capital, sim_capital_dev
-from .vfi import Workspace, labor_vfi_solve, labor_vfi_sweep, vfi_solve, vfi_sweep
+from . import vfi
+from .vfi import Workspace, labor_vfi_solve, labor_vfi_sweep, solve_batch_dev, vfi_solve, vfi_sweep
 
 __all__ = ["ge", "ge_batch", "ks_dist", "ks_panel", "stats", "ks_egm_solve", "ks_howard", "ks_params", "ks_policy_improve", "ks_vfi_solve", "dist_stationary", "dist_update_dev", "egm_solve", "egm_step", "egm_step_dev", "labor_egm_solve", "labor_egm_step",
            "AiyError", "LIB_PATH", "Workspace", "calibration", "declared_symbols", "lib",

@@ -47,6 +47,14 @@ struct BellArgs {
     double* pc;
     unsigned long long* diff;  // nullable, [2]
     unsigned long long* fold;  // nullable [2]: the table kernel folds the previous sweep's diff slots here
+    // batched candidate rates (config 4; A1 tree screen only).  C <= 1: a single candidate.
+    // C > 1: every per-state array above is C consecutive blocks of its single layout, diff is
+    // [C][2][2*kDiffSlots] (parity = sweep & 1 selects the set this sweep writes).
+    int C;
+    const double* rv;  // [C] device: r of each candidate
+    const double* wv;  // [C] device: w of each candidate
+    const int* stop;   // [C] device: nonzero = stopped at that sweep (skipped from then on)
+    int parity;
 };
 
 int launch_bell_table(const BellArgs& A, hipStream_t st);
@@ -56,6 +64,8 @@ int launch_bell_screen(const BellArgs& A, hipStream_t st);
 int launch_bell_tree(const BellArgs& A, hipStream_t st);
 int launch_bell_plain(const BellArgs& A, hipStream_t st);
 int launch_bell_merge(const BellArgs& A, int use_partial, hipStream_t st);
+int launch_bell_table_batch(const BellArgs& A, unsigned long long* slots, int sweep, double tol,
+                            hipStream_t st);
 size_t bell_partial_slots(const BellArgs& A);
 
 }  // namespace aiy

@@ -29,6 +29,7 @@
 //              policy_l = L(l), policy_c = c(l,k), and max|v_new − v_old| ignoring NaN via an
 //              order-independent atomicMax on IEEE bits.
 // Non-integer σ (or σ > 9) runs a plain exhaustive kernel (device pow/log).
+#include <algorithm>
 #include <type_traits>
 
 #include "aiy_common.hpp"
@@ -103,6 +104,34 @@ template <bool LAB>
 __device__ __forceinline__ double cash(double x, double y, double Ll) {
     if constexpr (LAB) return x + y * Ll;  // (1+r)a_j + (w s_i) L_l   (Labor_VFI.m:81)
     else return x + y;                     // (1+r)a_j + w s_i          (Aiyagari_VFI.m:72)
+}
+
+// ------------------------------------------------------------------------------ batches
+// Config 4 (BASELINE configs[3]): C candidate interest rates in one launch.  Every per-state
+// array is a [C] block of its single-candidate layout; candidate c sees BellArgs shifted to its
+// block, its own r and w, and its own diff slots (two parities, so sweep g's table kernel can
+// read sweep g-1's slots while the tree kernel of g writes the other set).
+__device__ __forceinline__ BellArgs bell_cand(const BellArgs& A, int c) {
+    BellArgs B = A;
+    const size_t o = (size_t)c * A.N * A.Na;
+    B.r = A.rv[c];
+    B.w = A.wv[c];
+    B.v_old += o;
+    B.EV += o;
+    if (B.Dt) B.Dt += o;
+    if (B.Dm8) B.Dm8 += (size_t)c * A.N * A.nb8;
+    if (B.Dm512) B.Dm512 += (size_t)c * A.N * A.nb512;
+    B.kf += o * A.Nl;
+    B.best0 += o;
+    B.idx0 += o;
+    if (B.hint) B.hint += o;
+    B.v_new += o;
+    B.idx += o;
+    if (B.pk) B.pk += o;
+    if (B.pc) B.pc += o;
+    B.diff += ((size_t)c * 2 + A.parity) * 2 * kDiffSlots;
+    B.C = 1;
+    return B;
 }
 
 // ------------------------------------------------------------------------------ 1. table
@@ -191,12 +220,93 @@ __global__ __launch_bounds__(kTableBlock) void bell_table_kernel(
     }
 }
 
+// Batched table (config 4): grid (x: 512 candidates of a row, y: C·N rows).  Besides the
+// single-candidate table it runs candidate c's stopping rule (Aiyagari_VFI.m:85-86): it folds
+// the diff slots the previous sweep's tree kernel left for c and, below tol, marks c stopped at
+// that sweep (stop[c] = sweep - 1) — then neither this sweep's table nor tree touches c again,
+// so c's buffers keep v_new, v_old and the policies of its stopping sweep (break semantics),
+// while the other candidates go on.  Every block of c takes the same decision from the same
+// slots; block (0, row 0 of c) records it and clears this sweep's slot set.
+__global__ __launch_bounds__(kTableBlock) void bell_table_batch_kernel(
+    int N, int Na, const double* __restrict__ P, const double* __restrict__ V, double beta,
+    int np, const double* __restrict__ a, double* __restrict__ EV, double* __restrict__ Dt,
+    double* __restrict__ Dm8, double* __restrict__ Dm512, int nb8, int nb512,
+    unsigned long long* __restrict__ slots, int* __restrict__ stop, int sweep, double tol) {
+    __shared__ double s_max[kTableBlock / 64];
+    __shared__ int s_stop;
+    const int c = blockIdx.y / N, i = blockIdx.y - c * N;
+    if (stop[c]) return;  // block-uniform
+    if (sweep > 1) {
+        if (threadIdx.x < 64) {
+            const int l = threadIdx.x;
+            const unsigned long long* sl = slots + ((size_t)c * 2 + ((sweep - 1) & 1)) * 2 * kDiffSlots;
+            unsigned long long m = sl[2 * l];
+            const int any = __ballot(sl[2 * l + 1] != 0ull) != 0ull;
+            for (int off = 32; off > 0; off >>= 1) {
+                const unsigned long long o = __shfl_xor(m, off);
+                m = o > m ? o : m;
+            }
+            if (l == 0) s_stop = any && aiy_bitsd(m) < tol;  // NaN-only: no stop (:85)
+        }
+        __syncthreads();
+        if (s_stop) {
+            if (blockIdx.x == 0 && i == 0 && threadIdx.x == 0) stop[c] = sweep - 1;
+            return;
+        }
+    }
+    if (blockIdx.x == 0 && i == 0 && threadIdx.x < 2 * kDiffSlots)
+        slots[((size_t)c * 2 + (sweep & 1)) * 2 * kDiffSlots + threadIdx.x] = 0ull;
+    const size_t o = (size_t)c * N * Na;
+    const int k = blockIdx.x * kTableBlock + threadIdx.x;
+    const bool ok = k < Na;
+    double D = -__builtin_inf();
+    if (ok) {
+        const size_t t = o + (size_t)i * Na + k;
+        const double acc = table_ev(N, Na, P, V + o, beta, i, k);
+        EV[t] = acc;
+        D = table_D(acc, np);
+        Dt[t] = D;
+    }
+    D = fmax(D, __shfl_xor(D, 1));
+    D = fmax(D, __shfl_xor(D, 2));
+    D = fmax(D, __shfl_xor(D, 4));
+    const size_t rb8 = ((size_t)c * N + i) * nb8, rb512 = ((size_t)c * N + i) * nb512;
+    if (ok && (k & 7) == 0) Dm8[rb8 + (k >> 3)] = D;
+    D = fmax(D, __shfl_xor(D, 8));
+    D = fmax(D, __shfl_xor(D, 16));
+    D = fmax(D, __shfl_xor(D, 32));
+    if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = D;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double m = s_max[0];
+        for (int q = 1; q < kTableBlock / 64; ++q) m = fmax(m, s_max[q]);
+        Dm512[rb512 + blockIdx.x] = m;
+    }
+}
+
+int launch_bell_table_batch(const BellArgs& A, unsigned long long* slots, int sweep, double tol,
+                            hipStream_t st) {
+    dim3 grid((A.Na + kTableBlock - 1) / kTableBlock, A.C * A.N);
+    bell_table_batch_kernel<<<grid, kTableBlock, 0, st>>>(
+        A.N, A.Na, A.P, A.v_old, A.beta, A.np, A.a, A.EV, A.Dt, A.Dm8, A.Dm512, A.nb8, A.nb512,
+        slots, const_cast<int*>(A.stop), sweep, tol);
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
+}
+
 // ------------------------------------------------------------------------------ 1b. kf
 // feasible prefix per (l, i, j): depends on (r, w, a, s, L) only, so a solve computes it once
 template <bool LAB>
-__global__ void bell_kf_kernel(BellArgs A) {
+__global__ void bell_kf_kernel(BellArgs A0) {
     int t = blockIdx.x * blockDim.x + threadIdx.x;
-    int n = A.N * A.Na;
+    int n = A0.N * A0.Na;
+    BellArgs A = A0;
+    if (A0.C > 1) {  // batched: t spans C blocks of (l, i, j)
+        const int c = t / (n * A0.Nl);
+        if (c >= A0.C) return;
+        A = bell_cand(A0, c);
+        t -= c * n * A0.Nl;
+    }
     if (t >= n * A.Nl) return;
     int l = t / n, ij = t - l * n;
     int i = ij / A.Na, j = ij - i * A.Na;
@@ -206,8 +316,15 @@ __global__ void bell_kf_kernel(BellArgs A) {
 
 // ------------------------------------------------------------------------------ 2. init
 template <int NP, bool LAB>
-__global__ void bell_init_kernel(BellArgs A) {
+__global__ void bell_init_kernel(BellArgs A0) {
     int t = blockIdx.x * blockDim.x + threadIdx.x;
+    BellArgs A = A0;
+    if (A0.C > 1) {
+        const int c = t / (A0.N * A0.Na);
+        if (c >= A0.C || A0.stop[c]) return;
+        A = bell_cand(A0, c);
+        t -= c * A0.N * A0.Na;
+    }
     if (t >= A.N * A.Na) return;
     const int Na = A.Na, Nl = A.Nl;
     int i = t / Na, j = t - i * Na;
@@ -603,10 +720,17 @@ __global__ __launch_bounds__(256, MINW) void bell_screen_kernel(BellArgs A, int 
 // The starting bar is the hint (last sweep's argmax) and its two neighbours, or — on a cold
 // start — the init kernel's candidate (best0/idx0).
 template <int NP, bool LAB, int R, int LB, int W>
-__global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A, int ntile) {
+__global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntile) {
     const int lane = threadIdx.x & 63;
     const int wave = readfirst(threadIdx.x >> 6);
-    const int item = (A.variant & 16) ? xcd_remap((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+    int item = (A0.variant & 16) ? xcd_remap((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+    BellArgs A = A0;
+    if (A0.C > 1) {  // batched candidates: blocks [c·N·ntile, (c+1)·N·ntile) are candidate c's
+        const int c = item / (A0.N * ntile);
+        if (A0.stop[c]) return;  // converged at an earlier sweep: its buffers stay as they are
+        A = bell_cand(A0, c);
+        item -= c * A0.N * ntile;
+    }
     const int tile = item % ntile;
     const int i = item / ntile;
     const int N = A.N, Na = A.Na, Nl = A.Nl;
@@ -1019,10 +1143,17 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A, int ntile
 // t_k over its block in floating point, and a candidate whose exact value reaches a lane's
 // running best passes that lane's test).
 template <int NP>
-__global__ __launch_bounds__(64) void bell_quad_kernel(BellArgs A, int ntile) {
+__global__ __launch_bounds__(64) void bell_quad_kernel(BellArgs A0, int ntile) {
     const int lane = threadIdx.x & 63;
     const int st = lane & 15, q4 = lane >> 4;
-    const int item = (A.variant & 16) ? xcd_remap((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+    int item = (A0.variant & 16) ? xcd_remap((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+    BellArgs A = A0;
+    if (A0.C > 1) {
+        const int c = item / (A0.N * ntile);
+        if (A0.stop[c]) return;
+        A = bell_cand(A0, c);
+        item -= c * A0.N * ntile;
+    }
     const int tile = item % ntile;
     const int i = item / ntile;
     const int Na = A.Na;
@@ -1346,7 +1477,7 @@ int launch_bell_table(const BellArgs& A, hipStream_t st) {
 }
 
 int launch_bell_kf(const BellArgs& A, hipStream_t st) {
-    int n = A.N * A.Na * A.Nl;
+    int n = std::max(A.C, 1) * A.N * A.Na * A.Nl;
     if (A.labor) bell_kf_kernel<true><<<cdiv(n, 256), 256, 0, st>>>(A);
     else bell_kf_kernel<false><<<cdiv(n, 256), 256, 0, st>>>(A);
     AIY_HIP(hipGetLastError());
@@ -1364,7 +1495,7 @@ struct Geo {
 
 template <int NP, bool LAB>
 static void run_init(const BellArgs& A, hipStream_t st) {
-    bell_init_kernel<NP, LAB><<<cdiv(A.N * A.Na, 128), 128, 0, st>>>(A);
+    bell_init_kernel<NP, LAB><<<cdiv((long long)std::max(A.C, 1) * A.N * A.Na, 128), 128, 0, st>>>(A);
 }
 template <int NP, bool LAB, int R, int MINW>
 static void screen_geo(const BellArgs& A, hipStream_t st) {
@@ -1393,7 +1524,7 @@ template <int NP, bool LAB, int R, int W>
 static void tree_geo(const BellArgs& A, hipStream_t st) {
     constexpr int LB = LAB ? 5 : 1;
     const int ntile = cdiv(A.Na, 64 * R);
-    bell_tree_kernel<NP, LAB, R, LB, W><<<A.N * ntile, 64 * W, 0, st>>>(A, ntile);
+    bell_tree_kernel<NP, LAB, R, LB, W><<<std::max(A.C, 1) * A.N * ntile, 64 * W, 0, st>>>(A, ntile);
 }
 // variant bit 0: 2 states per lane (A1 only); bits 1-2: waves per tile 1 (default), 2, 4, 8
 template <int NP, bool LAB, int R>
@@ -1410,7 +1541,7 @@ static void run_tree(const BellArgs& A, hipStream_t st) {
     if constexpr (NP > 0 && !LAB) {
         if (A.variant & 64) {  // four lanes per state, 16 states per wave
             const int ntile = cdiv(A.Na, 16);
-            bell_quad_kernel<NP><<<A.N * ntile, 64, 0, st>>>(A, ntile);
+            bell_quad_kernel<NP><<<std::max(A.C, 1) * A.N * ntile, 64, 0, st>>>(A, ntile);
             return;
         }
     }

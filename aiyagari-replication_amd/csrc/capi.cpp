@@ -376,6 +376,130 @@ int bell_solve_dev(aiy_ws* ws, BellCall c, double* v_a, double* v_b, double tol,
     return AIY_OK;
 }
 
+// Config 4 (BASELINE configs[3]): C candidate interest rates, each the A2 loop of
+// Aiyagari_VFI.m:147-171 from its own v_old, solved together: every sweep is ONE table launch
+// and ONE tree launch over all candidates still running (C·N·Na states), so the GPU sees C
+// times the parallelism of one solve.  Each candidate stops at its own first sweep below tol
+// (the table kernel applies :85 per candidate on the device and freezes it), so iteration
+// counts, v_new, v_old and policies are exactly those of C separate solves.  The host reads the
+// stop flags once per `spec_max` sweeps.  Buffers: sweep g reads buf[(g-1) & 1] and writes
+// buf[g & 1] with buf[0] = v_a, so a candidate that stopped at g* holds v_new in buf[g* & 1].
+int bell_solve_batch_dev(aiy_ws* ws, int64_t C, const double* r, const double* w, double* v_a,
+                         double* v_b, const double* a, const double* s, const double* P,
+                         double beta, double sigma, double tol, int64_t max_iter, int use_hint,
+                         int* idx, double* pk, double* pc, int64_t* iters, int* which,
+                         hipStream_t st) {
+    if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
+    if (C < 1 || C > (1 << 20)) return fail(AIY_BAD_SHAPE, "need 1 <= C <= 2^20 candidates");
+    if (!r || !w || !v_a || !v_b || !a || !s || !P || !idx || !iters || !which)
+        return fail(AIY_BAD_ARG, "NULL argument");
+    if (max_iter < 1) return fail(AIY_BAD_ARG, "max_iter must be >= 1");
+    for (int64_t c = 0; c < C; ++c)
+        if (!(r[c] == r[c]) || !(w[c] == w[c])) return fail(AIY_NON_FINITE, "non-finite r or w");
+    const size_t n = (size_t)ws->N * ws->Na;
+    const int np = is_int_ge(sigma, 2.0) && sigma <= 9.0 ? (int)sigma - 1 : 0;
+    if (np == 0 || C == 1) {
+        // generic sigma (plain sweeps) or a single rate: one solve after another, same results
+        for (int64_t c = 0; c < C; ++c) {
+            BellCall bc{};
+            bc.a = a; bc.s = s; bc.P = P; bc.r = r[c]; bc.w = w[c]; bc.beta = beta;
+            bc.sigma = sigma; bc.idx = idx + c * n; bc.pk = pk ? pk + c * n : nullptr;
+            bc.pc = pc ? pc + c * n : nullptr;
+            bc.hint = use_hint ? idx + c * n : nullptr;
+            AIY_TRY(bell_solve_dev(ws, bc, v_a + c * n, v_b + c * n, tol, max_iter, &iters[c],
+                                   &which[c], st));
+        }
+        return AIY_OK;
+    }
+    if ((size_t)C * n > (size_t)INT32_MAX) return fail(AIY_BAD_SHAPE, "C*N*Na must fit int32");
+    const int nb8 = (int)((ws->Na + 7) / 8), nb512 = (int)((ws->Na + 511) / 512);
+    if (ws->bC != C) {
+        ws->free_batch();
+        AIY_TRY(dalloc(&ws->bEV, C * n));
+        AIY_TRY(dalloc(&ws->bDt, C * n));
+        AIY_TRY(dalloc(&ws->bDm8, (size_t)C * ws->N * nb8));
+        AIY_TRY(dalloc(&ws->bDm512, (size_t)C * ws->N * nb512));
+        AIY_TRY(dalloc(&ws->bbest0, C * n));
+        AIY_TRY(dalloc(&ws->bidx0, C * n));
+        AIY_TRY(dalloc(&ws->bkf, C * n));
+        AIY_TRY(dalloc(&ws->bstop, (size_t)C));
+        AIY_TRY(dalloc(&ws->bslots, (size_t)C * 2 * 2 * kDiffSlots));
+        AIY_TRY(dalloc(&ws->brw, 2 * (size_t)C));
+        AIY_HIP(hipHostMalloc((void**)&ws->hstop, C * sizeof(int)));
+        AIY_HIP(hipHostMalloc((void**)&ws->hslots, (size_t)C * 2 * kDiffSlots * sizeof(unsigned long long)));
+        ws->bC = C;
+    }
+    AIY_TRY(ws_ensure_bell(ws, 1));  // diff/hitcount scratch and events (single-rate buffers)
+    AIY_HIP(hipMemcpyAsync(ws->brw, r, C * sizeof(double), hipMemcpyHostToDevice, st));
+    AIY_HIP(hipMemcpyAsync(ws->brw + C, w, C * sizeof(double), hipMemcpyHostToDevice, st));
+    AIY_HIP(hipMemsetAsync(ws->bstop, 0, C * sizeof(int), st));
+    BellArgs A{};
+    A.N = (int)ws->N; A.Na = (int)ws->Na; A.Nl = 1; A.labor = false; A.np = np;
+    A.coarse = ws->coarse; A.CK = ws->CK;
+    A.variant = ws->variant >= 0 ? ws->variant : (ws->Na <= 4096 ? 0 : 16);
+    A.variant &= ~(1 | 2 | 4 | 8);  // one state per lane, one wave per tile, tree screen
+    A.beta = beta; A.sigma = sigma; A.a = a; A.s = s; A.P = P;
+    A.EV = ws->bEV; A.Dt = ws->bDt; A.Dm8 = ws->bDm8; A.Dm512 = ws->bDm512;
+    A.nb = (int)((ws->Na + 63) / 64); A.nb8 = nb8; A.nb512 = nb512;
+    A.tree = true; A.best0 = ws->bbest0; A.idx0 = ws->bidx0; A.kf = ws->bkf;
+    A.hitcount = ws->count_hits ? ws->hitcount : nullptr;
+    A.idx = idx; A.pk = pk; A.pc = pc; A.diff = ws->bslots;
+    A.C = (int)C; A.rv = ws->brw; A.wv = ws->brw + C; A.stop = ws->bstop;
+    AIY_TRY(launch_bell_kf(A, st));  // per-candidate feasible prefixes, once per solve
+    ws->kf_ok = false;               // (the single-rate kf cache is not this table)
+    double* buf[2] = {v_a, v_b};
+    int64_t g = 0;
+    bool all_stopped = false;
+    const int64_t m = std::max(ws->spec_max, 1);
+    while (!all_stopped && g < max_iter) {
+        const int64_t gend = std::min(max_iter, g + m);
+        for (++g; g <= gend; ++g) {
+            A.v_old = buf[(g - 1) & 1];
+            A.v_new = buf[g & 1];
+            A.parity = (int)(g & 1);
+            A.hint = (g == 1 && !use_hint) ? nullptr : idx;
+            AIY_TRY(launch_bell_table_batch(A, ws->bslots, (int)g, tol, st));
+            if (!A.hint) AIY_TRY(launch_bell_init(A, st));
+            AIY_TRY(ws_timing_begin(ws, st));
+            AIY_TRY(launch_bell_tree(A, st));
+            AIY_TRY(ws_timing_end(ws, st));
+        }
+        --g;  // sweeps launched so far
+        AIY_HIP(hipMemcpyAsync(ws->hstop, ws->bstop, C * sizeof(int), hipMemcpyDeviceToHost, st));
+        AIY_HIP(hipStreamSynchronize(st));
+        all_stopped = true;
+        for (int64_t c = 0; c < C; ++c) all_stopped = all_stopped && ws->hstop[c] != 0;
+    }
+    // candidates still running after the last sweep G = max_iter: fold their sweep-G slots
+    // (its :85 test), else the loop was exhausted and v_old = v_new (:88)
+    const int64_t G = g;
+    bool any_running = false;
+    for (int64_t c = 0; c < C; ++c) any_running = any_running || ws->hstop[c] == 0;
+    if (any_running) {
+        for (int64_t c = 0; c < C; ++c)
+            if (ws->hstop[c] == 0)
+                AIY_HIP(hipMemcpyAsync(ws->hslots + c * 2 * kDiffSlots,
+                                       ws->bslots + ((size_t)c * 2 + (G & 1)) * 2 * kDiffSlots,
+                                       2 * kDiffSlots * sizeof(unsigned long long),
+                                       hipMemcpyDeviceToHost, st));
+        AIY_HIP(hipStreamSynchronize(st));
+    }
+    for (int64_t c = 0; c < C; ++c) {
+        int64_t it = ws->hstop[c];
+        if (it == 0) {
+            const double d = fold_slots_host(ws->hslots + c * 2 * kDiffSlots);
+            it = G;
+            if (!(d < tol))  // exhausted: v_old = v_new after the last sweep
+                AIY_HIP(hipMemcpyAsync(buf[(G - 1) & 1] + c * n, buf[G & 1] + c * n,
+                                       n * sizeof(double), hipMemcpyDeviceToDevice, st));
+        }
+        iters[c] = it;
+        which[c] = (int)(it & 1);
+    }
+    AIY_HIP(hipStreamSynchronize(st));
+    return AIY_OK;
+}
+
 }  // namespace aiy
 
 using namespace aiy;
@@ -537,6 +661,16 @@ int aiy_vfi_solve_dev(aiy_ws* ws, double* v_a, double* v_b, const double* a_grid
     c.a = a_grid; c.s = s; c.P = P; c.r = r; c.w = w; c.beta = beta; c.sigma = sigma;
     c.mode = mode; c.idx = idx; c.pk = policy_k; c.pc = policy_c;
     return bell_solve_dev(ws, c, v_a, v_b, tol, max_iter, iters, out_new, (hipStream_t)stream);
+}
+
+int aiy_vfi_solve_batch_dev(aiy_ws* ws, int64_t C, const double* r, const double* w,
+                            double* v_a, double* v_b, const double* a_grid, const double* s,
+                            const double* P, double beta, double sigma, double tol,
+                            int64_t max_iter, int use_hint, int32_t* idx, double* policy_k,
+                            double* policy_c, int64_t* iters, int32_t* which, void* stream) {
+    return bell_solve_batch_dev(ws, C, r, w, v_a, v_b, a_grid, s, P, beta, sigma, tol, max_iter,
+                                use_hint, idx, policy_k, policy_c, iters, which,
+                                (hipStream_t)stream);
 }
 
 int aiy_labor_vfi_sweep_dev(aiy_ws* ws, const double* v_old, const double* a_grid,

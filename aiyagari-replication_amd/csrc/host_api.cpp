@@ -87,6 +87,18 @@ int check_grid(const double* a, int64_t Na) {
     return AIY_OK;
 }
 
+// interp1 and griddedInterpolant reject repeated grid points: the interpolating entry points
+// (simulation, histogram lottery, KS panel) need a strictly increasing grid, else they would
+// divide by a[k+1] - a[k] = 0 (MATLAB raises an error there)
+int check_grid_strict(const double* a, int64_t Na) {
+    AIY_TRY(check_grid(a, Na));
+    for (int64_t k = 1; k < Na; ++k)
+        if (!(a[k] > a[k - 1]))
+            return fail(AIY_BAD_ARG, "grid must be strictly increasing (point %lld repeats point %lld)",
+                        (long long)k + 1, (long long)k);
+    return AIY_OK;
+}
+
 // stage the common Aiyagari inputs (a_grid, s, P) on the device; P transposed to row-major
 int stage_common(HostCtx* c, const double* a, const double* s, const double* P, int64_t N,
                  int64_t Na, double** da, double** ds, double** dP) {

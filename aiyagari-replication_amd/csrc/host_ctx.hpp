@@ -24,6 +24,7 @@ std::mutex& host_mutex();
 void cm_to_rows(const double* cm, int64_t N, int64_t Na, double* rows);
 void rows_to_cm(const double* rows, int64_t N, int64_t Na, double* cm);
 int check_grid(const double* a, int64_t Na);
+int check_grid_strict(const double* a, int64_t Na);
 int stage_common(HostCtx* c, const double* a, const double* s, const double* P, int64_t N,
                  int64_t Na, double** da, double** ds, double** dP);
 

@@ -17,6 +17,10 @@ struct SimArgs {
     double* sim_k;      // nullable [T]
     int* sim_z;         // nullable [T], 0-based
     int* status;        // [1] 0 ok, 1 find() empty
+    // batched chains (config 4): C > 1 runs C independent chains, one workgroup each; chain c
+    // reads pol + c·pcs and U + c·ucs and writes out[c], status[c] (no paths)
+    int C;
+    size_t pcs, ucs;
 };
 int launch_sim_capital(const SimArgs& A, hipStream_t st);
 }  // namespace aiy

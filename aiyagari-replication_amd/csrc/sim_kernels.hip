@@ -9,6 +9,8 @@
 // a_grid and the policy rows are staged in LDS when they fit (Na·(N+1) <= 18432 doubles),
 // otherwise read through L1/L2.
 // Uniform draws come from the host (MATLAB's rand stream), so the chain is reproducible.
+#include <algorithm>
+
 #include "aiy_common.hpp"
 #include "sim.hpp"
 
@@ -17,7 +19,14 @@ namespace aiy {
 constexpr int kSimLdsMax = 18432;  // doubles: 147 KiB of the 160 KiB LDS
 
 template <bool LDS>
-__global__ __launch_bounds__(64) void sim_capital_kernel(SimArgs A) {
+__global__ __launch_bounds__(64) void sim_capital_kernel(SimArgs A0) {
+    SimArgs A = A0;
+    if (A0.C > 1) {  // batched chains: one workgroup per candidate
+        A.pol += blockIdx.x * A0.pcs;
+        A.U += blockIdx.x * A0.ucs;
+        A.out += blockIdx.x;
+        A.status += blockIdx.x;
+    }
     extern __shared__ double lds[];
     const int lane = threadIdx.x;
     const int N = A.N, Na = A.Na;
@@ -125,7 +134,14 @@ __device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v,
 }
 
 template <bool LDS, bool PATH>
-__global__ __launch_bounds__(256) void sim_chain_kernel(SimArgs A) {
+__global__ __launch_bounds__(256) void sim_chain_kernel(SimArgs A0) {
+    SimArgs A = A0;
+    if (A0.C > 1) {  // batched chains: one workgroup per candidate
+        A.pol += blockIdx.x * A0.pcs;
+        A.U += blockIdx.x * A0.ucs;
+        A.out += blockIdx.x;
+        A.status += blockIdx.x;
+    }
     extern __shared__ double lds[];
     __shared__ unsigned long long F[kSimChunk];
     __shared__ double cs[16 * 16];
@@ -277,16 +293,16 @@ int launch_sim_capital(const SimArgs& A, hipStream_t st) {
         const long long need_pad = (long long)(A.Na + 64) * (A.N + 1);
         const bool path = A.sim_k || A.sim_z;
         if (need_pad <= kSimChainLdsMax) {
-            if (path) sim_chain_kernel<true, true><<<1, 256, sizeof(double) * need_pad, st>>>(A);
-            else sim_chain_kernel<true, false><<<1, 256, sizeof(double) * need_pad, st>>>(A);
+            if (path) sim_chain_kernel<true, true><<<std::max(A.C, 1), 256, sizeof(double) * need_pad, st>>>(A);
+            else sim_chain_kernel<true, false><<<std::max(A.C, 1), 256, sizeof(double) * need_pad, st>>>(A);
         } else {
-            if (path) sim_chain_kernel<false, true><<<1, 256, 0, st>>>(A);
-            else sim_chain_kernel<false, false><<<1, 256, 0, st>>>(A);
+            if (path) sim_chain_kernel<false, true><<<std::max(A.C, 1), 256, 0, st>>>(A);
+            else sim_chain_kernel<false, false><<<std::max(A.C, 1), 256, 0, st>>>(A);
         }
     } else if (need <= kSimLdsMax) {
-        sim_capital_kernel<true><<<1, 64, sizeof(double) * need, st>>>(A);
+        sim_capital_kernel<true><<<std::max(A.C, 1), 64, sizeof(double) * need, st>>>(A);
     } else {
-        sim_capital_kernel<false><<<1, 64, 0, st>>>(A);
+        sim_capital_kernel<false><<<std::max(A.C, 1), 64, 0, st>>>(A);
     }
     AIY_HIP(hipGetLastError());
     return AIY_OK;

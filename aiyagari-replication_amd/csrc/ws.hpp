@@ -64,6 +64,34 @@ struct aiy_ws {
     double* spec_pol = nullptr;                 // [spec_max][3][N*Na] (k, c, l)
     unsigned long long* spec_diff = nullptr;    // device [2*spec_max]
     unsigned long long* spec_hdiff = nullptr;   // pinned host [2*spec_max]
+    // batched candidate rates (config 4, aiy_vfi_solve_batch_dev): per-candidate blocks of the
+    // tree-screen scratch, sized for bC candidates
+    int64_t bC = 0;
+    double* bEV = nullptr;
+    double* bDt = nullptr;
+    double* bDm8 = nullptr;
+    double* bDm512 = nullptr;
+    double* bbest0 = nullptr;
+    int* bidx0 = nullptr;
+    int* bkf = nullptr;
+    int* bstop = nullptr;                  // device [bC]
+    unsigned long long* bslots = nullptr;  // device [bC][2][2*kDiffSlots]
+    double* brw = nullptr;                 // device [2][bC]: r then w
+    int* hstop = nullptr;                  // pinned [bC]
+    unsigned long long* hslots = nullptr;  // pinned [bC][2*kDiffSlots]
+    void free_batch() {
+        void* ps[] = {bEV, bDt, bDm8, bDm512, bbest0, bidx0, bkf, bstop, bslots, brw};
+        for (void* p : ps)
+            if (p) (void)hipFree(p);
+        if (hstop) (void)hipHostFree(hstop);
+        if (hslots) (void)hipHostFree(hslots);
+        bEV = bDt = bDm8 = bDm512 = bbest0 = brw = nullptr;
+        bidx0 = bkf = bstop = nullptr;
+        bslots = nullptr;
+        hstop = nullptr;
+        hslots = nullptr;
+        bC = 0;
+    }
     // timing of the dominant kernel
     bool timing = false, count_hits = false;
     std::vector<hipEvent_t> ev_start, ev_stop;
@@ -85,6 +113,7 @@ struct aiy_ws {
         for (void* p : ps)
             if (p) (void)hipFree(p);
         free_spec();
+        free_batch();
         if (hdiff) (void)hipHostFree(hdiff);
         EV = nullptr; T = nullptr; T32 = nullptr; Dm = nullptr; Dm8 = nullptr; Dt = nullptr; Dm512 = nullptr; touched = nullptr; best0 = nullptr; dis = nullptr; kf = nullptr; kf_cap = 0;
         kf_ok = false;
@@ -125,6 +154,11 @@ int ws_read_diff(aiy_ws* ws, hipStream_t st, double* d);
 int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st);
 int bell_solve_dev(aiy_ws* ws, BellCall c, double* v_a, double* v_b, double tol,
                    int64_t max_iter, int64_t* iters, int* out_new, hipStream_t st);
+int bell_solve_batch_dev(aiy_ws* ws, int64_t C, const double* r, const double* w, double* v_a,
+                         double* v_b, const double* a, const double* s, const double* P,
+                         double beta, double sigma, double tol, int64_t max_iter, int use_hint,
+                         int* idx, double* pk, double* pc, int64_t* iters, int* which,
+                         hipStream_t st);
 int launch_reduce_slots(const unsigned long long* slots, void* out, hipStream_t st);
 double fold_slots_host(const unsigned long long* h);
 int launch_disutility(const double* L, int Nl, double psi, double eta, double* dis,

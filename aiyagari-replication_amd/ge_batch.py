@@ -80,14 +80,20 @@ def walk(nodes: list[Node], res: dict, lo: float, hi: float, steps: int, tr: Tra
 
 def multisection(evaluate, r_low, r_high, max_steps=10, levels=6, tol=1e-5, rank=0, world=1,
                  allgather=None) -> Trace:
-    """evaluate(node) -> (K_s, K_d, iters) for the nodes this rank owns (index % world == rank);
-    allgather(list_of_triples) -> list over ranks of lists (None when world == 1)."""
+    """evaluate(node) -> (K_s, K_d, iters) for the nodes this rank owns (index % world == rank),
+    or, when `evaluate` has an `many` attribute, evaluate.many(nodes) -> list of triples for all
+    of them at once (the batched device path); allgather(list) -> list over ranks of lists
+    (None when world == 1)."""
     tr = Trace()
     lo, hi, done, step = r_low, r_high, False, 0
     while not done and step < max_steps:
         L = min(levels, max_steps - step)
         nodes = subtree(lo, hi, step + 1, L)
-        mine = [(q, evaluate(n)) for q, n in enumerate(nodes) if q % world == rank]
+        own = [q for q in range(len(nodes)) if q % world == rank]
+        if hasattr(evaluate, "many"):
+            mine = list(zip(own, evaluate.many([nodes[q] for q in own]))) if own else []
+        else:
+            mine = [(q, evaluate(nodes[q])) for q in own]
         if world > 1:
             parts = allgather(mine)
             allres = [x for part in parts for x in part]
@@ -174,23 +180,66 @@ def hip_vfi_evaluator(cal, v_start, T=10000, tol=1e-5, max_iter=1000):
     return vfi_evaluator(cal, solve, simulate, v_start, T, tol, max_iter)
 
 
+def ge_batch_call(r, v_start, cal, z1, k1, blocks, tol=1e-5, max_iter=1000, n_devices=1):
+    """aiy_ge_batch (C ABI): K_s, K_d and iteration count at every rate in `r`, each
+    from v_start, with uniforms blocks[c] (T-1 draws) for candidate c; z1 1-based."""
+    import ctypes as C
+    from ._capi import check, d, i64, ip, lib, ptr
+    r = np.ascontiguousarray(r, np.float64)
+    n = r.size
+    N, Na = cal["N"], cal["Na"]
+    U = np.asfortranarray(np.stack([np.asarray(b, np.float64) for b in blocks], axis=1))
+    T = U.shape[0] + 1
+    v = np.asfortranarray(v_start, dtype=np.float64)
+    a = np.ascontiguousarray(cal["a_grid"], np.float64)
+    s = np.ascontiguousarray(cal["s"], np.float64)
+    P = np.asfortranarray(cal["P"], dtype=np.float64)
+    Ks, Kd, it = np.empty(n), np.empty(n), np.empty(n, np.int64)
+    check(lib().aiy_ge_batch(ptr(r), i64(n), ptr(v), ptr(a), ptr(s), ptr(P), i64(N), i64(Na),
+                             d(cal["alpha"]), d(cal["delta"]), d(cal["beta"]), d(cal["sigma"]),
+                             d(cal["labor"]), d(tol), i64(max_iter), i64(z1), d(k1), i64(T),
+                             ptr(U), ip(n_devices), ptr(Ks), ptr(Kd), ptr(it)))
+    return Ks, Kd, it
+
+
+def hip_batch_evaluator(cal, v_start, T=10000, tol=1e-5, max_iter=1000, n_devices=1):
+    """The node evaluator on the batched device path: all of a round's nodes of this rank in
+    one aiy_ge_batch call (one batched solve and one batched launch of the chains per GPU).
+    Same per-node arithmetic as vfi_evaluator, so the traces are identical."""
+    N, Na, a = cal["N"], cal["Na"], cal["a_grid"]
+    head, blocks = mc_stream(T)
+    z1 = int(math.ceil(N * head[0]))
+    k1 = a[int(math.ceil(Na * head[1])) - 1]
+
+    def many(nodes):
+        Ks, Kd, it = ge_batch_call([n.r for n in nodes], v_start, cal, z1, k1,
+                                   [blocks[n.depth] for n in nodes], tol, max_iter, n_devices)
+        return [(float(Ks[q]), float(Kd[q]), int(it[q])) for q in range(len(nodes))]
+
+    def evaluate(node):
+        return many([node])[0]
+    evaluate.many = many
+    return evaluate
+
+
 def auto_levels(world: int) -> int:
     """Tree levels per round so that one round's 2^L - 1 candidates fit the ranks (one each)."""
     return max(1, int(math.floor(math.log2(world + 1))))
 
 
 def aiyagari_vfi_multisection(Na=400, levels=None, rank=0, world=1, allgather=None, r0=0.04,
-                              shocks="tauchen"):
+                              shocks="tauchen", batched=True):
     """Config 4: the GE of Aiyagari_VFI.m with candidate rates spread over `world` ranks.
-    Every rank solves r0 once (the common warm start), then the rounds.  levels=None picks
-    auto_levels(world); BASELINE's 64-candidate configuration is levels=6."""
+    Every rank solves r0 once (the common warm start), then the rounds; batched=True evaluates
+    each rank's nodes of a round in one batched device call (else one solve after another).
+    levels=None picks auto_levels(world); BASELINE's 64-candidate configuration is levels=6."""
     levels = auto_levels(world) if levels is None else levels
     from . import calibration as cb
     from .vfi import vfi_solve
     cal = cb.aiyagari(Na=Na, shocks=shocks)
     R0 = vfi_solve(np.zeros((cal["N"], Na)), cal["a_grid"], cal["s"], cal["P"], r0,
                    cb.wage(r0, cal["alpha"], cal["delta"]), cal["beta"], cal["sigma"])
-    ev = hip_vfi_evaluator(cal, R0["v_old"])
+    ev = (hip_batch_evaluator if batched else hip_vfi_evaluator)(cal, R0["v_old"])
     lo, hi = -0.05, 1 / cal["beta"] - 1
     return multisection(ev, lo, hi, levels=levels, rank=rank, world=world,
                         allgather=allgather if allgather else (torch_allgather if world > 1 else None))

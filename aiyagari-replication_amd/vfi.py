@@ -136,6 +136,24 @@ class Workspace:
         return it.value, which.value
 
 
+def solve_batch_dev(ws, r, w, v_a, v_b, a_grid, s, P, beta, sigma, tol, max_iter, idx,
+                    policy_k=None, policy_c=None, use_hint=False, stream=None):
+    """Config 4 on device (aiy_vfi_solve_batch_dev): C = len(r) rates solved together; v_a/v_b,
+    idx and the policies are [C][N][Na] tensors.  Returns (iters, which) as lists: candidate c
+    holds v_new in v_b[c] if which[c] else v_a[c] (its v_old in the other)."""
+    r = np.ascontiguousarray(r, np.float64)
+    w = np.ascontiguousarray(w, np.float64)
+    C = r.size
+    it = np.zeros(C, np.int64)
+    which = np.zeros(C, np.int32)
+    check(lib().aiy_vfi_solve_batch_dev(ws.handle, i64(C), ptr(r), ptr(w), ptr(v_a), ptr(v_b),
+                                        ptr(a_grid), ptr(s), ptr(P), d(beta), d(sigma), d(tol),
+                                        i64(max_iter), ip(1 if use_hint else 0), ptr(idx),
+                                        ptr(policy_k), ptr(policy_c), ptr(it), ptr(which),
+                                        stream_handle(stream)))
+    return [int(x) for x in it], [int(x) for x in which]
+
+
 # ------------------------------------------------------------------------------------ A3
 def _labor_call(fn, v_old, a_grid, s, P, labor_choice, r, w, beta, sigma, psi, eta, extra,
                 v_new=None, pol=None):

@@ -114,6 +114,19 @@ int aiy_dist_stationary(const int32_t* policy_idx, const double* policy_k, int v
                         double tol, int64_t max_iter, double* lambda, double* k_supply,
                         int64_t* iters, double* dist);
 
+/* Config 4 / SURVEY B2 `ge_batch` — excess demand at C candidate rates: for each r(c) the
+ * body of one GE step of Aiyagari_VFI.m:147-195: the VFI from v_start (N x Na, the common warm
+ * start) to tol, the Monte-Carlo capital supply from (z1 1-based, k1) with the candidate's own
+ * T-1 uniforms (column c of the (T-1) x C matrix `uniforms`), and K_d = labor·(α/(r+δ))^(1/(1-α)).
+ * The candidates are split over n_devices GPUs of this process (batched solve + batched chains
+ * per device, one host thread per device).  Out (C each): k_supply, k_demand, iters.  The
+ * bracketing logic (:196-204) stays with the caller.  a_grid must be strictly increasing. */
+int aiy_ge_batch(const double* r, int64_t C, const double* v_start, const double* a_grid,
+                 const double* s, const double* P, int64_t N, int64_t Na, double alpha,
+                 double delta, double beta, double sigma, double labor, double tol,
+                 int64_t max_iter, int64_t z1, double k1, int64_t T, const double* uniforms,
+                 int n_devices, double* k_supply, double* k_demand, int64_t* iters);
+
 /* A6 — replaces Krusell_Smith_VFI.m:149-168 (policy improvement with fminbnd).
  * value, k_opt: k x K x S column-major (S = 4); B 4; P 4 x 4; params = 13 doubles {beta, alpha,
  * delta, k_min, k_max, ug, ub, l_bar, mu, z_grid(1), z_grid(2), eps_grid(1), eps_grid(2)}.  nfev (nullable,
@@ -228,6 +241,18 @@ int aiy_vfi_solve_dev(aiy_ws* ws, double* v_a, double* v_b, const double* a_grid
                       double sigma, double tol, int64_t max_iter, int mode, int32_t* idx,
                       double* policy_k, double* policy_c, int64_t* iters, int* out_new,
                       void* stream);
+/* Config 4 (BASELINE configs[3]) on device: C candidate rates solved together, each the A2
+ * loop of Aiyagari_VFI.m:147-171 (its own stop at :85, break semantics :85-88).  r, w: host
+ * [C]; v_a (in: each candidate's starting v_old), v_b, idx, policy_k, policy_c: device
+ * [C][N][Na].  use_hint != 0: idx holds a hint (e.g. the r0 solution's argmax) on entry.
+ * Out (host [C]): iters = sweeps of each candidate, which = 1 if its v_new is in v_b (its
+ * v_old in v_a), else 0.  Every sweep is one launch pair over all running candidates; results
+ * equal C separate aiy_vfi_solve_dev calls bit for bit. */
+int aiy_vfi_solve_batch_dev(aiy_ws* ws, int64_t C, const double* r, const double* w,
+                            double* v_a, double* v_b, const double* a_grid, const double* s,
+                            const double* P, double beta, double sigma, double tol,
+                            int64_t max_iter, int use_hint, int32_t* idx, double* policy_k,
+                            double* policy_c, int64_t* iters, int32_t* which, void* stream);
 int aiy_labor_vfi_sweep_dev(aiy_ws* ws, const double* v_old, const double* a_grid,
                             const double* s, const double* P, const double* labor_choice,
                             double r, double w, double beta, double sigma, double psi,
