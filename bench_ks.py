@@ -86,8 +86,19 @@ def ks_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, exchange="halo", r
     nodes = nk * nK * 4
     cols = halo.columns if halo is not None else (nK - (K1 - K0) if world > 1 else 0)
     sh.close()
+    # Algorithmic bytes per node and Howard sweep (each array touched once): the slope rebuild
+    # reads V and writes dV (16 B); the sweep reads k_opt and the segment hint (12 B), the V/dV
+    # columns its forecast reads (16 B, each column once) and writes V (8 B) -> 52 B.
+    bpn = 52
+    gbs = nodes * bpn / (th / howard) / 1e9 / world  # per GPU
     return {"metric": "Krusell-Smith bellman_value evals/sec (Howard sweeps, fp64)",
             "value": nodes * howard / th, "unit": "evals/s", "n_gpus": world,
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": 8000.0, "unit": "GB/s",
+                         "frac": gbs / 8000.0,
+                         "basis": f"{bpn} B algorithmic per node per Howard sweep (slopes: V in, dV "
+                                  f"out; sweep: k_opt, segment hint, forecast V/dV columns in, V "
+                                  f"out) x {nodes // world} nodes per GPU / sweep time; the "
+                                  f"working set (V, dV, k_opt: 200 MB) is HBM-resident"},
             "scaling": "strong", "vfi_iteration_ms": (ti + th) * 1e3,
             "howard_ms_per_sweep": th / howard * 1e3, "improve_ms": ti * 1e3,
             "workload": f"Krusell_Smith_VFI k={nk} K={nK} S=4 ({nodes} nodes, BASELINE "
