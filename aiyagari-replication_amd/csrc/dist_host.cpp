@@ -87,7 +87,8 @@ int aiy_dist_stationary(const int32_t* policy_idx, const double* policy_k, int v
         return fail(AIY_BAD_ARG, "NULL argument");
     if (N < 1 || Na < 2) return fail(AIY_BAD_SHAPE, "need N >= 1 and Na >= 2");
     if (max_iter < 1) return fail(AIY_BAD_ARG, "max_iter must be >= 1");
-    AIY_TRY(check_grid(a_grid, Na));
+    // the lottery divides by a(k+1) - a(k): repeated nodes are rejected (interp1 would error)
+    AIY_TRY(policy_k ? check_grid_strict(a_grid, Na) : check_grid(a_grid, Na));
     std::lock_guard<std::mutex> lk(host_mutex());
     HostCtx* c;
     AIY_TRY(get_ctx(N, Na, 1, &c));

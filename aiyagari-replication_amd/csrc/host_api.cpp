@@ -256,6 +256,27 @@ using namespace aiy;
 
 extern "C" {
 
+int aiy_release_all(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (auto& kv : g_ctx) {  // each context's buffers live on its own device
+        (void)hipSetDevice(std::get<0>(kv.first));
+        kv.second.reset();
+    }
+    g_ctx.clear();
+    (void)hipSetDevice(cur);
+    return AIY_OK;
+}
+
+int64_t aiy_host_cache_bytes(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    int64_t b = 0;
+    for (auto& kv : g_ctx)
+        for (auto& q : kv.second->bufs) b += (int64_t)q.second.second;
+    return b;
+}
+
 int aiy_vfi_sweep(const double* v_old, const double* a_grid, const double* s, const double* P,
                   int64_t N, int64_t Na, double r, double w, double beta, double sigma,
                   double* v_new, double* policy_k, double* policy_c, int32_t* policy_idx) {

@@ -399,6 +399,9 @@ int ks_vfi_solve(double* value, double* k_opt, const double* k_grid, const doubl
                  int64_t* iters, double* rel_diff) {
     if (!k_opt || !iters || !rel_diff) return fail(AIY_BAD_ARG, "NULL argument");
     if (max_vfi < 1 || howard_steps < 0) return fail(AIY_BAD_ARG, "max_vfi >= 1, howard_steps >= 0");
+    // the checks ks_stage makes, before the multi-device branch (which does not stage)
+    if (!value || !k_grid || !K_grid || !B || !P || !params) return fail(AIY_BAD_ARG, "NULL argument");
+    if (nk < 3 || nK < 1) return fail(AIY_BAD_SHAPE, "need k_size >= 3 and K_size >= 1");
     if (n_devices > 1) return ks_vfi_solve_multi(value, k_opt, k_grid, K_grid, B, P, params, nk,
                                                  nK, howard_steps, tol, max_vfi, n_devices,
                                                  iters, rel_diff);

@@ -152,8 +152,8 @@ int ks_simulate_capital(const double* k_opt, const double* k_grid, const double*
         return fail(AIY_BAD_ARG, "NULL argument");
     AIY_TRY(check_panel_shape(T, population));
     if (nk < 2 || nK < 2) return fail(AIY_BAD_SHAPE, "need k_size, K_size >= 2");
-    AIY_TRY(check_grid(k_grid, nk));
-    AIY_TRY(check_grid(K_grid, nK));
+    AIY_TRY(check_grid_strict(k_grid, nk));  // griddedInterpolant rejects repeated points
+    AIY_TRY(check_grid_strict(K_grid, nK));
     // MATLAB's lookup (:227-231) maps only z in z_grid and eps in eps_grid; other codes error
     std::vector<int8_t> hz(T), he((size_t)T * population);
     for (int64_t t = 0; t < T; ++t) {

@@ -37,7 +37,7 @@ int aiy_sim_capital(const double* policy_k, int vfi_layout, const double* a_grid
                     const double* uniforms, double* k_supply, double* sim_k, int32_t* sim_z) {
     if (!policy_k || !P || !k_supply) return fail(AIY_BAD_ARG, "NULL argument");
     if (N < 1 || Na < 2) return fail(AIY_BAD_SHAPE, "need N >= 1 and Na >= 2");
-    AIY_TRY(check_grid(a_grid, Na));
+    AIY_TRY(check_grid_strict(a_grid, Na));  // interp1 (:113) rejects repeated points
     std::lock_guard<std::mutex> lk(host_mutex());
     HostCtx* c;
     AIY_TRY(get_ctx(N, Na, 1, &c));

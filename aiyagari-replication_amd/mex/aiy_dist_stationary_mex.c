@@ -24,6 +24,7 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     }
     double K = 0, dist = 0;
     int64_t it = 0;
+    aiy_begin();
     int rc = aiy_dist_stationary(idx, on_grid ? NULL : pol, vfi, a, P, (int64_t)N, (int64_t)Na,
                                  tol, max_iter, mxGetPr(plhs[0]), &K, &it, &dist);
     free(idx);

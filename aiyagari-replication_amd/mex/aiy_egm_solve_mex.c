@@ -17,6 +17,7 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     mxArray* pk = aiy_out(Na, N);
     double dist = 0;
     int64_t it = 0;
+    aiy_begin();
     aiy_check(aiy_egm_solve(mxGetPr(plhs[0]), a, s, P, (int64_t)N, (int64_t)Na, r, w, beta, sigma,
                             amin, tol, max_iter, mxGetPr(pk), &dist, &it));
     if (nlhs > 1) plhs[1] = pk; else mxDestroyArray(pk);

@@ -19,6 +19,7 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     mxArray* pl = aiy_out(Na, N);
     double dist = 0;
     int64_t it = 0;
+    aiy_begin();
     aiy_check(aiy_labor_egm_solve(mxGetPr(plhs[0]), a, s, P, (int64_t)N, (int64_t)Na, r, w, beta,
                                   sigma, phi, theta, amin, tol, max_iter, mxGetPr(pk), mxGetPr(pl),
                                   &dist, &it));

@@ -30,6 +30,7 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
         }
     }
     int64_t it = 0;
+    aiy_begin();
     int rc = aiy_labor_vfi_solve(mxGetPr(vo), a, s, P, L, (int64_t)N, (int64_t)Na, (int64_t)Nl, r, w,
                                  beta, sigma, psi, eta, tol, max_iter, mxGetPr(outs[0]),
                                  mxGetPr(outs[1]), mxGetPr(outs[2]), mxGetPr(outs[3]), NULL, &it);

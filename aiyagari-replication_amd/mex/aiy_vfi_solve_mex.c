@@ -19,6 +19,7 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     mxArray* pk = aiy_out(N, Na);
     mxArray* pc = aiy_out(N, Na);
     int64_t it = 0;
+    aiy_begin();
     int rc = aiy_vfi_solve(mxGetPr(vo), a, s, P, (int64_t)N, (int64_t)Na, r, w, beta, sigma, tol,
                            max_iter, mxGetPr(plhs[0]), mxGetPr(pk), mxGetPr(pc), NULL, &it);
     aiy_check(rc);

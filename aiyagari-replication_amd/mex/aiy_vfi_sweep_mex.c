@@ -14,6 +14,7 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     mxArray* pk = aiy_out(N, Na);
     mxArray* pc = aiy_out(N, Na);
     int32_t* idx = (int32_t*)malloc(sizeof(int32_t) * N * Na);
+    aiy_begin();
     int rc = aiy_vfi_sweep(v, a, s, P, (int64_t)N, (int64_t)Na, r, w, beta, sigma, mxGetPr(plhs[0]),
                            mxGetPr(pk), mxGetPr(pc), idx);
     if (rc == AIY_OK && nlhs > 3) {

@@ -10,7 +10,7 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     const double* kg = aiy_vec(prhs[1], "k_grid", 0, &nk);
     const double* Kg = aiy_vec(prhs[2], "K_grid", 0, &nK);
     if (mxGetNumberOfElements(prhs[0]) != nk * nK * 4)
-        mexErrMsgIdAndTxt("aiy:shape", "k_opt must be k_size x K_size x 4");
+        aiy_err("aiy:shape", "k_opt must be k_size x K_size x 4");
     aiy_in(prhs[0], "k_opt", 0, 0);
     const double* B = aiy_vec(prhs[3], "B", 4, NULL);
     const double* P = aiy_in(prhs[4], "P", 4, 4);
@@ -22,6 +22,7 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     memcpy(mxGetPr(plhs[0]), mxGetPr(prhs[0]), sizeof(double) * nk * nK * 4);
     int64_t it = 0;
     double diff = 0;
+    aiy_begin();
     aiy_check(ks_egm_solve(mxGetPr(plhs[0]), kg, Kg, B, P, prm, (int64_t)nk, (int64_t)nK, tol,
                            maxe, &it, &diff));
     if (nlhs > 1) plhs[1] = mxCreateDoubleScalar((double)it);

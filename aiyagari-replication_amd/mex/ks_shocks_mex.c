@@ -8,18 +8,19 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     aiy_nargs(nrhs, 4, 4, nlhs, 2, "[zi_shock,epsi_shock] = ks_shocks_mex(T,population,uniforms,params)");
     double Td = aiy_scalar(prhs[0], "T"), popd = aiy_scalar(prhs[1], "population");
     if (!(Td >= 1 && popd >= 1) || Td != (double)(int64_t)Td || popd != (double)(int64_t)popd)
-        mexErrMsgIdAndTxt("aiy:shape", "T and population must be positive integers");
+        aiy_err("aiy:shape", "T and population must be positive integers");
     int64_t T = (int64_t)Td, pop = (int64_t)popd;
     const double* U = aiy_vec(prhs[2], "uniforms", (mwSize)ks_shock_draws(T, pop), NULL);
     const double* prm = aiy_vec(prhs[3], "params", 13, NULL);
     mxArray* zi = aiy_out((mwSize)T, 1);
     mxArray* ep = aiy_out((mwSize)T, (mwSize)pop);
+    aiy_begin();
     int rc = ks_shocks(T, pop, U, prm, mxGetPr(zi), mxGetPr(ep));
     if (rc != AIY_OK) {
         mxDestroyArray(zi);
         mxDestroyArray(ep);
-        aiy_check(rc);
     }
+    aiy_check(rc);
     plhs[0] = zi;
     if (nlhs > 1) plhs[1] = ep;
     else mxDestroyArray(ep);

@@ -10,23 +10,24 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     const double* kg = aiy_vec(prhs[1], "k_grid", 0, &nk);
     const double* Kg = aiy_vec(prhs[2], "K_grid", 0, &nK);
     if (mxGetNumberOfElements(prhs[0]) != nk * nK * 4)
-        mexErrMsgIdAndTxt("aiy:shape", "k_opt must be k_size x K_size x 4");
+        aiy_err("aiy:shape", "k_opt must be k_size x K_size x 4");
     const double* ko = aiy_in(prhs[0], "k_opt", 0, 0);
     const double* zi = aiy_vec(prhs[3], "zi_shock", 0, &T);
     const double* ep = aiy_in(prhs[4], "epsi_shock", T, 0);
     const double* kp = aiy_vec(prhs[5], "k_population", 0, &pop);
     if (mxGetN(prhs[4]) != pop)
-        mexErrMsgIdAndTxt("aiy:shape", "epsi_shock must be numel(zi_shock) x numel(k_population)");
+        aiy_err("aiy:shape", "epsi_shock must be numel(zi_shock) x numel(k_population)");
     mxArray* K_ts = aiy_out(T, 1);
     mxArray* kout = aiy_out(pop, 1);
     memcpy(mxGetPr(kout), kp, sizeof(double) * pop);
+    aiy_begin();
     int rc = ks_simulate_capital(ko, kg, Kg, (int64_t)nk, (int64_t)nK, zi, ep, (int64_t)T,
                                  (int64_t)pop, mxGetPr(kout), mxGetPr(K_ts));
     if (rc != AIY_OK) {
         mxDestroyArray(K_ts);
         mxDestroyArray(kout);
-        aiy_check(rc);
     }
+    aiy_check(rc);
     plhs[0] = K_ts;
     if (nlhs > 1) plhs[1] = kout;
     else mxDestroyArray(kout);

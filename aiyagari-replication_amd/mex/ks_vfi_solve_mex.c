@@ -10,7 +10,7 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     const double* kg = aiy_vec(prhs[2], "k_grid", 0, &nk);
     const double* Kg = aiy_vec(prhs[3], "K_grid", 0, &nK);
     if (mxGetNumberOfElements(prhs[0]) != nk * nK * 4 || mxGetNumberOfElements(prhs[1]) != nk * nK * 4)
-        mexErrMsgIdAndTxt("aiy:shape", "value and k_opt must be k_size x K_size x 4");
+        aiy_err("aiy:shape", "value and k_opt must be k_size x K_size x 4");
     aiy_in(prhs[0], "value", 0, 0);
     aiy_in(prhs[1], "k_opt", 0, 0);
     const double* B = aiy_vec(prhs[4], "B", 4, NULL);
@@ -27,6 +27,7 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     memcpy(mxGetPr(ko), mxGetPr(prhs[1]), sizeof(double) * nk * nK * 4);
     int64_t it = 0;
     double rel = 0;
+    aiy_begin();
     aiy_check(ks_vfi_solve(mxGetPr(plhs[0]), mxGetPr(ko), kg, Kg, B, P, prm, (int64_t)nk,
                            (int64_t)nK, H, tol, maxv, nd, &it, &rel));
     if (nlhs > 1) plhs[1] = ko; else mxDestroyArray(ko);

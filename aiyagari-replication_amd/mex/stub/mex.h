@@ -33,6 +33,7 @@ double mxGetScalar(const mxArray* a);
 void mexErrMsgIdAndTxt(const char* id, const char* fmt, ...);
 int mexAtExit(void (*fn)(void));
 void mexLock(void);
+void mexUnlock(void);
 #ifdef __cplusplus
 }
 #endif

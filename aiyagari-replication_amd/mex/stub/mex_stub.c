@@ -74,8 +74,17 @@ void mexErrMsgIdAndTxt(const char* id, const char* fmt, ...) {
     snprintf(g_err_id, sizeof g_err_id, "%s", id);
     longjmp(g_jmp, 1);
 }
-int mexAtExit(void (*fn)(void)) { (void)fn; return 0; }
-void mexLock(void) {}
+/* MATLAB keeps one exit function and one lock count per MEX file; the stub links every
+ * gateway into one library, so it keeps a list of the registered exit functions (one per
+ * gateway) and one lock count, which the tests read to check that calls are balanced. */
+static void (*g_atexit[64])(void);
+static int g_natexit = 0, g_lock = 0;
+int mexAtExit(void (*fn)(void)) {
+    if (g_natexit < 64) g_atexit[g_natexit++] = fn;
+    return 0;
+}
+void mexLock(void) { ++g_lock; }
+void mexUnlock(void) { --g_lock; }
 
 /* ---- harness entry points (ctypes) ---- */
 typedef void (*mexfn)(int, mxArray**, int, const mxArray**);
@@ -95,3 +104,12 @@ mxArray* stub_double_array3(mwSize a, mwSize b, mwSize c) {
     mwSize d[3] = {a, b, c};
     return mxCreateNumericArray(3, d, mxDOUBLE_CLASS, mxREAL);
 }
+/* `clear mex`: run every registered exit function once (MATLAB does so when it unloads the
+ * files), then forget them; returns how many ran */
+int stub_clear_mex(void) {
+    int n = g_natexit;
+    for (int q = 0; q < n; ++q) g_atexit[q]();
+    g_natexit = 0;
+    return n;
+}
+int stub_lock_depth(void) { return g_lock; }

@@ -45,6 +45,14 @@ int aiy_device_count(void);
  * Host tier (MATLAB layouts).  VFI arrays N x Na; EGM arrays Na x N; KS k x K x S.
  * ====================================================================================== */
 
+/* Lifecycle.  The host tier keeps device buffers, workspaces and streams
+ * per (device, shape) across calls.  aiy_release_all frees every one of them (the gateways
+ * register it with mexAtExit, so `clear all` / `clear mex` — Krusell_Smith_VFI.m:2 — leaves
+ * no device memory behind); the next call re-creates what it needs.  aiy_host_cache_bytes
+ * reports the device bytes those caches hold (0 after a release). */
+int aiy_release_all(void);
+int64_t aiy_host_cache_bytes(void);
+
 /* A1 — replaces Aiyagari_VFI.m:68-83 (one Bellman sweep).
  * in : v_old N x Na, a_grid Na (non-decreasing), s N, P N x N, r, w, beta, sigma
  * out: v_new, policy_k, policy_c (N x Na); policy_idx (N x Na, 1-based, may be NULL) */

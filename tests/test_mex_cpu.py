@@ -88,3 +88,63 @@ def test_ks_panel_gateways_validate(cal):
         mexstub.call("ks_simulate_capital_mex", 2, np.zeros((10, 4, 4)), np.linspace(0, 1, 10),
                      np.linspace(30, 50, 4), np.full(5, 3.0), np.ones((5, 3)), np.ones(3))
     assert e.value.id == "aiy:BAD_ARG"
+
+
+def test_ge_batch_gateway_validation(cal):
+    v = np.zeros((7, 20))
+    U = np.full((99, 2), 0.5)
+    args = [np.array([0.01, 0.02]), v, cal["a_grid"], cal["s"], cal["P"], 0.36, 0.08, 0.96, 5.0,
+            1.0, 1e-5, 1000.0, 1.0, float(cal["a_grid"][0]), U, 1.0]
+    with pytest.raises(mexstub.MexError) as e:
+        mexstub.call("aiy_ge_batch_mex", 3, *args[:-1])
+    assert e.value.id == "aiy:usage"
+    bad = list(args)
+    bad[14] = np.full((99, 3), 0.5)          # one column of uniforms per candidate rate
+    with pytest.raises(mexstub.MexError) as e:
+        mexstub.call("aiy_ge_batch_mex", 3, *bad)
+    assert e.value.id == "aiy:shape"
+    bad = list(args)
+    bad[12] = 1.5                              # z1 must be an integer
+    with pytest.raises(mexstub.MexError) as e:
+        mexstub.call("aiy_ge_batch_mex", 3, *bad)
+    assert e.value.id == "aiy:type"
+    bad = list(args)
+    a = cal["a_grid"].copy()
+    a[3] = a[2]                                # repeated grid point: interp1 would error
+    bad[2] = a
+    with pytest.raises(mexstub.MexError) as e:
+        mexstub.call("aiy_ge_batch_mex", 3, *bad)
+    assert e.value.id == "aiy:BAD_ARG"
+
+
+def test_sim_gateway_layout_is_explicit_when_ambiguous(cal):
+    P = np.eye(7)
+    pol = np.zeros((7, 7))                     # Na == N: N x Na and Na x N look alike
+    with pytest.raises(mexstub.MexError) as e:
+        mexstub.call("aiy_sim_capital_mex", 1, pol, np.arange(7.0), P, 1.0, 0.0, np.full(9, 0.5))
+    assert e.value.id == "aiy:shape" and "layout" in str(e.value)
+
+
+def test_lifecycle_lock_balanced_and_release_registered(cal):
+    """Every call leaves the lock count where it found it, errors included, and the first call
+    that reaches the library registers the exit function; `clear mex` runs it, which frees the
+    host-tier caches (B3)."""
+    L = mexstub.lib()
+    d0 = L.stub_lock_depth()
+    for _ in range(2):
+        try:
+            mexstub.call("aiy_vfi_sweep_mex", 3, np.zeros((7, 20)), cal["a_grid"][::-1].copy(),
+                         cal["s"], cal["P"], 0.04, 1.0, 0.96, 5.0)
+        except mexstub.MexError:
+            pass
+        try:
+            mexstub.call("aiy_vfi_sweep_mex", 3, np.zeros((7, 20)))
+        except mexstub.MexError:
+            pass
+    assert L.stub_lock_depth() == d0
+    assert L.stub_clear_mex() >= 1
+    import ctypes as C
+    from tests.conftest import load_pkg
+    lib = load_pkg().lib()
+    lib.aiy_host_cache_bytes.restype = C.c_int64
+    assert lib.aiy_host_cache_bytes() == 0

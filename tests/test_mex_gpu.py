@@ -88,3 +88,39 @@ def test_ks_panel_gateways(pkg, gpu, golden):
     K_ts, kf = mexstub.call("ks_simulate_capital_mex", 2, g["k_opt"], g["k_grid"], g["K_grid"],
                             zi, ep, np.full(pop, g["K_grid"][0]))
     assert np.array_equal(K_ts.ravel(), g["K_ts"]) and np.array_equal(kf.ravel(), g["k_final"])
+
+
+def test_clear_mex_releases_device_buffers(pkg, gpu, golden):
+    """B3: `clear mex` (mexAtExit -> aiy_release_all) frees every cached device buffer of the
+    host tier; the next call re-creates them and gives the same answer."""
+    import ctypes as C
+    lib = pkg.lib()
+    lib.aiy_host_cache_bytes.restype = C.c_int64
+    g = golden("a1_vfi_defaults")
+    args = (np.zeros((7, 400)), g["a_grid"], g["s"], g["P"], float(g["r"]), float(g["w"]), 0.96,
+            5.0, 1e-5, 1000.0)
+    first = mexstub.call("aiy_vfi_solve_mex", 5, *args)
+    assert lib.aiy_host_cache_bytes() > 0
+    assert mexstub.lib().stub_lock_depth() == 0
+    assert mexstub.lib().stub_clear_mex() >= 1
+    assert lib.aiy_host_cache_bytes() == 0
+    again = mexstub.call("aiy_vfi_solve_mex", 5, *args)
+    for x, y in zip(first, again):
+        assert np.array_equal(x, y)
+
+
+def test_ge_batch_gateway(pkg, gpu):
+    """Config 4 through the MATLAB-facing boundary equals the Python host mirror."""
+    cal = pkg.calibration.aiyagari(Na=400)
+    w0 = pkg.calibration.wage(0.04, cal["alpha"], cal["delta"])
+    v0 = corc.vfi_solve(np.zeros((7, 400)), cal["a_grid"], cal["s"], cal["P"], 0.04, w0,
+                        cal["beta"], cal["sigma"])["v_old"]
+    r = np.array([-0.004166666666666667, -0.027083333333333334, 0.01875])
+    U = no.matlab_rand_stream(2 + 3 * 9999)[2:].reshape(3, 9999).T  # one block per candidate
+    ks, kd, it = mexstub.call("aiy_ge_batch_mex", 3, r, v0, cal["a_grid"], cal["s"], cal["P"],
+                              cal["alpha"], cal["delta"], cal["beta"], cal["sigma"], cal["labor"],
+                              1e-5, 1000.0, 6.0, float(cal["a_grid"][57]), U, 1.0)
+    Ks, Kd, It = pkg.ge_batch.ge_batch_call(r, v0, cal, 6, float(cal["a_grid"][57]),
+                                            [U[:, c] for c in range(3)])
+    assert np.array_equal(ks[:, 0], Ks) and np.array_equal(kd[:, 0], Kd)
+    assert np.array_equal(it[:, 0].astype(np.int64), It)
