@@ -22,6 +22,9 @@ struct KsArgs {
     double beta, k_min, k_max, tol;
     int howard, max_vfi;
     int* seg_hint;  // nullable [node]: k-segment of clamp(k_opt), written by improve, a hint for Howard
+    // several s blocks in one launch (sharded path): blockIdx.y = q handles nodes
+    // node0 + q·sstride + [0, n_local); ns = 1 (sstride unused) otherwise
+    int ns, sstride;
 };
 struct KsParams {  // the 13-double parameter block, in order
     double beta, alpha, delta, k_min, k_max, ug, ub, l_bar, mu, z1, z2, e1, e2;

@@ -1,5 +1,6 @@
 // Device tier of the Krusell-Smith VFI (A6/A7) for one process per GPU: a handle owns one
-// shard — the K range [K0, K1) of all four s — and runs the improvement, Howard and
+// shard — the K range [K0, K1) of all four s, or of one z's two s ((K, Z) slices, so the
+// reference's K = 4 grid spreads over 8 ranks) — and runs the improvement, Howard and
 // relative-difference kernels on it, reading full k x K x S arrays already in HBM.  The
 // caller (aiyagari-replication_amd/ks_dist.py) exchanges the owned value slices between
 // ranks with an RCCL all-gather after every Howard sweep.
@@ -17,6 +18,7 @@
 struct ks_dev {
     int dev = 0;
     int nk = 0, nK = 0, K0 = 0, K1 = 0;
+    int s0 = 0, s1 = 4;  // owned s blocks [s0, s1): all four, or one z's pair ((K, Z) slices)
     double beta = 0, k_min = 0, k_max = 0;
     double* kg = nullptr;
     double* P = nullptr;
@@ -29,12 +31,15 @@ struct ks_dev {
 };
 
 namespace aiy {
-static KsArgs shard_args(const ks_dev* h, int s) {
+// the shard's nodes: K in [K0, K1) of every owned s, the s blocks as blockIdx.y of one launch
+static KsArgs shard_args(const ks_dev* h) {
     KsArgs A{};
     A.nk = h->nk;
     A.nK = h->nK;
-    A.node0 = (s * h->nK + h->K0) * h->nk;
+    A.node0 = (h->s0 * h->nK + h->K0) * h->nk;
     A.n_local = (h->K1 - h->K0) * h->nk;
+    A.ns = h->s1 - h->s0;
+    A.sstride = h->nK * h->nk;
     A.k_grid = h->kg;
     A.P = h->P;
     A.slice = h->sl;
@@ -62,10 +67,17 @@ int ks_dev_destroy(ks_dev* h) {
 int ks_dev_create(const double* k_grid, const double* K_grid, const double* B, const double* P,
                   const double* params, int64_t nk, int64_t nK, int64_t K0, int64_t K1,
                   ks_dev** out) {
+    return ks_dev_create_slice(k_grid, K_grid, B, P, params, nk, nK, K0, K1, 0, 4, out);
+}
+
+int ks_dev_create_slice(const double* k_grid, const double* K_grid, const double* B,
+                        const double* P, const double* params, int64_t nk, int64_t nK,
+                        int64_t K0, int64_t K1, int64_t s0, int64_t s1, ks_dev** out) {
     if (!out || !k_grid || !K_grid || !B || !P || !params) return fail(AIY_BAD_ARG, "NULL argument");
     if (nk < 3 || nK < 1 || nk * nK * 4 > (1ll << 30))
         return fail(AIY_BAD_SHAPE, "need k_size >= 3, K_size >= 1");
     if (K0 < 0 || K1 > nK || K0 >= K1) return fail(AIY_BAD_ARG, "shard [K0, K1) must be inside [0, K_size)");
+    if (s0 < 0 || s1 > 4 || s0 >= s1) return fail(AIY_BAD_ARG, "shard [s0, s1) must be inside [0, 4)");
     AIY_TRY(check_grid(k_grid, nk));
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return fail(AIY_NO_DEVICE, "no HIP device visible");
@@ -74,7 +86,7 @@ int ks_dev_create(const double* k_grid, const double* K_grid, const double* B, c
     std::vector<KsSlice> sl;
     ks_slices(p, B, K_grid, (int)nK, sl);
     std::vector<char> need(4 * nK, 0);
-    for (int s = 0; s < 4; ++s)
+    for (int64_t s = s0; s < s1; ++s)
         for (int64_t K = K0; K < K1; ++K) {
             need[s * nK + K] = 1;
             const int kp = sl[s * nK + K].kp_idx;
@@ -89,6 +101,7 @@ int ks_dev_create(const double* k_grid, const double* K_grid, const double* B, c
     ks_dev* h = new ks_dev();
     (void)hipGetDevice(&h->dev);
     h->nk = (int)nk; h->nK = (int)nK; h->K0 = (int)K0; h->K1 = (int)K1;
+    h->s0 = (int)s0; h->s1 = (int)s1;
     h->beta = p.beta; h->k_min = p.k_min; h->k_max = p.k_max;
     h->ncols = (int)cols.size();
     const size_t n = (size_t)nk * nK * 4;
@@ -118,8 +131,8 @@ int ks_dev_create(const double* k_grid, const double* K_grid, const double* B, c
 int ks_dev_improve(ks_dev* h, const double* V, double* kopt, void* stream) {
     if (!h || !V || !kopt) return fail(AIY_BAD_ARG, "NULL argument");
     hipStream_t st = (hipStream_t)stream;
-    AIY_TRY(launch_ks_slopes_cols(shard_args(h, 0), h->cols, h->ncols, V, h->dV, st));
-    for (int s = 0; s < 4; ++s) AIY_TRY(launch_ks_improve(shard_args(h, s), V, h->dV, kopt, nullptr, st));
+    AIY_TRY(launch_ks_slopes_cols(shard_args(h), h->cols, h->ncols, V, h->dV, st));
+    AIY_TRY(launch_ks_improve(shard_args(h), V, h->dV, kopt, nullptr, st));
     return AIY_OK;
 }
 
@@ -128,8 +141,8 @@ int ks_dev_howard(ks_dev* h, const double* V, const double* kopt, double* Vout, 
     if (!h || !V || !kopt || !Vout) return fail(AIY_BAD_ARG, "NULL argument");
     if (V == Vout) return fail(AIY_BAD_ARG, "Howard sweeps are Jacobi: V and Vout must differ");
     hipStream_t st = (hipStream_t)stream;
-    AIY_TRY(launch_ks_slopes_cols(shard_args(h, 0), h->cols, h->ncols, V, h->dV, st));
-    for (int s = 0; s < 4; ++s) AIY_TRY(launch_ks_howard(shard_args(h, s), V, h->dV, kopt, Vout, st));
+    AIY_TRY(launch_ks_slopes_cols(shard_args(h), h->cols, h->ncols, V, h->dV, st));
+    AIY_TRY(launch_ks_howard(shard_args(h), V, h->dV, kopt, Vout, st));
     return AIY_OK;
 }
 
@@ -139,7 +152,7 @@ int ks_dev_reldiff(ks_dev* h, const double* V, const double* Vold, void* out, vo
     if (!h || !V || !Vold || !out) return fail(AIY_BAD_ARG, "NULL argument");
     hipStream_t st = (hipStream_t)stream;
     AIY_HIP(hipMemsetAsync(h->slots, 0, 2 * kDiffSlots * sizeof(unsigned long long), st));
-    for (int s = 0; s < 4; ++s) AIY_TRY(launch_ks_reldiff(shard_args(h, s), V, Vold, h->slots, st));
+    AIY_TRY(launch_ks_reldiff(shard_args(h), V, Vold, h->slots, st));
     AIY_TRY(launch_reduce_slots(h->slots, out, st));
     return AIY_OK;
 }

@@ -241,6 +241,13 @@ static int ks_vfi_solve_multi_impl(double* value, double* k_opt, const double* k
         A.seg_hint = sh.seg;
         return A;
     };
+    // the four s blocks of a shard in one launch each (blockIdx.y = s)
+    auto args4 = [&](KsShard& sh) {
+        KsArgs A = args(sh, 0);
+        A.ns = 4;
+        A.sstride = (int)(nK * nk);
+        return A;
+    };
     // peer copies of the columns each shard reads from others (after all shards finished)
     auto exchange = [&]() -> int {
         for (auto& sh : S) {
@@ -281,8 +288,7 @@ static int ks_vfi_solve_multi_impl(double* value, double* k_opt, const double* k
             if ((it - 1) % 5 == 0) {
                 KsArgs A0 = args(sh, 0);
                 KS_TRY(launch_ks_slopes_cols(A0, sh.dcols, (int)sh.cols.size(), sh.V, sh.dV, sh.st));
-                for (int si = 0; si < 4; ++si)
-                    KS_TRY(launch_ks_improve(args(sh, si), sh.V, sh.dV, sh.kopt, nullptr, sh.st));
+                KS_TRY(launch_ks_improve(args4(sh), sh.V, sh.dV, sh.kopt, nullptr, sh.st));
             }
         }
         for (int64_t h = 0; h < howard_steps; ++h) {
@@ -290,8 +296,7 @@ static int ks_vfi_solve_multi_impl(double* value, double* k_opt, const double* k
                 KS_CHECK(hipSetDevice(sh.dev));
                 KsArgs A0 = args(sh, 0);
                 KS_TRY(launch_ks_slopes_cols(A0, sh.dcols, (int)sh.cols.size(), sh.V, sh.dV, sh.st));
-                for (int si = 0; si < 4; ++si)
-                    KS_TRY(launch_ks_howard(args(sh, si), sh.V, sh.dV, sh.kopt, sh.V2, sh.st));
+                KS_TRY(launch_ks_howard(args4(sh), sh.V, sh.dV, sh.kopt, sh.V2, sh.st));
                 std::swap(sh.V, sh.V2);
             }
             KS_TRY(exchange());
@@ -300,8 +305,7 @@ static int ks_vfi_solve_multi_impl(double* value, double* k_opt, const double* k
         for (auto& sh : S) {
             KS_CHECK(hipSetDevice(sh.dev));
             KS_CHECK(hipMemsetAsync(sh.slots, 0, 2 * kDiffSlots * sizeof(unsigned long long), sh.st));
-            for (int si = 0; si < 4; ++si)
-                KS_TRY(launch_ks_reldiff(args(sh, si), sh.V, sh.Vold, sh.slots, sh.st));
+            KS_TRY(launch_ks_reldiff(args4(sh), sh.V, sh.Vold, sh.slots, sh.st));
         }
         for (auto& sh : S) {
             KS_CHECK(hipSetDevice(sh.dev));

@@ -18,6 +18,8 @@
 //            the complete VFI loop — improvement every 5th iteration, H Howard sweeps, the
 //            relative-difference stop (:195-203) — in ONE launch (barriers between phases).
 //   tiled    slopes / improve / howard / reldiff as separate grid-wide kernels (any size).
+#include <algorithm>
+
 #include "aiy_common.hpp"
 #include "ks.hpp"
 #include "pchip_dev.hpp"
@@ -181,7 +183,7 @@ __global__ void ks_improve_kernel(KsArgs A, const double* __restrict__ V,
                                   int* __restrict__ nfev) {
     int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= A.n_local) return;
-    int n = A.node0 + t;
+    int n = A.node0 + blockIdx.y * A.sstride + t;
     KsView W{A.k_grid, V, dV};
     int nf = 0;
     const double kp = improve_node(A, W, n, &nf);
@@ -196,7 +198,7 @@ __global__ void ks_howard_kernel(KsArgs A, const double* __restrict__ V,
                                  double* __restrict__ Vn) {
     int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= A.n_local) return;
-    int n = A.node0 + t;
+    int n = A.node0 + blockIdx.y * A.sstride + t;
     KsView W{A.k_grid, V, dV};
     Vn[n] = howard_node(A, W, n, k_opt[n]);
 }
@@ -209,7 +211,7 @@ __global__ void ks_reldiff_kernel(KsArgs A, const double* __restrict__ V,
     bool ok = false;
     double d = 0;
     if (t < A.n_local) {
-        int n = A.node0 + t;
+        int n = A.node0 + blockIdx.y * A.sstride + t;
         d = fabs(V[n] - Vold[n]) / (fabs(Vold[n]) + 1e-10);
         ok = d == d;
     }
@@ -353,19 +355,19 @@ int launch_ks_slopes_cols(const KsArgs& A, const int* cols, int ncols, const dou
 }
 int launch_ks_improve(const KsArgs& A, const double* V, const double* dV, double* kopt,
                       int* nfev, hipStream_t st) {
-    ks_improve_kernel<<<cdiv(A.n_local, 128), 128, 0, st>>>(A, V, dV, kopt, nfev);
+    ks_improve_kernel<<<dim3(cdiv(A.n_local, 128), std::max(A.ns, 1)), 128, 0, st>>>(A, V, dV, kopt, nfev);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }
 int launch_ks_howard(const KsArgs& A, const double* V, const double* dV, const double* kopt,
                      double* Vn, hipStream_t st) {
-    ks_howard_kernel<<<cdiv(A.n_local, 256), 256, 0, st>>>(A, V, dV, kopt, Vn);
+    ks_howard_kernel<<<dim3(cdiv(A.n_local, 256), std::max(A.ns, 1)), 256, 0, st>>>(A, V, dV, kopt, Vn);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }
 int launch_ks_reldiff(const KsArgs& A, const double* V, const double* Vold,
                       unsigned long long* slots, hipStream_t st) {
-    ks_reldiff_kernel<<<cdiv(A.n_local, 256), 256, 0, st>>>(A, V, Vold, slots);
+    ks_reldiff_kernel<<<dim3(cdiv(A.n_local, 256), std::max(A.ns, 1)), 256, 0, st>>>(A, V, Vold, slots);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }

@@ -1,8 +1,9 @@
 """E3 / BASELINE config 5 — the Krusell-Smith VFI (Krusell_Smith_VFI.m:141-204) sharded over
 ranks, one process per GPU, torch.distributed (RCCL over xGMI on GPUs, gloo on CPU).
 
-Rank r owns the aggregate-capital range K in [K0, K1) for all four s (the (K, Z) slices of
-SURVEY §8(e) E3).  Policy improvement is local given V.  A Jacobi Howard sweep reads, for each
+Rank r owns the aggregate-capital range K in [K0, K1) for all four s, or — with more ranks
+than K points — for the two s of one aggregate state z (the (K, Z) slices of SURVEY §8(e) E3,
+`shard_slices`).  Policy improvement is local given V.  A Jacobi Howard sweep reads, for each
 owned node, the value columns at the forecast K'_idx(s, K) for all s' (Krusell_Smith_VFI.m:
 335-349) and nothing else.  So after every sweep a rank receives exactly the columns its
 nodes forecast into that other ranks own (the halo, `halo_plan`; point-to-point isend/irecv
@@ -28,6 +29,30 @@ def shard_range(nK: int, rank: int, world: int):
     return nK * rank // world, nK * (rank + 1) // world
 
 
+def shard_slices(nK: int, rank: int, world: int):
+    """(K0, K1, s0, s1): the rank's shard, K in [K0, K1) of the s blocks [s0, s1).  Up to nK
+    ranks split the K range (all four s each); up to 2·nK ranks split the (K, Z) slices —
+    s = 0, 1 share one aggregate state z, s = 2, 3 the other — half the ranks per z, each half
+    splitting the K range (the reference's K = 4 grid then uses 8 ranks)."""
+    if world <= nK:
+        K0, K1 = shard_range(nK, rank, world)
+        return K0, K1, 0, 4
+    if world > 2 * nK:
+        raise ValueError(f"{world} ranks exceed the 2·K_size = {2 * nK} (K, Z) slices")
+    h = (world + 1) // 2
+    if rank < h:
+        K0, K1 = shard_range(nK, rank, h)
+        return K0, K1, 0, 2
+    K0, K1 = shard_range(nK, rank - h, world - h)
+    return K0, K1, 2, 4
+
+
+def owned_columns(nK: int, rank: int, world: int):
+    """Flat value columns c = s·nK + K (rows of V viewed as (4·nK, k)) the rank owns."""
+    K0, K1, s0, s1 = shard_slices(nK, rank, world)
+    return [s * nK + K for s in range(s0, s1) for K in range(K0, K1)]
+
+
 def forecast_index(K_grid, B, params):
     """K'_idx(s, K), 0-based, shape (4, nK): ks_forecast_index of the C ABI (host-only, the
     same ks_slices the kernels use, so the halo is exactly what they read)."""
@@ -40,23 +65,27 @@ def forecast_index(K_grid, B, params):
 
 
 def halo_plan(kp_idx, nK: int, world: int):
-    """plan[q][p] = sorted K columns rank q reads that rank p owns (p != q; [] on the
-    diagonal): the forecast targets K'_idx(s, K) of q's nodes, all s (:343-349)."""
-    ranges = [shard_range(nK, q, world) for q in range(world)]
-    owner = np.empty(nK, np.int64)
-    for q, (a, b) in enumerate(ranges):
-        owner[a:b] = q
+    """plan[q][p] = sorted flat columns (s'·nK + K') rank q reads that rank p owns (p != q;
+    [] on the diagonal): for every node q owns, the forecast column K'_idx(s, K) of all four
+    s' (Krusell_Smith_VFI.m:343-349)."""
+    owner = np.empty(4 * nK, np.int64)
+    for q in range(world):
+        owner[owned_columns(nK, q, world)] = q
+    kp = np.asarray(kp_idx)
     plan = [[[] for _ in range(world)] for _ in range(world)]
-    for q, (a, b) in enumerate(ranges):
-        need = np.unique(np.asarray(kp_idx)[:, a:b])
+    for q in range(world):
+        K0, K1, s0, s1 = shard_slices(nK, q, world)
+        targets = np.unique(kp[s0:s1, K0:K1])
+        need = sorted({sn * nK + int(t) for t in targets for sn in range(4)})
         for c in need:
             if owner[c] != q:
-                plan[q][int(owner[c])].append(int(c))
+                plan[q][int(owner[c])].append(c)
     return plan
 
 
 class HaloExchange:
-    """Per-sweep exchange of the halo columns (4 x len x k slabs of V) between ranks."""
+    """Per-sweep exchange of the halo columns (rows of V viewed as (4·nK, k)) between ranks:
+    one batched set of point-to-point sends/receives (RCCL over xGMI on GPUs)."""
 
     def __init__(self, plan, rank: int, world: int, device, nk: int, dtype):
         import torch
@@ -69,7 +98,7 @@ class HaloExchange:
                 self.sends.append((p, torch.tensor(plan[p][rank], device=device)))
             if plan[rank][p]:   # what I read from p
                 cols = torch.tensor(plan[rank][p], device=device)
-                self.recvs.append((p, cols, torch.empty((4, len(plan[rank][p]), nk),
+                self.recvs.append((p, cols, torch.empty((len(plan[rank][p]), nk),
                                                         dtype=dtype, device=device)))
         self.columns = sum(len(c) for _, c, _ in self.recvs)
 
@@ -77,9 +106,10 @@ class HaloExchange:
         import torch
         import torch.distributed as dist
         nccl = dist.get_backend() == "nccl"
+        flat = V.view(-1, V.shape[-1])
         ops, staged = [], []
         for p, cols in self.sends:
-            buf = V.index_select(1, cols)
+            buf = flat.index_select(0, cols)
             ops.append(dist.P2POp(dist.isend, buf if nccl else buf.cpu(), p))
         for p, cols, buf in self.recvs:
             rb = buf if nccl else torch.empty(buf.shape, dtype=buf.dtype)
@@ -89,22 +119,24 @@ class HaloExchange:
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
         for cols, rb in staged:
-            V.index_copy_(1, cols, rb.to(V.device))
+            flat.index_copy_(0, cols, rb.to(V.device))
 
 
 class HipShard:
-    """The device-tier handle (ks_dev_*) for this rank's K range."""
+    """The device-tier handle (ks_dev_*) for this rank's shard: K in [K0, K1) of the s blocks
+    [s0, s1) (all four by default; one z's pair for (K, Z) slices)."""
 
-    def __init__(self, k_grid, K_grid, B, P, params, K0, K1):
+    def __init__(self, k_grid, K_grid, B, P, params, K0, K1, s0=0, s1=4):
         kg = np.ascontiguousarray(k_grid, np.float64)
         Kg = np.ascontiguousarray(K_grid, np.float64)
-        self.K0, self.K1 = K0, K1
+        self.K0, self.K1, self.s0, self.s1 = K0, K1, s0, s1
         self.kp_idx = forecast_index(Kg, B, params)
         h = vp()
-        check(lib().ks_dev_create(ptr(kg), ptr(Kg), ptr(np.ascontiguousarray(B, np.float64)),
-                                  ptr(np.asfortranarray(P, dtype=np.float64)),
-                                  ptr(np.ascontiguousarray(params, np.float64)), i64(kg.size),
-                                  i64(Kg.size), i64(K0), i64(K1), C.byref(h)))
+        check(lib().ks_dev_create_slice(ptr(kg), ptr(Kg), ptr(np.ascontiguousarray(B, np.float64)),
+                                        ptr(np.asfortranarray(P, dtype=np.float64)),
+                                        ptr(np.ascontiguousarray(params, np.float64)),
+                                        i64(kg.size), i64(Kg.size), i64(K0), i64(K1), i64(s0),
+                                        i64(s1), C.byref(h)))
         self._h = h
 
     def close(self):
@@ -132,24 +164,26 @@ class HipShard:
         return float(o[0:1].view(torch.float64)[0]) if int(o[1]) != 0 else math.nan
 
 
-def _exchange(V, K0, K1, rank, world, nK):
-    """All-gather the owned (4, K1-K0, k) slices of V into every rank's V (in place)."""
+def _exchange(V, rank, world, nK):
+    """All-gather every rank's owned columns of V (rows of the (4·nK, k) view) into every
+    rank's V, in place."""
     import torch
     import torch.distributed as dist
-    ranges = [shard_range(nK, q, world) for q in range(world)]
-    kmax = max(b - a for a, b in ranges)
-    mine = torch.zeros((4, kmax, V.shape[2]), dtype=V.dtype, device=V.device)
-    mine[:, :K1 - K0, :] = V[:, K0:K1, :]
+    cols = [owned_columns(nK, q, world) for q in range(world)]
+    m = max(len(c) for c in cols)
+    flat = V.view(-1, V.shape[-1])
+    mine = torch.zeros((m, flat.shape[1]), dtype=V.dtype, device=V.device)
+    mine[:len(cols[rank])] = flat.index_select(0, torch.tensor(cols[rank], device=V.device))
     if dist.get_backend() == "nccl":
-        out = torch.empty((world,) + tuple(mine.shape), dtype=V.dtype, device=V.device)
+        out = torch.empty((world, m, flat.shape[1]), dtype=V.dtype, device=V.device)
         dist.all_gather_into_tensor(out, mine)
     else:  # gloo: stage through host memory
         parts = [torch.empty_like(mine, device="cpu") for _ in range(world)]
         dist.all_gather(parts, mine.cpu())
         out = torch.stack(parts).to(V.device)
-    for q, (a, b) in enumerate(ranges):
+    for q in range(world):
         if q != rank:
-            V[:, a:b, :] = out[q, :, :b - a, :]
+            flat.index_copy_(0, torch.tensor(cols[q], device=V.device), out[q, :len(cols[q])])
 
 
 def _allreduce_max(x: float, device):
@@ -173,7 +207,8 @@ def ks_vfi_solve_dist(value, k_opt, shard, nK, howard_steps=50, tol=1e-6, max_vf
     import torch
     import torch.distributed as dist
     V = value
-    K0, K1 = shard.K0, shard.K1
+    nk = V.shape[-1]
+    own = torch.tensor(owned_columns(nK, rank, world), device=V.device)
     halo = None
     if world > 1:
         dist.barrier()   # first collective on every rank before any point-to-point
@@ -181,10 +216,12 @@ def ks_vfi_solve_dist(value, k_opt, shard, nK, howard_steps=50, tol=1e-6, max_vf
             plan = halo_plan(shard.kp_idx, nK, world)
             halo = HaloExchange(plan, rank, world, V.device, V.shape[2], V.dtype)
             if poison:
-                keep = set(range(K0, K1)) | {c for p in range(world) for c in plan[rank][p]}
-                for c in range(nK):
+                keep = set(owned_columns(nK, rank, world)) | \
+                    {c for p in range(world) for c in plan[rank][p]}
+                flat = V.view(-1, nk)
+                for c in range(4 * nK):
                     if c not in keep:
-                        V[:, c, :] = math.nan
+                        flat[c] = math.nan
         elif exchange != "allgather":
             raise ValueError(f"exchange must be 'halo' or 'allgather', not {exchange!r}")
     V2 = V.clone()
@@ -195,23 +232,24 @@ def ks_vfi_solve_dist(value, k_opt, shard, nK, howard_steps=50, tol=1e-6, max_vf
             shard.improve(V, k_opt)
         for _ in range(howard_steps):                      # Jacobi Howard sweeps (:172-192)
             shard.howard(V, k_opt, V2)
-            if halo is None:
-                V2[:, :K0, :] = V[:, :K0, :]
-                V2[:, K1:, :] = V[:, K1:, :]
+            if halo is None:  # V2 holds the shard's new nodes; carry the rest over, then gather
+                fresh = V2.view(-1, nk).index_select(0, own)
+                V2.copy_(V)
+                V2.view(-1, nk).index_copy_(0, own, fresh)
             V, V2 = V2, V
             if halo is not None:
                 halo(V)
             elif world > 1:
-                _exchange(V, K0, K1, rank, world, nK)
+                _exchange(V, rank, world, nK)
         rel = shard.reldiff(V, Vold)                       # :195
         if world > 1:
             rel = _allreduce_max(rel, V.device)
         if rel < tol:
             break
     if world > 1:                                          # every rank leaves with all of both
-        _exchange(k_opt, K0, K1, rank, world, nK)
+        _exchange(k_opt, rank, world, nK)
         if halo is not None:
-            _exchange(V, K0, K1, rank, world, nK)
+            _exchange(V, rank, world, nK)
     if V is not value:
         value.copy_(V)
     return it, rel

@@ -33,8 +33,9 @@ def ks_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, exchange="halo", r
     kd = pkg.ks_dist
     kg, Kg, P, V0 = pkg.calibration.krusell_smith(k_size=nk, K_size=nK)
     B = np.array([0.1, 0.97, 0.08, 0.975])
-    K0, K1 = kd.shard_range(nK, rank, world)
-    sh = kd.HipShard(kg, Kg, B, P, pkg.ks_params(), K0, K1)
+    K0, K1, s0, s1 = kd.shard_slices(nK, rank, world)
+    sh = kd.HipShard(kg, Kg, B, P, pkg.ks_params(), K0, K1, s0, s1)
+    own = torch.tensor(kd.owned_columns(nK, rank, world), device=dev)
     V = torch.as_tensor(np.ascontiguousarray(V0.transpose(2, 1, 0)), device=dev)
     V2 = V.clone()
     ko = torch.ones_like(V)
@@ -49,14 +50,15 @@ def ks_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, exchange="halo", r
         nonlocal V, V2
         for _ in range(n):
             sh.howard(V, ko, V2)
-            if halo is None:
-                V2[:, :K0, :] = V[:, :K0, :]
-                V2[:, K1:, :] = V[:, K1:, :]
+            if halo is None and world > 1:
+                fresh = V2.view(-1, nk).index_select(0, own)
+                V2.copy_(V)
+                V2.view(-1, nk).index_copy_(0, own, fresh)
             V, V2 = V2, V
             if halo is not None:
                 halo(V)
             elif world > 1:
-                kd._exchange(V, K0, K1, rank, world, nK)
+                kd._exchange(V, rank, world, nK)
 
     def sync():
         torch.cuda.synchronize()
@@ -84,7 +86,7 @@ def ks_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, exchange="halo", r
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ti, th = float(t[0]), float(t[1])
     nodes = nk * nK * 4
-    cols = halo.columns if halo is not None else (nK - (K1 - K0) if world > 1 else 0)
+    cols = halo.columns if halo is not None else (4 * nK - len(own) if world > 1 else 0)
     sh.close()
     # Algorithmic bytes per node and Howard sweep (each array touched once): the slope rebuild
     # reads V and writes dV (16 B); the sweep reads k_opt and the segment hint (12 B), the V/dV
@@ -104,8 +106,9 @@ def ks_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, exchange="halo", r
             "workload": f"Krusell_Smith_VFI k={nk} K={nK} S=4 ({nodes} nodes, BASELINE "
                         f"configs[4] scaling size), ALM B={[float(b) for b in B]}, one VFI "
                         f"iteration = improvement + {howard} Howard sweeps, median of {reps}",
-            "parallelism": f"K-range shards over {world} ranks, {exchange} exchange per "
-                           f"Howard sweep (rank 0 receives {cols} K columns x 4 s)"}
+            "parallelism": f"(K, Z) shards over {world} ranks (rank 0: K [{K0}, {K1}), s "
+                           f"[{s0}, {s1})), {exchange} exchange per Howard sweep (rank 0 "
+                           f"receives {cols} (s, K) columns of {nk} values)"}
 
 
 def main():

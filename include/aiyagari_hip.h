@@ -295,6 +295,12 @@ typedef struct ks_dev ks_dev;
 int ks_dev_create(const double* k_grid, const double* K_grid, const double* B, const double* P,
                   const double* params, int64_t nk, int64_t nK, int64_t K0, int64_t K1,
                   ks_dev** out);
+/* (K, Z) slices: the shard K in [K0, K1) of the s blocks [s0, s1) only —
+ * s = 0, 1 share the first aggregate state z and s = 2, 3 the second, so [0, 2) / [2, 4) are
+ * the two Z slices of a K range.  ks_dev_create(...) == ks_dev_create_slice(..., 0, 4, ...). */
+int ks_dev_create_slice(const double* k_grid, const double* K_grid, const double* B,
+                        const double* P, const double* params, int64_t nk, int64_t nK,
+                        int64_t K0, int64_t K1, int64_t s0, int64_t s1, ks_dev** out);
 int ks_dev_destroy(ks_dev* h);
 /* :148-168 policy improvement (pchip slopes + fminbnd) on the shard */
 int ks_dev_improve(ks_dev* h, const double* V, double* kopt, void* stream);

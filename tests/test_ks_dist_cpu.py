@@ -24,8 +24,9 @@ def _pkg():
 class OracleShard:
     """Shard backend on the C restatement (tensors (4, K, k) on CPU)."""
 
-    def __init__(self, p, kg, Kg, B, P, K0, K1):
+    def __init__(self, p, kg, Kg, B, P, K0, K1, s0=0, s1=4):
         self.p, self.kg, self.Kg, self.B, self.P, self.K0, self.K1 = p, kg, Kg, B, P, K0, K1
+        self.s0, self.s1 = s0, s1
 
     @staticmethod
     def _np(V):
@@ -36,7 +37,7 @@ class OracleShard:
         import torch
         ko, _ = corc.ks_policy_improve(self.p, self.kg, self.Kg, self._np(V), self.B, self.P)
         kt = torch.from_numpy(np.ascontiguousarray(ko.transpose(2, 1, 0)))
-        kopt[:, self.K0:self.K1, :] = kt[:, self.K0:self.K1, :]
+        kopt[self.s0:self.s1, self.K0:self.K1, :] = kt[self.s0:self.s1, self.K0:self.K1, :]
 
     def howard(self, V, kopt, Vout):
         from oracle import corc
@@ -44,10 +45,11 @@ class OracleShard:
         Vn = corc.ks_howard(self.p, self.kg, self.Kg, self._np(V), self._np(kopt), self.B,
                             self.P, 1)
         vt = torch.from_numpy(np.ascontiguousarray(Vn.transpose(2, 1, 0)))
-        Vout[:, self.K0:self.K1, :] = vt[:, self.K0:self.K1, :]
+        Vout[self.s0:self.s1, self.K0:self.K1, :] = vt[self.s0:self.s1, self.K0:self.K1, :]
 
     def reldiff(self, V, Vold):
-        a, b = V[:, self.K0:self.K1, :].numpy(), Vold[:, self.K0:self.K1, :].numpy()
+        a = V[self.s0:self.s1, self.K0:self.K1, :].numpy()
+        b = Vold[self.s0:self.s1, self.K0:self.K1, :].numpy()
         d = np.abs(a - b) / (np.abs(b) + 1e-10)
         return float(np.nanmax(d)) if not np.all(np.isnan(d)) else math.nan
 
@@ -71,10 +73,10 @@ def _worker(rank, world, port, outdir, nK, exchange="halo"):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     kd = _pkg().ks_dist
     cp, kg, Kg, P, V0, B = _setup(nK)
-    K0, K1 = kd.shard_range(len(Kg), rank, world)
+    K0, K1, s0, s1 = kd.shard_slices(len(Kg), rank, world)
     V = torch.from_numpy(np.ascontiguousarray(V0.transpose(2, 1, 0)))
     ko = torch.ones_like(V)
-    sh = OracleShard(cp, kg, Kg, B, P, K0, K1)
+    sh = OracleShard(cp, kg, Kg, B, P, K0, K1, s0, s1)
     sh.kp_idx = kd.forecast_index(Kg, B, _pkg().ks_params())  # host-only C ABI call
     it, rel = kd.ks_vfi_solve_dist(V, ko, sh, len(Kg), howard_steps=3, tol=1e-6, max_vfi=6,
                                    rank=rank, world=world, exchange=exchange,
@@ -86,7 +88,8 @@ def _worker(rank, world, port, outdir, nK, exchange="halo"):
 
 
 @pytest.mark.parametrize("world,nK,exchange", [(2, 4, "halo"), (3, 5, "halo"), (3, 8, "halo"),
-                                               (2, 4, "allgather")])
+                                               (2, 4, "allgather"), (4, 2, "halo"),
+                                               (3, 2, "allgather")])
 def test_gloo_sharded_equals_unsharded(tmp_path, world, nK, exchange):
     """Halo runs poison every column a rank neither owns nor reads with NaN: equality with the
     unsharded solve then proves the halo plan covers every read."""
@@ -116,6 +119,25 @@ def test_shard_ranges_cover():
             assert all(rs[i][1] == rs[i + 1][0] and rs[i][0] < rs[i][1] for i in range(world - 1))
 
 
+@pytest.mark.parametrize("nK", [1, 2, 3, 4, 5, 64])
+def test_kz_slices_partition_every_node(nK):
+    """(K, Z) slices: up to 2·nK ranks, every (s, K) column owned by exactly one rank, every
+    shard non-empty; the reference's K = 4 grid spreads over 8 ranks as one (K, z) each."""
+    kd = _pkg().ks_dist
+    for world in range(1, 2 * nK + 1):
+        seen = []
+        for r in range(world):
+            K0, K1, s0, s1 = kd.shard_slices(nK, r, world)
+            assert 0 <= K0 < K1 <= nK and (s0, s1) in ((0, 4), (0, 2), (2, 4))
+            seen += kd.owned_columns(nK, r, world)
+        assert sorted(seen) == list(range(4 * nK))
+    with pytest.raises(ValueError):
+        kd.shard_slices(nK, 0, 2 * nK + 1)
+    if nK == 4:
+        assert [kd.shard_slices(4, r, 8) for r in range(8)] == \
+            [(K, K + 1, 0, 2) for K in range(4)] + [(K, K + 1, 2, 4) for K in range(4)]
+
+
 def test_forecast_index_and_halo_plan():
     """ks_forecast_index (host-only) is the clamp + nearest-index rule of bellman_value
     (Krusell_Smith_VFI.m:335-343); halo_plan lists exactly the foreign columns a rank reads."""
@@ -132,16 +154,18 @@ def test_forecast_index_and_halo_plan():
             Kp = np.clip(np.exp(b0 + b1 * np.log(Kg)), Kg[0], Kg[-1])
             want = np.argmin(np.abs(Kg[None, :] - Kp[:, None]), axis=1)
             assert np.array_equal(kp[s], want)
-        for world in (2, 3, 8):
-            plan = kd.halo_plan(kp, 64, world)
+        for nK, world in ((64, 2), (64, 3), (64, 8), (4, 8), (4, 6)):
+            kpn = kd.forecast_index(np.linspace(30.0, 50.0, nK), B, prm) if nK != 64 else kp
+            plan = kd.halo_plan(kpn, nK, world)
             for q in range(world):
-                a, b = kd.shard_range(64, q, world)
-                need = set(np.unique(kp[:, a:b]).tolist()) - set(range(a, b))
+                K0, K1, s0, s1 = kd.shard_slices(nK, q, world)
+                mine = set(kd.owned_columns(nK, q, world))
+                targets = np.unique(kpn[s0:s1, K0:K1]).tolist()
+                need = {sn * nK + t for t in targets for sn in range(4)} - mine
                 got = [c for p in range(world) for c in plan[q][p]]
                 assert sorted(got) == sorted(need) and not plan[q][q]
                 for p in range(world):
-                    pa, pb = kd.shard_range(64, p, world)
-                    assert all(pa <= c < pb for c in plan[q][p])
+                    assert set(plan[q][p]) <= set(kd.owned_columns(nK, p, world))
     # identity ALM: every node forecasts its own K, so no halo at all
     kp = kd.forecast_index(Kg, np.array([0.0, 1.0, 0.0, 1.0]), prm)
     assert np.array_equal(kp, np.tile(np.arange(64), (4, 1)))

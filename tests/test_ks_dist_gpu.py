@@ -31,8 +31,8 @@ def _run(rank, world, nK, steps=8, vfi=7, exchange="halo"):
     pkg = _pkg()
     kg, Kg, P, V0 = _setup(nK)
     prm = pkg.ks_params()
-    K0, K1 = pkg.ks_dist.shard_range(nK, rank, world)
-    sh = pkg.ks_dist.HipShard(kg, Kg, B_ALM, P, prm, K0, K1)
+    K0, K1, s0, s1 = pkg.ks_dist.shard_slices(nK, rank, world)
+    sh = pkg.ks_dist.HipShard(kg, Kg, B_ALM, P, prm, K0, K1, s0, s1)
     V = torch.as_tensor(np.ascontiguousarray(V0.transpose(2, 1, 0)), device="cuda:0")
     ko = torch.ones_like(V)
     it, rel = pkg.ks_dist.ks_vfi_solve_dist(V, ko, sh, nK, howard_steps=steps, tol=1e-6,
@@ -77,6 +77,20 @@ def test_two_ranks_gloo_equal_single_device(pkg, gpu, tmp_path, nK, exchange):
     mp.spawn(_worker, args=(2, port, str(tmp_path), nK, exchange), nprocs=2, join=True)
     Vr, kr, itr, relr = _reference(nK)
     for rank in range(2):
+        assert np.array_equal(np.load(Path(tmp_path, f"V{rank}.npy")), Vr)
+        assert np.array_equal(np.load(Path(tmp_path, f"k{rank}.npy")), kr)
+        assert json.loads(Path(tmp_path, f"m{rank}.json").read_text())["it"] == itr
+
+
+@pytest.mark.parametrize("world,nK,exchange", [(8, 4, "halo"), (6, 4, "allgather")])
+def test_kz_slices_on_one_card(pkg, gpu, tmp_path, world, nK, exchange):
+    """(K, Z) slices: the reference's K = 4 grid over 8 ranks (one (K, z) pair each) and over 6,
+    HIP shards of the device tier (ks_dev_create_slice) sharing the card, gloo exchange."""
+    import torch.multiprocessing as mp
+    port = 29900 + (os.getpid() % 1000) + world + 10 * (exchange == "halo")
+    mp.spawn(_worker, args=(world, port, str(tmp_path), nK, exchange), nprocs=world, join=True)
+    Vr, kr, itr, relr = _reference(nK)
+    for rank in range(world):
         assert np.array_equal(np.load(Path(tmp_path, f"V{rank}.npy")), Vr)
         assert np.array_equal(np.load(Path(tmp_path, f"k{rank}.npy")), kr)
         assert json.loads(Path(tmp_path, f"m{rank}.json").read_text())["it"] == itr
