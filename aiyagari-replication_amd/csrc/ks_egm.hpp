@@ -28,4 +28,7 @@ struct KsEgmOut {
 size_t ks_egm_lds_bytes(int nk, int nK);
 bool ks_egm_fits(int nk, int nK);
 int launch_ks_egm_solve(const KsEgmArgs& A, double* kopt, KsEgmOut* out, hipStream_t st);
+size_t ks_egm_jacobi_lds_bytes(int nk);
+int launch_ks_egm_jacobi(const KsEgmArgs& A, const double* src, double* dst,
+                         unsigned long long* slots, int* status, hipStream_t st);
 }  // namespace aiy

@@ -13,6 +13,8 @@
 #include "ks_egm.hpp"
 #include "ws.hpp"
 
+#include <algorithm>
+
 namespace aiy {
 
 // per-pair scalars in the script's order with libm (:101-112 tables, :139-175)
@@ -125,6 +127,93 @@ int ks_egm_solve(double* k_opt, const double* k_grid, const double* K_grid, cons
     if (o.status)
         return fail(AIY_NON_FINITE, "an (s, K) pair had fewer than 2 valid EGM points "
                                     "(griddedInterpolant needs two; Krusell_Smith_EGM.m:196)");
+    return AIY_OK;
+}
+
+// F1 — the Jacobi variant of the KS EGM iteration: every (s, K) pair of a sweep reads the
+// previous sweep's k_opt, all pairs of a sweep in one launch.  NOT the reference's result (the
+// script is Gauss-Seidel, Krusell_Smith_EGM.m:199); same stop rule (:204-207).  Sweeps are
+// enqueued in batches with one diff-slot set each and read back once per batch.
+int ks_egm_solve_jacobi(double* k_opt, const double* k_grid, const double* K_grid,
+                        const double* B, const double* P, const double* params, int64_t nk,
+                        int64_t nK, double tol, int64_t max_iter, int64_t* iters, double* diff) {
+    if (!k_opt || !k_grid || !K_grid || !B || !P || !params || !iters || !diff)
+        return fail(AIY_BAD_ARG, "NULL argument");
+    if (nk < 3 || nK < 1) return fail(AIY_BAD_SHAPE, "need k_size >= 3 and K_size >= 1");
+    if (ks_egm_jacobi_lds_bytes((int)nk) > 150 * 1024)
+        return fail(AIY_BAD_SHAPE, "k_size too large for one workgroup per (s, K) pair");
+    if (max_iter < 1 || max_iter > 2147483647) return fail(AIY_BAD_ARG, "max_iter in [1, 2^31)");
+    AIY_TRY(check_grid(k_grid, nk));
+    for (int64_t q = 0; q < nK; ++q)
+        if (!(K_grid[q] > 0) || !std::isfinite(K_grid[q]))
+            return fail(AIY_NON_FINITE, "K_grid must be positive and finite");
+    std::lock_guard<std::mutex> lk(host_mutex());
+    HostCtx* c;
+    AIY_TRY(get_ctx(4 * nK, nk, 1, &c));
+    std::vector<KsEgmPair> pairs;
+    ks_egm_pairs(params, K_grid, B, (int)nK, pairs);
+    double Pr[16];
+    for (int i = 0; i < 4; ++i)
+        for (int m = 0; m < 4; ++m) Pr[i * 4 + m] = P[i + m * 4];
+    const size_t n = (size_t)nk * nK * 4;
+    constexpr int kBatch = 16;
+    // ring of kBatch + 1 policy buffers: sweep g reads slot (g-1) % R and writes slot g % R, so
+    // the sweeps a batch runs past the stopping sweep never overwrite its output
+    constexpr int R = kBatch + 1;
+    double *dkg, *dP, *ring;
+    KsEgmPair* dpairs;
+    unsigned long long* dslots;
+    int* dstatus;
+    AIY_TRY(c->buf("egmj_kg", nk * sizeof(double), (void**)&dkg));
+    AIY_TRY(c->buf("egmj_P", sizeof Pr, (void**)&dP));
+    AIY_TRY(c->buf("egmj_ring", (size_t)R * n * sizeof(double), (void**)&ring));
+    AIY_TRY(c->buf("egmj_pairs", pairs.size() * sizeof(KsEgmPair), (void**)&dpairs));
+    AIY_TRY(c->buf("egmj_slots", kBatch * 2 * kDiffSlots * sizeof(unsigned long long), (void**)&dslots));
+    AIY_TRY(c->buf("egmj_status", sizeof(int), (void**)&dstatus));
+    AIY_HIP(hipMemcpyAsync(dkg, k_grid, nk * sizeof(double), hipMemcpyHostToDevice, c->st));
+    AIY_HIP(hipMemcpyAsync(dP, Pr, sizeof Pr, hipMemcpyHostToDevice, c->st));
+    AIY_HIP(hipMemcpyAsync(ring, k_opt, n * sizeof(double), hipMemcpyHostToDevice, c->st));
+    AIY_HIP(hipMemcpyAsync(dpairs, pairs.data(), pairs.size() * sizeof(KsEgmPair),
+                           hipMemcpyHostToDevice, c->st));
+    AIY_HIP(hipMemsetAsync(dstatus, 0, sizeof(int), c->st));
+    KsEgmArgs A{};
+    A.nk = (int)nk; A.nK = (int)nK; A.max_iter = (int)max_iter; A.k_grid = dkg; A.P = dP;
+    A.pairs = dpairs; A.beta = params[0]; A.k_min = params[3]; A.k_max = params[4]; A.tol = tol;
+    auto slot = [&](int64_t g) { return ring + (size_t)(g % R) * n; };
+    std::vector<unsigned long long> hs(kBatch * 2 * kDiffSlots);
+    int64_t done = 0, stop = 0;
+    double d_last = NAN;
+    int status = 0;
+    while (!stop && done < max_iter) {
+        const int64_t m = std::min<int64_t>(kBatch, max_iter - done);
+        AIY_HIP(hipMemsetAsync(dslots, 0, m * 2 * kDiffSlots * sizeof(unsigned long long), c->st));
+        for (int64_t t = 0; t < m; ++t) {
+            const int64_t g = done + 1 + t;
+            AIY_TRY(launch_ks_egm_jacobi(A, slot(g - 1), slot(g),
+                                         dslots + t * 2 * kDiffSlots, dstatus, c->st));
+        }
+        AIY_HIP(hipMemcpyAsync(hs.data(), dslots, m * 2 * kDiffSlots * sizeof(unsigned long long),
+                               hipMemcpyDeviceToHost, c->st));
+        AIY_HIP(hipMemcpyAsync(&status, dstatus, sizeof(int), hipMemcpyDeviceToHost, c->st));
+        AIY_HIP(hipStreamSynchronize(c->st));
+        if (status) break;
+        for (int64_t t = 0; t < m; ++t) {
+            d_last = fold_slots_host(hs.data() + t * 2 * kDiffSlots);
+            if (d_last < tol) {
+                stop = done + 1 + t;
+                break;
+            }
+        }
+        if (!stop) done += m;
+    }
+    if (status)
+        return fail(AIY_NON_FINITE, "an (s, K) pair had fewer than 2 valid EGM points "
+                                    "(griddedInterpolant needs two; Krusell_Smith_EGM.m:196)");
+    const int64_t g = stop ? stop : max_iter;
+    AIY_HIP(hipMemcpyAsync(k_opt, slot(g), n * sizeof(double), hipMemcpyDeviceToHost, c->st));
+    AIY_HIP(hipStreamSynchronize(c->st));
+    *iters = g;
+    *diff = d_last;
     return AIY_OK;
 }
 

@@ -138,6 +138,100 @@ __global__ __launch_bounds__(kEgmThreads) void ks_egm_solve_kernel(KsEgmArgs A, 
     }
 }
 
+// F1 — the Jacobi variant (NOT the reference's result: the script is Gauss-Seidel, :199).
+// Every (s_i, K_i) pair of a sweep reads the previous sweep's k_opt (`src`), so the pairs are
+// independent: one workgroup per pair, all pairs of a sweep in one launch (4·K_size-way
+// parallel instead of one workgroup walking them in order).  The per-pair phases A/B/C are the
+// Gauss-Seidel kernel's; each workgroup also folds max|dst - src| over its column (NaN ignored)
+// into the sweep's diff slots for the stop rule (:204).
+__global__ __launch_bounds__(kEgmThreads) void ks_egm_jacobi_kernel(KsEgmArgs A,
+                                                                    const double* __restrict__ src,
+                                                                    double* __restrict__ dst,
+                                                                    unsigned long long* slots,
+                                                                    int* status) {
+    extern __shared__ double lds[];
+    const int nk = A.nk, nK = A.nK;
+    double* kg = lds;
+    double* kc = kg + nk;
+    double* xs = kc + nk;
+    double* ys = xs + nk;
+    __shared__ int s_lo, s_nv;
+    const int tid = threadIdx.x;
+    const int pair = blockIdx.x, s_i = pair / nK;
+    const KsEgmPair& pr = A.pairs[pair];
+    for (int q = tid; q < nk; q += blockDim.x) kg[q] = A.k_grid[q];
+    if (tid == 0) {
+        s_lo = 0;
+        s_nv = 0;
+    }
+    __syncthreads();
+    for (int t = tid; t < nk; t += blockDim.x) {  // A (:155-189)
+        const double kp = kg[t];
+        const int seg = seg_of_dev(kg, nk, kp);
+        double em = 0.0;
+#pragma unroll
+        for (int s_j = 0; s_j < 4; ++s_j) {
+            const double* col = src + (size_t)(s_j * nK + pr.kd[s_j]) * nk;
+            const double kpn = pchip_local(kg, col, nk, seg, kp);
+            const double cn = fmax((pr.Rn[s_j] * kp + pr.Wn[s_j]) - kpn, 1e-8);
+            em = em + (A.P[s_i * 4 + s_j] * pr.Rn[s_j]) / cn;
+        }
+        const double c = 1 / (A.beta * em);
+        kc[t] = ((c + kp) - pr.We) / pr.R;
+    }
+    __syncthreads();
+    for (int t = tid; t < nk; t += blockDim.x) {  // B (:193-195)
+        const double v = kc[t];
+        int rank = 0;
+        for (int j = 0; j < nk; ++j) {
+            const double u = kc[j];
+            rank += (sort_gt(v, u) || (j < t && !sort_gt(u, v))) ? 1 : 0;
+        }
+        xs[rank] = v;
+        ys[rank] = kg[t];
+        if (v < A.k_min) atomicAdd(&s_lo, 1);
+        if (v >= A.k_min && v <= A.k_max) atomicAdd(&s_nv, 1);
+    }
+    __syncthreads();
+    const int lo = s_lo, nv = s_nv;
+    if (nv < 2) {  // block-uniform: griddedInterpolant needs two points
+        if (tid == 0) atomicOr(status, 1);
+        block_max_to_slots(false, 0.0, slots);
+        return;
+    }
+    const double* x = xs + lo;
+    const double* y = ys + lo;
+    const size_t base = (size_t)pair * nk;
+    bool ok = false;
+    double dmax = 0.0;
+    for (int t = tid; t < nk; t += blockDim.x) {  // C (:196-199)
+        const double q = kg[t];
+        double v;
+        if (q < x[0]) v = y[0];
+        else if (q > x[nv - 1]) v = y[nv - 1];
+        else v = pchip_local(x, y, nv, seg_of_dev(x, nv, q), q);
+        v = fmin(v, A.k_max);
+        v = fmax(v, A.k_min);
+        dst[base + t] = v;
+        const double d = fabs(v - src[base + t]);
+        if (d == d) {
+            dmax = ok ? fmax(dmax, d) : d;
+            ok = true;
+        }
+    }
+    block_max_to_slots(ok, dmax, slots);
+}
+
+size_t ks_egm_jacobi_lds_bytes(int nk) { return sizeof(double) * 4ull * nk; }
+
+int launch_ks_egm_jacobi(const KsEgmArgs& A, const double* src, double* dst,
+                         unsigned long long* slots, int* status, hipStream_t st) {
+    ks_egm_jacobi_kernel<<<4 * A.nK, kEgmThreads, ks_egm_jacobi_lds_bytes(A.nk), st>>>(
+        A, src, dst, slots, status);
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
+}
+
 size_t ks_egm_lds_bytes(int nk, int nK) {
     return sizeof(double) * (4ull * nk + 2ull * nk * nK * 4);
 }

@@ -63,13 +63,16 @@ def ks_vfi_solve(value, k_opt, k_grid, K_grid, B, P, params, howard_steps=50, to
     return dict(value=V, k_opt=ko, iters=it.value, rel_diff=rel.value)
 
 
-def ks_egm_solve(k_opt, k_grid, K_grid, B, P, params, tol=1e-6, max_iter=10000):
+def ks_egm_solve(k_opt, k_grid, K_grid, B, P, params, tol=1e-6, max_iter=10000, jacobi=False):
     """A8 — replaces the EGM loop of Krusell_Smith_EGM.m:130-209 for one ALM vector B
-    (Gauss-Seidel over (s, K) as the script).  Returns dict(k_opt, iters, diff)."""
+    (Gauss-Seidel over (s, K) as the script).  jacobi=True: the F1 Jacobi variant
+    (ks_egm_solve_jacobi — NOT the reference's result, all pairs of a sweep in parallel).
+    Returns dict(k_opt, iters, diff)."""
     ko = np.array(k_opt, dtype=np.float64, order="F", copy=True)
     nk, nK, nS = ko.shape
     kg, Kg, B, P, prm = _arrs(k_grid, K_grid, B, P, params)
     it, diff = C.c_int64(), C.c_double()
-    check(lib().ks_egm_solve(ptr(ko), ptr(kg), ptr(Kg), ptr(B), ptr(P), ptr(prm), i64(nk),
-                             i64(nK), d(tol), i64(max_iter), C.byref(it), C.byref(diff)))
+    fn = lib().ks_egm_solve_jacobi if jacobi else lib().ks_egm_solve
+    check(fn(ptr(ko), ptr(kg), ptr(Kg), ptr(B), ptr(P), ptr(prm), i64(nk), i64(nK), d(tol),
+             i64(max_iter), C.byref(it), C.byref(diff)))
     return dict(k_opt=ko, iters=it.value, diff=diff.value)

@@ -169,6 +169,16 @@ int ks_egm_solve(double* k_opt, const double* k_grid, const double* K_grid, cons
                  const double* P, const double* params, int64_t nk, int64_t nK, double tol,
                  int64_t max_iter, int64_t* iters, double* diff);
 
+/* F1 — the Jacobi variant of A8, flagged NON-PARITY: every (s, K) pair of a
+ * sweep reads the previous sweep's k_opt (the script is Gauss-Seidel, Krusell_Smith_EGM.m:199,
+ * so this converges to the same fixed point within tol but along a different path and in a
+ * different number of sweeps).  All pairs of a sweep run in parallel, one workgroup each.
+ * Same arguments, layout, stop rule and errors as ks_egm_solve; bit-exact against the C/numpy
+ * Jacobi restatements (oracle/). */
+int ks_egm_solve_jacobi(double* k_opt, const double* k_grid, const double* K_grid,
+                        const double* B, const double* P, const double* params, int64_t nk,
+                        int64_t nK, double tol, int64_t max_iter, int64_t* iters, double* diff);
+
 /* F3 — replaces the shock simulation Krusell_Smith_VFI.m:57-94 (also Krusell_Smith_EGM.m).
  * uniforms: the script's `rand` stream, ks_shock_draws(T, population) values in its draw order
  * (T-1 aggregate draws :63/:65, `population` draws :71, then (T-1)*population draws with t

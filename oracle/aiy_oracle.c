@@ -681,8 +681,20 @@ static void pchip_slopes_n(int64_t n, const double* x, const double* y, double* 
 }
 
 /* One Gauss-Seidel sweep (Krusell_Smith_EGM.m:133-200); k_opt k x K x S column-major. */
+/* One sweep over the (s_i, K_i) pairs reading the next-period policy from `src` and writing
+ * each pair's column of `dst`: src == dst is the script's Gauss-Seidel order
+ * (Krusell_Smith_EGM.m:199 overwrites k_opt in place); src = a copy of the sweep's input is the
+ * Jacobi variant (F1, not the reference's result). */
+static int ks_egm_sweep2(const orc_ks_params* p, int64_t nk, int64_t nK, const double* k_grid,
+                         const orc_ks_egm_pair* pairs, const double* P, const double* src,
+                         double* dst);
 int orc_ks_egm_sweep(const orc_ks_params* p, int64_t nk, int64_t nK, const double* k_grid,
                      const orc_ks_egm_pair* pairs, const double* P, double* k_opt) {
+    return ks_egm_sweep2(p, nk, nK, k_grid, pairs, P, k_opt, k_opt);
+}
+static int ks_egm_sweep2(const orc_ks_params* p, int64_t nk, int64_t nK, const double* k_grid,
+                         const orc_ks_egm_pair* pairs, const double* P, const double* src,
+                         double* k_opt) {
     double* d4 = (double*)malloc(sizeof(double) * 4 * nk);
     double* kc = (double*)malloc(sizeof(double) * nk);
     int64_t* ord = (int64_t*)malloc(sizeof(int64_t) * nk);
@@ -695,7 +707,7 @@ int orc_ks_egm_sweep(const orc_ks_params* p, int64_t nk, int64_t nK, const doubl
             const orc_ks_egm_pair* q = pairs + s_i * nK + K_i;
             const double* col[4];
             for (int s_j = 0; s_j < 4; ++s_j) {
-                col[s_j] = k_opt + ((int64_t)s_j * nK + q->kd[s_j]) * nk;
+                col[s_j] = src + ((int64_t)s_j * nK + q->kd[s_j]) * nk;
                 orc_pchip_slopes(nk, k_grid, col[s_j], d4 + s_j * nk);
             }
             for (int64_t t = 0; t < nk; ++t) {
@@ -763,6 +775,37 @@ int orc_ks_egm_solve(const orc_ks_params* p, int64_t nk, int64_t nK, const doubl
     for (it = 1; it <= max_iter; ++it) {
         memcpy(old, k_opt, sizeof(double) * nk * nK * 4);
         rc = orc_ks_egm_sweep(p, nk, nK, k_grid, pairs, P, k_opt);
+        if (rc) break;
+        dmax = NAN;
+        for (int64_t n = 0; n < nk * nK * 4; ++n) {
+            double d = fabs(k_opt[n] - old[n]);
+            if (d == d && !(dmax >= d)) dmax = d;
+        }
+        if (dmax < tol) break;
+    }
+    if (it > max_iter) it = max_iter;
+    *iters = it;
+    *diff = dmax;
+    free(pairs);
+    free(old);
+    return rc;
+}
+
+/* F1: the Jacobi variant of the KS EGM iteration (every pair of a sweep reads the previous
+ * sweep's k_opt) — NOT the reference's result (the script is Gauss-Seidel, :199); same stop
+ * rule (:204-207). */
+int orc_ks_egm_solve_jacobi(const orc_ks_params* p, int64_t nk, int64_t nK, const double* k_grid,
+                            const double* K_grid, const double* B, const double* P, double tol,
+                            int64_t max_iter, double* k_opt, int64_t* iters, double* diff) {
+    orc_ks_egm_pair* pairs = (orc_ks_egm_pair*)malloc(sizeof(orc_ks_egm_pair) * 4 * nK);
+    double* old = (double*)malloc(sizeof(double) * nk * nK * 4);
+    orc_ks_egm_pairs(p, nK, K_grid, B, pairs);
+    int rc = 0;
+    int64_t it;
+    double dmax = NAN;
+    for (it = 1; it <= max_iter; ++it) {
+        memcpy(old, k_opt, sizeof(double) * nk * nK * 4);
+        rc = ks_egm_sweep2(p, nk, nK, k_grid, pairs, P, old, k_opt);
         if (rc) break;
         dmax = NAN;
         for (int64_t n = 0; n < nk * nK * 4; ++n) {

@@ -128,6 +128,9 @@ int orc_ks_egm_sweep(const orc_ks_params* p, int64_t nk, int64_t nK, const doubl
 int orc_ks_egm_solve(const orc_ks_params* p, int64_t nk, int64_t nK, const double* k_grid,
                      const double* K_grid, const double* B, const double* P, double tol,
                      int64_t max_iter, double* k_opt, int64_t* iters, double* diff);
+int orc_ks_egm_solve_jacobi(const orc_ks_params* p, int64_t nk, int64_t nK, const double* k_grid,
+                     const double* K_grid, const double* B, const double* P, double tol,
+                     int64_t max_iter, double* k_opt, int64_t* iters, double* diff);
 
 #ifdef __cplusplus
 }

@@ -28,6 +28,7 @@ def lib():
                      "orc_egm_step", "orc_egm_solve", "orc_labor_egm_step", "orc_labor_egm_solve",
                      "orc_sim_capital", "orc_dist_update_ongrid", "orc_dist_update_lottery",
                      "orc_ks_policy_improve", "orc_ks_howard", "orc_ks_egm_solve", "orc_num_threads",
+                     "orc_ks_egm_solve_jacobi",
                      "orc_dist_stationary"):
             getattr(L, name).restype = C.c_int
         L.orc_ks_bellman.restype = _d
@@ -266,14 +267,14 @@ def ks_vfi_solve(p, k_grid, K_grid, V, k_opt, B, P, howard=50, tol=1e-6, max_vfi
 
 
 # ---------------------------------------------------------------- A8
-def ks_egm_solve(p, k_grid, K_grid, B, P, k_opt, tol=1e-6, max_iter=10000):
+def ks_egm_solve(p, k_grid, K_grid, B, P, k_opt, tol=1e-6, max_iter=10000, jacobi=False):
     """Krusell_Smith_EGM.m:130-209 (C restatement).  P is MATLAB's 4x4 (row s_i)."""
     k_grid, K_grid, B = map(f64, (k_grid, K_grid, B))
     Pr = np.ascontiguousarray(P, dtype=np.float64)
     ko = np.array(k_opt, dtype=np.float64, order="F", copy=True)
     nk, nK, _ = ko.shape
     it, diff = C.c_int64(), C.c_double()
-    rc = lib().orc_ks_egm_solve(C.byref(p), _i64(nk), _i64(nK), _p(k_grid), _p(K_grid), _p(B),
+    rc = (lib().orc_ks_egm_solve_jacobi if jacobi else lib().orc_ks_egm_solve)(C.byref(p), _i64(nk), _i64(nK), _p(k_grid), _p(K_grid), _p(B),
                                 _p(Pr), _d(tol), _i64(max_iter), ko.ctypes.data_as(_P),
                                 C.byref(it), C.byref(diff))
     if rc:

@@ -843,17 +843,19 @@ def _pchip_slopes_n(x, y):
     return pchip_slopes(x, y)
 
 
-def ks_egm_sweep(p, k_grid, K_grid, B, P, k_opt, pairs=None):
+def ks_egm_sweep(p, k_grid, K_grid, B, P, k_opt, pairs=None, src=None):
     """One Gauss-Seidel sweep of Krusell_Smith_EGM.m:133-200: k_opt(:,K_i,s_i) is overwritten
     as soon as it is computed and read by later (s, K) pairs.  k_opt is [k, K, s] (modified in
-    place and returned)."""
+    place and returned).  src (F1, not the reference): read the next-period policy from this
+    array instead — src = a copy of the sweep's input gives the Jacobi variant."""
     nk, nK, _ = k_opt.shape
+    src = k_opt if src is None else src
     pairs = pairs or ks_egm_pairs(p, K_grid, B)
     k_min, k_max, beta = p["k_min"], p["k_max"], p["beta"]
     for s_i in range(4):
         for K_i in range(nK):
             q = pairs[s_i * nK + K_i]
-            cols = [k_opt[:, q["kd"][s_j], s_j].copy() for s_j in range(4)]
+            cols = [src[:, q["kd"][s_j], s_j].copy() for s_j in range(4)]
             slopes = [pchip_slopes(k_grid, c) for c in cols]
             kc = np.empty(nk)
             for kp_i in range(nk):
@@ -888,15 +890,16 @@ def ks_egm_sweep(p, k_grid, K_grid, B, P, k_opt, pairs=None):
     return k_opt
 
 
-def ks_egm_solve(p, k_grid, K_grid, B, P, k_opt, tol=1e-6, max_iter=10000):
-    """Krusell_Smith_EGM.m:130-209 for one B: sweeps until max|Δk_opt| < tol."""
+def ks_egm_solve(p, k_grid, K_grid, B, P, k_opt, tol=1e-6, max_iter=10000, jacobi=False):
+    """Krusell_Smith_EGM.m:130-209 for one B: sweeps until max|Δk_opt| < tol (jacobi=True:
+    the F1 Jacobi variant, every pair reads the previous sweep's k_opt — not the reference)."""
     k_opt = np.array(k_opt, dtype=np.float64, copy=True)
     pairs = ks_egm_pairs(p, K_grid, B)
     diff = float("nan")
     it = 0
     for it in range(1, max_iter + 1):
         old = k_opt.copy()
-        ks_egm_sweep(p, k_grid, K_grid, B, P, k_opt, pairs)
+        ks_egm_sweep(p, k_grid, K_grid, B, P, k_opt, pairs, src=old if jacobi else None)
         dd = np.abs(k_opt - old)
         diff = float(np.nanmax(dd)) if not np.all(np.isnan(dd)) else float("nan")
         if diff < tol:

@@ -64,3 +64,29 @@ def test_bad_inputs(pkg, gpu, golden):
         pkg.ks_egm_solve(g["k_opt0"], g["k_grid"][::-1].copy(), g["K_grid"], g["B"], g["P"], prm)
     with pytest.raises(pkg.AiyError):
         pkg.ks_egm_solve(g["k_opt0"], g["k_grid"], -g["K_grid"], g["B"], g["P"], prm)
+
+
+@pytest.mark.parametrize("B,nK,nk,max_iter", [(None, 4, 100, 10000),
+                                              ((0.1, 0.97, 0.08, 0.975), 4, 100, 40),
+                                              ((0.05, 0.985, 0.03, 0.99), 16, 300, 25)])
+def test_jacobi_variant_matches_jacobi_restatement(pkg, gpu, golden, B, nK, nk, max_iter):
+    """F1, flagged non-parity: the Jacobi KS EGM (one workgroup per (s, K) pair, all pairs of a
+    sweep in one launch) equals the C Jacobi restatement bit for bit — iteration count, policy,
+    last diff — at the reference size to tol (1085 sweeps vs Gauss-Seidel's 994) and on other
+    ALMs/sizes; its fixed point agrees with the reference's Gauss-Seidel one within tol."""
+    from oracle import np_oracle as no
+    g, prm = _setup(golden)
+    if B is None:
+        kg, Kg, P, k0, Bv = g["k_grid"], g["K_grid"], g["P"], g["k_opt0"], g["B"]
+    else:
+        _, kg, Kg, P, _, _ = no.ks_setup(k_size=nk, K_size=nK)
+        Bv = np.array(B)
+        k0 = 0.9 * np.repeat(np.repeat(kg[:, None, None], nK, 1), 4, 2)
+    R = pkg.ks_egm_solve(k0, kg, Kg, Bv, P, prm, tol=1e-6, max_iter=max_iter, jacobi=True)
+    Ro = corc.ks_egm_solve(_cparams(prm), kg, Kg, Bv, P, k0, tol=1e-6, max_iter=max_iter,
+                           jacobi=True)
+    assert R["iters"] == Ro["iters"]
+    assert np.array_equal(R["k_opt"], Ro["k_opt"])
+    assert R["diff"] == Ro["diff"]
+    if B is None:
+        assert R["iters"] == 1085 and np.max(np.abs(R["k_opt"] - g["k_opt_final"])) < 1e-4

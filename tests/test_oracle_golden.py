@@ -137,3 +137,25 @@ def test_ks_egm_bitwise(golden):
     # properties of the converged policy: inside [k_min, k_max], nondecreasing in k
     assert (rf["k_opt"] >= float(g["k_min"])).all() and (rf["k_opt"] <= float(g["k_max"])).all()
     assert (np.diff(rf["k_opt"], axis=0) >= 0).all()
+
+
+def test_ks_egm_jacobi_variant_restatements_agree(golden):
+    """F1 (not the reference's result): the Jacobi KS EGM sweep — every (s, K) pair reads the
+    previous sweep's k_opt instead of Krusell_Smith_EGM.m:199's in-place Gauss-Seidel update —
+    restated in C and numpy, bit-identical to each other; it differs from the Gauss-Seidel
+    iterate after one sweep but converges to the same fixed point within tolerance."""
+    from oracle import np_oracle as no
+    g = golden("ks_egm_defaults")
+    p = _ks_cparams(g)
+    args = (p, g["k_grid"], g["K_grid"], g["B"], g["P"], g["k_opt0"])
+    pn, *_ = no.ks_setup()
+    for m in (1, 2):
+        rc = corc.ks_egm_solve(*args, max_iter=m, jacobi=True)
+        rn = no.ks_egm_solve(pn, g["k_grid"], g["K_grid"], g["B"], g["P"], g["k_opt0"],
+                             max_iter=m, jacobi=True)
+        assert np.array_equal(rc["k_opt"], rn["k_opt"]) and rc["diff"] == rn["diff"]
+    assert not np.array_equal(corc.ks_egm_solve(*args, max_iter=1, jacobi=True)["k_opt"],
+                              g["k_opt1"])
+    rj = corc.ks_egm_solve(*args, tol=1e-6, max_iter=10000, jacobi=True)
+    assert rj["diff"] < 1e-6
+    assert np.max(np.abs(rj["k_opt"] - g["k_opt_final"])) < 1e-3
