@@ -67,6 +67,11 @@ def test_ks_egm_shape_and_usage(cal):
     with pytest.raises(mexstub.MexError) as e:
         mexstub.call("ks_egm_solve_mex", 1, np.zeros((10, 4, 4)))
     assert e.value.id == "aiy:usage"
+    with pytest.raises(mexstub.MexError) as e:
+        mexstub.call("ks_egm_solve_mex", 1, np.zeros((11, 4, 4)), np.linspace(0, 1, 11),
+                     np.linspace(30, 50, 4), np.array([0, 1, 0, 1.0]), np.eye(4), np.zeros(13),
+                     1e-6, 10.0, 2.0)
+    assert e.value.id == "aiy:type"
 
 
 def test_ks_panel_gateways_validate(cal):

@@ -76,6 +76,20 @@ def test_ks_egm_gateway(pkg, gpu, golden):
     assert float(diff[0, 0]) == float(g["diff3"])
 
 
+def test_ks_egm_gateway_jacobi(pkg, gpu, golden):
+    """ks_egm_solve_mex(..., jacobi=1): the F1 variant (flagged non-parity) through the gateway
+    equals the library's Jacobi solve bit for bit."""
+    g = golden("ks_egm_defaults")
+    prm = pkg.ks_params()
+    ko, it, diff = mexstub.call("ks_egm_solve_mex", 3, g["k_opt0"], g["k_grid"], g["K_grid"],
+                                g["B"], g["P"], prm, 1e-6, 40.0, 1.0)
+    R = pkg.ks_egm_solve(g["k_opt0"], g["k_grid"], g["K_grid"], g["B"], g["P"], prm, tol=1e-6,
+                         max_iter=40, jacobi=True)
+    assert int(it[0, 0]) == R["iters"] == 40
+    assert np.array_equal(ko.reshape(R["k_opt"].shape, order="F"), R["k_opt"])
+    assert float(diff[0, 0]) == R["diff"]
+
+
 def test_ks_panel_gateways(pkg, gpu, golden):
     """ks_shocks_mex / ks_simulate_capital_mex (Krusell_Smith_VFI.m:57-94, :206-248) reproduce
     the committed panel fixture."""
