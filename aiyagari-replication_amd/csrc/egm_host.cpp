@@ -14,6 +14,11 @@
 
 namespace aiy {
 
+static int fail_nonmonotone() {
+    return fail(AIY_BAD_ARG, "endogenous grid a_hat is not increasing: interp1 in the "
+                             "reference would sort it or fail (Aiyagari_EGM.m:95)");
+}
+
 static int ensure_egm(aiy_ws* ws) {
     size_t n = (size_t)ws->N * ws->Na;
     if (!ws->g0) AIY_HIP(hipMalloc((void**)&ws->g0, n * sizeof(double)));
@@ -26,13 +31,10 @@ static int ensure_egm(aiy_ws* ws) {
     return AIY_OK;
 }
 
-int egm_step_dev(aiy_ws* ws, const double* c, const double* a, const double* s, const double* P,
-                 double r, double w, double beta, double sigma, double amin, bool labor,
-                 double phi, double theta, double* cout, double* pk, double* pl, double* diff_out,
-                 hipStream_t st) {
-    if (!ws || !c || !a || !s || !P || !cout || !pk) return fail(AIY_BAD_ARG, "NULL argument");
-    if (labor && !(phi == phi && theta == theta)) return fail(AIY_NON_FINITE, "phi/theta");
-    AIY_TRY(ensure_egm(ws));
+static EgmArgs egm_args(aiy_ws* ws, const double* c, const double* a, const double* s,
+                        const double* P, double r, double w, double beta, double sigma,
+                        double amin, bool labor, double phi, double theta, double* cout,
+                        double* pk, double* pl) {
     EgmArgs A{};
     A.N = (int)ws->N;
     A.Na = (int)ws->Na;
@@ -44,8 +46,18 @@ int egm_step_dev(aiy_ws* ws, const double* c, const double* a, const double* s, 
     A.ahat = ws->g0; A.cnext = ws->g1; A.cout = cout; A.pk = pk; A.pl = pl;
     A.diff = ws->diff;
     A.flags = (unsigned*)ws->gi;
-    AIY_HIP(hipMemsetAsync(ws->diff, 0, 2 * kDiffSlots * sizeof(unsigned long long), st));
-    AIY_HIP(hipMemsetAsync(ws->gi, 0, sizeof(int), st));
+    return A;
+}
+
+int egm_step_dev(aiy_ws* ws, const double* c, const double* a, const double* s, const double* P,
+                 double r, double w, double beta, double sigma, double amin, bool labor,
+                 double phi, double theta, double* cout, double* pk, double* pl, double* diff_out,
+                 hipStream_t st) {
+    if (!ws || !c || !a || !s || !P || !cout || !pk) return fail(AIY_BAD_ARG, "NULL argument");
+    if (labor && !(phi == phi && theta == theta)) return fail(AIY_NON_FINITE, "phi/theta");
+    AIY_TRY(ensure_egm(ws));
+    EgmArgs A = egm_args(ws, c, a, s, P, r, w, beta, sigma, amin, labor, phi, theta, cout, pk, pl);
+    // the RHS kernel clears the diff slots and the flag word itself (no memset launches)
     AIY_TRY(ws_timing_begin(ws, st));
     AIY_TRY(launch_egm_step(A, st));
     AIY_TRY(ws_timing_end(ws, st));
@@ -61,9 +73,75 @@ static int read_egm(aiy_ws* ws, hipStream_t st, double* d) {
     AIY_HIP(hipMemcpyAsync(h + 2 * kDiffSlots, ws->gi, sizeof(int), hipMemcpyDeviceToHost, st));
     AIY_HIP(hipStreamSynchronize(st));
     *d = fold_slots_host(h);
-    if ((unsigned)h[2 * kDiffSlots] & 1u)
-        return fail(AIY_BAD_ARG, "endogenous grid a_hat is not increasing: interp1 in the "
-                                 "reference would sort it or fail (Aiyagari_EGM.m:95)");
+    if ((unsigned)h[2 * kDiffSlots] & 1u) return fail_nonmonotone();
+    return AIY_OK;
+}
+
+// The solve loop (Aiyagari_EGM.m:74-108, labour :67-105) with speculative batches, as the VFI
+// solve (capi.cpp, bell_solve_spec): steps are deterministic, so m steps are enqueued between
+// reads — step g reads ring slot (g−1) mod R and writes slot g mod R, its dist lands in its
+// own slot set and its flag word — and one D2H read per batch finds the first step whose dist
+// is not above tol.  The ring keeps that step's policy_c; its policy_k (and policy_l) were
+// overwritten by later speculative steps, so the stopping step is re-run from its input
+// (identical values).  Iteration count, dist and outputs equal the one-read-per-step loop's.
+static int egm_solve_spec(aiy_ws* ws, const EgmArgs& A0, double* c0, double tol,
+                          int64_t max_iter, double** cur_out, double* dist, int64_t* iters,
+                          hipStream_t st) {
+    const int M = ws->spec_max, R = M + 1;
+    const size_t n = (size_t)ws->N * ws->Na, nb = n * sizeof(double);
+    const int SW = 2 * kDiffSlots + 2;  // per step: {max bits, any} slots, then the flag word
+    if (ws->egm_spec_n != n || ws->egm_spec_m != M) {
+        ws->free_egm_spec();
+        AIY_HIP(hipMalloc((void**)&ws->egm_ring, (size_t)R * nb));
+        AIY_HIP(hipMalloc((void**)&ws->egm_slots, (size_t)M * SW * sizeof(unsigned long long)));
+        AIY_HIP(hipHostMalloc((void**)&ws->egm_hslots, (size_t)M * SW * sizeof(unsigned long long)));
+        ws->egm_spec_n = n;
+        ws->egm_spec_m = M;
+    }
+    auto slot = [&](int64_t g) { return ws->egm_ring + (size_t)(g % R) * n; };
+    AIY_HIP(hipMemcpyAsync(slot(0), c0, nb, hipMemcpyDeviceToDevice, st));
+    auto step = [&](int64_t g, int t) {
+        EgmArgs A = A0;
+        A.c = slot(g - 1);
+        A.cout = slot(g);
+        A.diff = ws->egm_slots + (size_t)t * SW;
+        A.flags = (unsigned*)(ws->egm_slots + (size_t)t * SW + 2 * kDiffSlots);
+        return launch_egm_step(A, st);
+    };
+    int64_t done = 0, stop = 0, last_enq = 0;
+    double d_prev = NAN, d_last = NAN, d_stop = 1.0;
+    while (!stop && done < max_iter) {
+        int64_t m = M;
+        if (d_last == d_last && d_prev == d_prev && d_last < d_prev && d_last > 0) {
+            const double need = std::ceil(std::log(tol / d_last) / std::log(d_last / d_prev));
+            if (need >= 1 && need < (double)m) m = (int64_t)need;
+        }
+        m = std::min<int64_t>(std::max<int64_t>(m, 1), max_iter - done);
+        for (int64_t t = 0; t < m; ++t) AIY_TRY(step(done + 1 + t, (int)t));
+        last_enq = done + m;
+        AIY_HIP(hipMemcpyAsync(ws->egm_hslots, ws->egm_slots,
+                               (size_t)m * SW * sizeof(unsigned long long),
+                               hipMemcpyDeviceToHost, st));
+        AIY_HIP(hipStreamSynchronize(st));
+        for (int64_t t = 0; t < m; ++t) {
+            const unsigned long long* h = ws->egm_hslots + (size_t)t * SW;
+            if ((unsigned)h[2 * kDiffSlots] & 1u) return fail_nonmonotone();
+            const double d = fold_slots_host(h);
+            d_prev = d_last;
+            d_last = d;
+            d_stop = d;
+            if (!(d > tol)) {  // Aiyagari_EGM.m:74 `while dist > tol`
+                stop = done + 1 + t;
+                break;
+            }
+        }
+        if (!stop) done += m;
+    }
+    const int64_t g = stop ? stop : done;
+    if (g > 0 && g != last_enq) AIY_TRY(step(g, 0));  // policy_k/l of the stopping step
+    *cur_out = g > 0 ? slot(g) : slot(0);
+    *dist = d_stop;
+    *iters = g;
     return AIY_OK;
 }
 
@@ -96,6 +174,11 @@ static int egm_host(double* pc, const double* a, const double* s, const double* 
         AIY_TRY(read_egm(c->ws, c->st, &d));
         cur = nxt;
         it = 1;
+    } else if (c->ws->spec_max > 1 && max_iter > 0) {
+        AIY_TRY(ensure_egm(c->ws));
+        const EgmArgs A = egm_args(c->ws, cur, da, ds, dP, r, w, beta, sigma, amin, labor, phi,
+                                   theta, nxt, dpk, labor ? dpl : nullptr);
+        AIY_TRY(egm_solve_spec(c->ws, A, cur, tol, max_iter, &cur, &d, &it, c->st));
     } else {
         while (d > tol && it < max_iter) {  // Aiyagari_EGM.m:74
             ++it;

@@ -3,15 +3,14 @@
 //   A5: Aiyagari_Endogenous_Labor_EGM.m:68-104 (GE copy :174-211)
 // Arrays are [N][Na] (== MATLAB's Na x N policy_c, column j = productivity state).
 //
-// Kernel 1 (one thread per asset node a, all N states): u'(c_m) once per (m, a), then for
-//   every j the Euler right-hand side Σ_m ((β(1+r))·P(j,m))·c_m^-σ in m order (:80-85),
-//   c̃ = RHS^(-1/σ) (:88) and the endogenous grid â = ((c̃ + a) − w s_j)/(1+r) (:92) — with
-//   the labour FOC l = ((w s_j) c̃^-σ / φ)^(1/θ) (:86) and â = ((c̃ + a) − (w s_j) l)/(1+r) (:87)
-//   in A5.
-// Kernel 2 (one thread per (j, a)): interp1(â_j, y, a_grid(a), 'linear', 'extrap') by binary
-//   search on the monotone â_j (y = a_grid in A4, c̃_j in A5), the borrowing clamp, the
-//   recovered policies, and max|c_next − c| ignoring NaN (:106) via atomicMax on IEEE bits.
-//   It also flags a non-increasing â_j (MATLAB's interp1 would sort or error there).
+// Kernel 1 (one thread per (j, a)): u'(c_m) once per (m, a), the Euler right-hand side
+//   Σ_m ((β(1+r))·P(j,m))·c_m^-σ in m order (:80-85), c̃ = RHS^(-1/σ) (:88) and the endogenous
+//   grid â = ((c̃ + a) − w s_j)/(1+r) (:92) — with the labour FOC l = ((w s_j) c̃^-σ / φ)^(1/θ)
+//   (:86) and â = ((c̃ + a) − (w s_j) l)/(1+r) (:87) in A5.
+// Kernel 2 (one thread per (j, a)): interp1(â_j, y, a_grid(a), 'linear', 'extrap') on the
+//   monotone â_j (y = a_grid in A4, c̃_j in A5), the borrowing clamp, the recovered policies,
+//   and max|c_next − c| ignoring NaN (:106) via atomicMax on IEEE bits.  It also flags a
+//   non-increasing â_j (MATLAB's interp1 would sort or error there).
 // HBM-bound: 24 B per state per iteration (c in, c_next out, policy_k out), +8 B with labour.
 #include "aiy_common.hpp"
 #include "egm.hpp"
@@ -28,78 +27,154 @@ __device__ __forceinline__ double labor_dev(double c, double ws, double sigma, i
     return (1.0 / theta == 1.0) ? x : aiy_pow(x, 1.0 / theta);
 }
 
-template <int NMAX>
-__global__ void egm_rhs_kernel(EgmArgs A) {
-    int a_i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (a_i >= A.Na) return;
+// Kernel 1: one workgroup per 64 asset nodes, one wave per productivity state.  Phase 1: wave m
+// evaluates u'(c_m) for its 64 nodes into LDS (once per (m, a), as the script's vectorised
+// u_prime_c(policy_c) does).  Phase 2: wave j forms the Euler sum over m in m order from LDS,
+// then one non-integer power and the endogenous grid — one pow per thread instead of N in a
+// row, and N times as many waves in flight.  The first workgroup also clears this step's diff
+// slots and flags (the interp kernel of the same step accumulates into them).
+__global__ __launch_bounds__(1024) void egm_rhs_kernel(EgmArgs A) {
+    __shared__ double s_up[16][64];
+    const int lane = threadIdx.x & 63, m = threadIdx.x >> 6;  // blockDim = 64·N
     const int N = A.N, Na = A.Na;
-    double up[NMAX];
-#pragma unroll
-    for (int m = 0; m < NMAX; ++m)
-        if (m < N) up[m] = uprime_dev(A.c[(size_t)m * Na + a_i], A.sigma, A.ns);
-    const double coef0 = A.beta * (1 + A.r);
-    const double ag = A.a[a_i];
-    for (int j = 0; j < N; ++j) {
-        double acc = 0.0;
-#pragma unroll
-        for (int m = 0; m < NMAX; ++m)
-            if (m < N) acc = acc + (coef0 * A.P[j * N + m]) * up[m];
-        double cn = aiy_pow(acc, -1.0 / A.sigma);  // :88
-        double ws = A.w * A.s[j];
-        double ah;
-        if (A.labor) {
-            double ls = labor_dev(cn, ws, A.sigma, A.ns, A.phi, A.theta);
-            ah = ((cn + ag) - ws * ls) / (1 + A.r);
-        } else {
-            ah = ((cn + ag) - ws) / (1 + A.r);
-        }
-        A.ahat[(size_t)j * Na + a_i] = ah;
-        A.cnext[(size_t)j * Na + a_i] = cn;
+    const int a_i = blockIdx.x * 64 + lane;
+    const bool ok = a_i < Na;
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < 2 * kDiffSlots) A.diff[threadIdx.x] = 0ull;
+        if (threadIdx.x == 0) *A.flags = 0u;
     }
+    s_up[m][lane] = ok ? uprime_dev(A.c[(size_t)m * Na + a_i], A.sigma, A.ns) : 0.0;
+    __syncthreads();
+    if (!ok) return;
+    const int j = m;
+    const double coef0 = A.beta * (1 + A.r);
+    double acc = 0.0;
+    for (int q = 0; q < N; ++q) acc = acc + (coef0 * A.P[j * N + q]) * s_up[q][lane];
+    const double cn = aiy_pow(acc, -1.0 / A.sigma);  // :88
+    const double ws = A.w * A.s[j];
+    const double ag = A.a[a_i];
+    double ah;
+    if (A.labor) {
+        const double ls = labor_dev(cn, ws, A.sigma, A.ns, A.phi, A.theta);
+        ah = ((cn + ag) - ws * ls) / (1 + A.r);
+    } else {
+        ah = ((cn + ag) - ws) / (1 + A.r);
+    }
+    A.ahat[(size_t)j * Na + a_i] = ah;
+    A.cnext[(size_t)j * Na + a_i] = cn;
 }
 
-__global__ void egm_interp_kernel(EgmArgs A) {
-    int t = blockIdx.x * blockDim.x + threadIdx.x;
+// #{k in [lo, hi) : x[k] <= q} + lo for a per-lane query (binary search, global memory)
+__device__ __forceinline__ int count_le(const double* __restrict__ x, int lo, int hi, double q) {
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (x[mid] <= q) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// Kernel 2: one wave per (j, 64 consecutive asset nodes).  interp1's segment is
+// clamp(#{k : â_k <= a}, 1, Na−1) − 1 (seg_of_dev).  The wave's queries a_grid(a0..a0+63)
+// are increasing, so on an increasing â every lane's count lies between the counts of the
+// first and the last query.  Those two come from a 64-ary search (each round, 64 lanes load
+// 64 evenly spaced pivots and one ballot narrows the range 64-fold: 3 dependent rounds at
+// Na = 20,000 instead of 15); the â values between them (≤ 256) are staged in LDS in one round
+// trip and each lane finishes its count there.  A wider spread (or a non-increasing â, which
+// the flag turns into an error) falls back to a per-lane search over the narrowed range, so
+// the count — and everything after it — is the plain binary search's.
+__global__ __launch_bounds__(256) void egm_interp_kernel(EgmArgs A, int ntile) {
+    __shared__ double s_x[4][256];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int Na = A.Na;
+    const int wv = blockIdx.x * 4 + wave;
     bool ok = false;
     double d = 0.0;
-    if (t < A.N * A.Na) {
-        const int Na = A.Na;
-        int j = t / Na, a_i = t - j * Na;
+    if (wv < A.N * ntile) {  // wave-uniform
+        const int j = wv / ntile, tile = wv - j * ntile;
+        const int a0 = tile * 64, a_i = a0 + lane;
+        const int last = min(63, Na - 1 - a0);
+        const bool okl = lane <= last;
+        const size_t t = (size_t)j * Na + (okl ? a_i : a0);
         const double* __restrict__ x = A.ahat + (size_t)j * Na;
         const double* __restrict__ y = A.labor ? A.cnext + (size_t)j * Na : A.a;
-        double q = A.a[a_i];
-        int sgi = seg_of_dev(x, Na, q);
-        double tt = (q - x[sgi]) / (x[sgi + 1] - x[sgi]);
-        double g = y[sgi] + tt * (y[sgi + 1] - y[sgi]);
-        if (a_i > 0 && !(x[a_i - 1] < x[a_i])) atomicOr(A.flags, 1u);
-        double ws = A.w * A.s[j];
-        double cn;
-        if (A.labor) {
-            if (q < A.amin) g = A.amin;  // :91 (a no-op for a_grid >= amin)
-            cn = g;
-            double l = labor_dev(g, ws, A.sigma, A.ns, A.phi, A.theta);      // :95
-            double k = ((1 + A.r) * q + ws * l) - g;                           // :98
-            A.pk[t] = k < 0 ? 0.0 : k;                                         // :99
-            if (A.pl) A.pl[t] = l;
-        } else {
-            if (g < A.amin) g = A.amin;  // :98
-            A.pk[t] = g;
-            cn = ((1 + A.r) * q + ws) - g;  // :102
+        const double q = A.a[okl ? a_i : a0 + last];
+        const double q0 = readlane_d(q, 0), q1 = readlane_d(q, last);
+        int lo0 = 0, hi0 = Na, lo1 = 0, hi1 = Na;
+        while (lo0 < hi0 || lo1 < hi1) {  // wave-uniform bounds
+            const int st0 = max((hi0 - lo0 + 63) >> 6, 1), st1 = max((hi1 - lo1 + 63) >> 6, 1);
+            const int k0 = lo0 + (lane + 1) * st0 - 1, k1 = lo1 + (lane + 1) * st1 - 1;
+            const bool v0 = k0 < hi0, v1 = k1 < hi1;
+            const double x0 = v0 ? x[k0] : 0.0, x1 = v1 ? x[k1] : 0.0;
+            const int c0 = __popcll(__ballot(v0 && x0 <= q0));
+            const int c1 = __popcll(__ballot(v1 && x1 <= q1));
+            if (lo0 < hi0) {
+                const int nh = lo0 + (c0 + 1) * st0 - 1;
+                lo0 += c0 * st0;
+                hi0 = nh < hi0 ? nh : hi0;
+            }
+            if (lo1 < hi1) {
+                const int nh = lo1 + (c1 + 1) * st1 - 1;
+                lo1 += c1 * st1;
+                hi1 = nh < hi1 ? nh : hi1;
+            }
         }
-        A.cout[t] = cn;
-        d = fabs(cn - A.c[t]);
-        ok = (d == d);
+        // every lane's count is in [lo0, lo1] (increasing â and queries)
+        int cnt;
+        const int span = lo1 - lo0;
+        if (span >= 0 && span <= 256) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = lo0 + u * 64 + lane;
+                if (u * 64 + lane < span) s_x[wave][u * 64 + lane] = x[k];
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            int lo = 0, hi = span;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (s_x[wave][mid] <= q) lo = mid + 1;
+                else hi = mid;
+            }
+            cnt = lo0 + lo;
+        } else {
+            cnt = count_le(x, min(lo0, lo1), max(lo0, lo1), q);
+        }
+        int sgi = cnt - 1;
+        sgi = sgi < 0 ? 0 : sgi;
+        sgi = sgi > Na - 2 ? Na - 2 : sgi;
+        if (okl) {
+            const double tt = (q - x[sgi]) / (x[sgi + 1] - x[sgi]);
+            double g = y[sgi] + tt * (y[sgi + 1] - y[sgi]);
+            if (a_i > 0 && !(x[a_i - 1] < x[a_i])) atomicOr(A.flags, 1u);
+            const double ws = A.w * A.s[j];
+            double cn;
+            if (A.labor) {
+                if (q < A.amin) g = A.amin;  // :91 (a no-op for a_grid >= amin)
+                cn = g;
+                const double l = labor_dev(g, ws, A.sigma, A.ns, A.phi, A.theta);  // :95
+                const double k = ((1 + A.r) * q + ws * l) - g;                       // :98
+                A.pk[t] = k < 0 ? 0.0 : k;                                           // :99
+                if (A.pl) A.pl[t] = l;
+            } else {
+                if (g < A.amin) g = A.amin;  // :98
+                A.pk[t] = g;
+                cn = ((1 + A.r) * q + ws) - g;  // :102
+            }
+            A.cout[t] = cn;
+            d = fabs(cn - A.c[t]);
+            ok = (d == d);
+        }
     }
     block_max_to_slots(ok, d, A.diff);
 }
 
 int launch_egm_step(const EgmArgs& A, hipStream_t st) {
     if (A.N > 16) return fail(AIY_BAD_SHAPE, "EGM kernels support N <= 16 productivity states");
-    if (A.N <= 8) egm_rhs_kernel<8><<<(A.Na + 127) / 128, 128, 0, st>>>(A);
-    else egm_rhs_kernel<16><<<(A.Na + 127) / 128, 128, 0, st>>>(A);
+    const int ntile = (A.Na + 63) / 64;
+    egm_rhs_kernel<<<ntile, 64 * A.N, 0, st>>>(A);
     AIY_HIP(hipGetLastError());
-    int n = A.N * A.Na;
-    egm_interp_kernel<<<(n + 255) / 256, 256, 0, st>>>(A);
+    egm_interp_kernel<<<(A.N * ntile + 3) / 4, 256, 0, st>>>(A, ntile);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }

@@ -64,6 +64,19 @@ struct aiy_ws {
     double* spec_pol = nullptr;                 // [spec_max][3][N*Na] (k, c, l)
     unsigned long long* spec_diff = nullptr;    // device [2*spec_max]
     unsigned long long* spec_hdiff = nullptr;   // pinned host [2*spec_max]
+    // speculative EGM solve: ring of spec_max + 1 policy_c buffers, per-step diff slots + flag
+    size_t egm_spec_n = 0;
+    int egm_spec_m = 0;
+    double* egm_ring = nullptr;
+    unsigned long long* egm_slots = nullptr;    // device [spec_max][2*kDiffSlots + 2]
+    unsigned long long* egm_hslots = nullptr;   // pinned host, same shape
+    void free_egm_spec() {
+        if (egm_ring) (void)hipFree(egm_ring);
+        if (egm_slots) (void)hipFree(egm_slots);
+        if (egm_hslots) (void)hipHostFree(egm_hslots);
+        egm_ring = nullptr; egm_slots = nullptr; egm_hslots = nullptr;
+        egm_spec_n = 0; egm_spec_m = 0;
+    }
     // batched candidate rates (config 4, aiy_vfi_solve_batch_dev): per-candidate blocks of the
     // tree-screen scratch, sized for bC candidates
     int64_t bC = 0;
@@ -114,6 +127,7 @@ struct aiy_ws {
             if (p) (void)hipFree(p);
         free_spec();
         free_batch();
+        free_egm_spec();
         if (hdiff) (void)hipHostFree(hdiff);
         EV = nullptr; T = nullptr; T32 = nullptr; Dm = nullptr; Dm8 = nullptr; Dt = nullptr; Dm512 = nullptr; touched = nullptr; best0 = nullptr; dis = nullptr; kf = nullptr; kf_cap = 0;
         kf_ok = false;
