@@ -82,6 +82,44 @@ __device__ __forceinline__ double bell_val(double c, double ev, double sigma, do
     else return u + ev;                        // Aiyagari_VFI.m:79
 }
 
+// Screen values t[m] = dd[m]·max(cx[m], 0)^NP of M independent (candidate or bound, state)
+// pairs, computed stage by stage with scheduling barriers between the stages so that the M
+// chains interleave.  On gfx950 a dependent fp64 VALU op waits ~16-18 cycles for its operand
+// while independent ones issue every ~4-6 (tools/micro/fp64_latency.hip): written per pair the
+// compiler emits each pair's 5-deep chain back to back and the wave stalls on every op.  The
+// operation sequence per pair is aiy_ipow's, so every t is the unstaged expression's bit for
+// bit and the screen's rounding analysis is unchanged.
+#define AIY_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
+template <int NP, int M>
+__device__ __forceinline__ void screen_t(double (&t)[M], const double (&cx)[M],
+                                         const double (&dd)[M]) {
+    double c[M], p[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) c[m] = fmax(cx[m], 0.0);
+    AIY_SCHED_BARRIER();
+#pragma unroll
+    for (int m = 0; m < M; ++m) p[m] = c[m];
+    constexpr int top = 31 - __builtin_clz((unsigned)NP);
+#pragma unroll
+    for (int b = top - 1; b >= 0; --b) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) p[m] = p[m] * p[m];
+        AIY_SCHED_BARRIER();
+        if ((NP >> b) & 1) {
+#pragma unroll
+            for (int m = 0; m < M; ++m) p[m] = p[m] * c[m];
+            AIY_SCHED_BARRIER();
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) t[m] = dd[m] * p[m];
+}
+// pairs per stage group: 8 candidates × the sub-states of a lane, at most ~16 chains
+template <int RL>
+struct StageGroup {
+    static constexpr int G = RL <= 2 ? 8 : (RL <= 4 ? 4 : 2);
+};
+
 // (max value, first index) merge; NaN never enters (MATLAB max omits NaN)
 __device__ __forceinline__ bool lexi_take(double val, int q, double& best, int& idx) {
     if (val != val) return false;
@@ -865,24 +903,43 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
         // eight block bounds at once (independent dependency chains, so their latencies
         // overlap): lanes l0 + stride*u of (dv, av) hold (Dmax, a at the block start); bit u
         // of the result is set when some sub-state passes bound u (u < cnt)
+        constexpr int RL = R * LB, G = StageGroup<RL>::G;
         auto mask8 = [&](double dv, double av, int l0, int stride, int cnt)
                          __attribute__((always_inline)) {
-            double tmax[8];
+            double dmax[8], a0[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const int ln = min(l0 + stride * u, 63);
-                const double dmax = readlane_d(dv, ln), a0 = readlane_d(av, ln);
-                double tm = -__builtin_inf();
+                dmax[u] = readlane_d(dv, ln);
+                a0[u] = readlane_d(av, ln);
+            }
+            bool pu[8];
 #pragma unroll
-                for (int r = 0; r < R; ++r)
+            for (int g0 = 0; g0 < 8; g0 += G) {
+                double cx[G * RL], dd[G * RL], t[G * RL];
 #pragma unroll
-                    for (int q = 0; q < LB; ++q)
-                        tm = fmax(tm, (dmax - B[r][q]) * aiy_ipow(fmax(coh[r][q] - a0, 0.0), NP));
-                tmax[u] = tm;
+                for (int gu = 0; gu < G; ++gu)
+#pragma unroll
+                    for (int r = 0; r < R; ++r)
+#pragma unroll
+                        for (int q = 0; q < LB; ++q) {
+                            const int m = (gu * R + r) * LB + q;
+                            cx[m] = coh[r][q] - a0[g0 + gu];
+                            dd[m] = dmax[g0 + gu] - B[r][q];
+                        }
+                AIY_SCHED_BARRIER();
+                screen_t<NP, G * RL>(t, cx, dd);
+#pragma unroll
+                for (int gu = 0; gu < G; ++gu) {
+                    bool pass = false;
+#pragma unroll
+                    for (int m = gu * RL; m < (gu + 1) * RL; ++m) pass = pass || t[m] >= kThr;
+                    pu[g0 + gu] = pass;
+                }
             }
             unsigned m = 0;
 #pragma unroll
-            for (int u = 0; u < 8; ++u) m |= (__any(tmax[u] >= kThr) ? 1u : 0u) << u;
+            for (int u = 0; u < 8; ++u) m |= (__any(pu[u]) ? 1u : 0u) << u;
             return m & ((1u << cnt) - 1u);
         };
         // candidates [k0, k1), k1 - k0 <= 8, of superblock sbase staged in LDS.  The exact
@@ -895,30 +952,44 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
 #pragma unroll
             for (int kk = 0; kk < 8; ++kk)  // broadcast reads, all in flight together
                 tk[kk] = s_cand[wave][k0 - sbase + kk];  // whole 64-block staged; kk >= k1 - k0 masked below
-            double tmax[8];
+            bool pk[8];
 #pragma unroll
-            for (int kk = 0; kk < 8; ++kk) {
-                double tm = -__builtin_inf();
+            for (int g0 = 0; g0 < 8; g0 += G) {
+                double cx[G * RL], dd[G * RL], t[G * RL];
 #pragma unroll
-                for (int r = 0; r < R; ++r)
+                for (int gk = 0; gk < G; ++gk)
 #pragma unroll
-                    for (int q = 0; q < LB; ++q) {
-                        const double c = fmax(coh[r][q] - tk[kk].x, 0.0);
-                        const double t = (tk[kk].y - B[r][q]) * aiy_ipow(c, NP);
-                        const int lin = (l0 + q) + Nl * (k0 + kk);
-                        tm = (lin == idx[r]) ? tm : fmax(tm, t);
-                    }
-                tmax[kk] = tm;
+                    for (int r = 0; r < R; ++r)
+#pragma unroll
+                        for (int q = 0; q < LB; ++q) {
+                            const int m = (gk * R + r) * LB + q;
+                            cx[m] = coh[r][q] - tk[g0 + gk].x;
+                            dd[m] = tk[g0 + gk].y - B[r][q];
+                        }
+                AIY_SCHED_BARRIER();
+                screen_t<NP, G * RL>(t, cx, dd);
+#pragma unroll
+                for (int gk = 0; gk < G; ++gk) {
+                    bool pass = false;
+#pragma unroll
+                    for (int r = 0; r < R; ++r)
+#pragma unroll
+                        for (int q = 0; q < LB; ++q) {
+                            const int lin = (l0 + q) + Nl * (k0 + g0 + gk);
+                            pass = pass || (t[(gk * R + r) * LB + q] >= kThr && lin != idx[r]);
+                        }
+                    pk[g0 + gk] = pass;
+                }
             }
             {  // one wave vote first: almost always no candidate passes
-                double tall = tmax[0];
+                bool pall = false;
 #pragma unroll
-                for (int kk = 1; kk < 8; ++kk) tall = fmax(tall, tmax[kk]);
-                if (!__any(tall >= kThr)) return;
+                for (int kk = 0; kk < 8; ++kk) pall = pall || pk[kk];
+                if (!__any(pall)) return;
             }
             unsigned vote = 0;
 #pragma unroll
-            for (int kk = 0; kk < 8; ++kk) vote |= (__any(tmax[kk] >= kThr) ? 1u : 0u) << kk;
+            for (int kk = 0; kk < 8; ++kk) vote |= (__any(pk[kk]) ? 1u : 0u) << kk;
             vote &= (1u << (k1 - k0)) - 1u;
             if (!vote) return;
             stamp(2);
