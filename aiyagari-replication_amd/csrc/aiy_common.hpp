@@ -48,6 +48,36 @@ __device__ __forceinline__ double readlane_d(double x, int l) {
     return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
 
+// DPP lane moves (no LDS round trip, unlike __shfl_xor's ds_bpermute): lanes whose source is
+// outside the pattern's row keep their own value.  Controls: quad_perm [1,0,3,2] = 0xB1 (lane
+// ^ 1), [2,3,0,1] = 0x4E (lane ^ 2), row_shl:4 = 0x104 (lane + 4 within a row of 16),
+// row_mirror = 0x140, row_half_mirror = 0x141, row_bcast:15 = 0x142, row_bcast:31 = 0x143.
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ unsigned dpp_u32(unsigned x) {
+    return (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, CTRL, ROWS, 0xf, false);
+}
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ unsigned long long dpp_u64(unsigned long long x) {
+    const unsigned lo = dpp_u32<CTRL, ROWS>((unsigned)x);
+    const unsigned hi = dpp_u32<CTRL, ROWS>((unsigned)(x >> 32));
+    return ((unsigned long long)hi << 32) | lo;
+}
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ double dpp_d(double x) {
+    return __builtin_bit_cast(double, dpp_u64<CTRL, ROWS>(__builtin_bit_cast(unsigned long long, x)));
+}
+// max over the wave of an unsigned 64-bit key, valid in lane 63 (DPP reduction ladder)
+__device__ __forceinline__ unsigned long long wave_max_u64_lane63(unsigned long long k) {
+    auto mx = [](unsigned long long a, unsigned long long b) { return a > b ? a : b; };
+    k = mx(k, dpp_u64<0xB1>(k));
+    k = mx(k, dpp_u64<0x4E>(k));
+    k = mx(k, dpp_u64<0x141>(k));
+    k = mx(k, dpp_u64<0x140>(k));
+    k = mx(k, dpp_u64<0x142, 0xa>(k));
+    k = mx(k, dpp_u64<0x143, 0xc>(k));
+    return k;
+}
+
 // first k in [0, n) with a[k] >= x  (== count of a[k] < x), a non-decreasing.
 __device__ __forceinline__ int lower_bound_dev(const double* __restrict__ a, int n, double x) {
     int lo = 0, hi = n;
@@ -89,9 +119,11 @@ __device__ __forceinline__ void block_max_to_slots(bool ok, double d,
     __shared__ int s_any[16];
     unsigned long long key = ok ? (unsigned long long)aiy_dbits(d) : 0ull;
     int any = __ballot(ok) != 0ull;
-    for (int off = 32; off > 0; off >>= 1) {
-        unsigned long long o = __shfl_xor(key, off);
-        key = o > key ? o : key;
+    key = wave_max_u64_lane63(key);
+    {
+        const unsigned lo = __builtin_amdgcn_readlane((int)(unsigned)key, 63);
+        const unsigned hi = __builtin_amdgcn_readlane((int)(unsigned)(key >> 32), 63);
+        key = ((unsigned long long)hi << 32) | lo;
     }
     const int wave = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
     if ((threadIdx.x & 63) == 0) {

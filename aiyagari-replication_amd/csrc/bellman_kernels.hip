@@ -771,7 +771,7 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
     }
     const int tile = item % ntile;
     const int i = item / ntile;
-    const int N = A.N, Na = A.Na, Nl = A.Nl;
+    const int N = A.N, Na = A.Na, Nl = LAB ? A.Nl : 1;  // (A1: one "labour level")
     const size_t nall = (size_t)N * Na;
     const double* __restrict__ a = A.a;
     const double* __restrict__ Drow = A.Dt + (size_t)i * Na;
@@ -781,6 +781,21 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
     __shared__ double2 s_cand[W][512];  // each wave's current superblock: (a_k, D_k)
     __shared__ double s_xb[W][64 * R];  // best exchange
     __shared__ int s_xi[W][64 * R];
+
+    // loads that do not depend on the start-up below, issued first so that their latency
+    // overlaps it: the level-0 bounds of the first 64 superblocks (first labour group) and v_old
+    double dm0_pre, a0_pre;
+    {
+        const bool oks = lane < A.nb512;
+        dm0_pre = oks ? A.Dm512[(size_t)i * A.nb512 + lane] : -__builtin_inf();
+        a0_pre = oks ? a[lane << 9] : 0.0;
+    }
+    double vo_pre[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int j = jbase + r * 64 + lane;
+        vo_pre[r] = (j < Na && wave == 0) ? A.v_old[(size_t)i * Na + j] : 0.0;
+    }
 
     double x[R], best[R];
     int idx[R];
@@ -886,8 +901,15 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
                 if (okq) kg = max(kg, A.kf[(l0 + q) * nall + t]);
             }
         }
-        for (int off = 32; off > 0; off >>= 1) kg = max(kg, __shfl_xor(kg, off));
-        kg = readfirst(kg);
+        if (A.r > -1.0) {
+            // coh is increasing in j when 1 + r > 0, so every feasible prefix kf is
+            // non-decreasing along the tile: the maximum sits in the last valid lane
+            const int jl = min(Na - 1, jbase + 64 * R - 1);  // the tile's last state
+            kg = readlane_i(kg, (jl - jbase) & 63);
+        } else {
+            for (int off = 32; off > 0; off >>= 1) kg = max(kg, __shfl_xor(kg, off));
+            kg = readfirst(kg);
+        }
         if (kg == 0) continue;
         if (l0 > 0) exchange();  // the previous group left per-wave bests
         auto set_B = [&]() __attribute__((always_inline)) {
@@ -1030,14 +1052,22 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
             dm8 = oku ? A.Dm8[(size_t)i * A.nb8 + sub] : -__builtin_inf();
             a8 = oku ? a[sub << 3] : 0.0;
         };
-        auto superblock = [&](int sb, int bsel, int bstep, double dm8, double a8)
-                              __attribute__((always_inline)) {
+        // one superblock, blocks b with b % bstep == bsel, in two halves.  prep: the bound tests
+        // of its 64-blocks and 8-blocks (v_readlane of the sub-block bounds, no memory) and the
+        // loads of the candidates of every passing 64-block into registers.  finish: those
+        // registers to LDS, then the fine screen of every passing 8-block.  The main loop runs
+        // prep of superblock n+1 before finish of superblock n, so the candidate loads of n+1
+        // are in flight while n is screened (a bar raised by n's exact path only makes n+1's
+        // bound tests, done against the older bar, pass more: never fewer candidates).
+        auto prep = [&](int sb, int bsel, int bstep, double dm8, double a8, double2 (&st)[8])
+                        __attribute__((always_inline)) -> unsigned long long {
             stamp(0);
             const int sbase = sb << 9;  // first candidate of the superblock
+            // 64-block maxima at lanes 8b (the only lanes read): lane ^ 1, lane ^ 2, lane + 4
             double dm64 = dm8;
-            dm64 = fmax(dm64, __shfl_xor(dm64, 1));
-            dm64 = fmax(dm64, __shfl_xor(dm64, 2));
-            dm64 = fmax(dm64, __shfl_xor(dm64, 4));
+            dm64 = fmax(dm64, dpp_d<0xB1>(dm64));
+            dm64 = fmax(dm64, dpp_d<0x4E>(dm64));
+            dm64 = fmax(dm64, dpp_d<0x104>(dm64));
             // blocks inside the feasible range and owned by this wave
             const int nblock = min(8, (kg - sbase + 63) >> 6);
             unsigned own = 0;
@@ -1051,16 +1081,21 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
                 if (A.hitcount || A.trace) nblk += nsub;
                 pass |= (unsigned long long)mask8(dm8, a8, 8 * b, 1, nsub) << (8 * b);
             }
-            if (!pass) {
-                stamp(1);
-                return;
-            }
 #pragma unroll
             for (int b = 0; b < 8; ++b)  // all loads issued before any is used
                 if ((pass >> (8 * b)) & 0xffull) {
                     const int k = min(sbase + (b << 6) + lane, Na - 1);
-                    s_cand[wave][(b << 6) + lane] = make_double2(a[k], Drow[k]);
+                    st[b] = make_double2(a[k], Drow[k]);
                 }
+            stamp(1);
+            return pass;
+        };
+        auto finish = [&](int sb, unsigned long long pass, const double2 (&st)[8])
+                          __attribute__((always_inline)) {
+            const int sbase = sb << 9;
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                if ((pass >> (8 * b)) & 0xffull) s_cand[wave][(b << 6) + lane] = st[b];
             __builtin_amdgcn_wave_barrier();  // a wave reads only its own slice
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             stamp(1);
@@ -1085,8 +1120,17 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
             const unsigned long long m = __ballot(hk >= 0);
             if (m) sfirst = min(readlane_i(hk, __builtin_ctzll(m)) >> 9, nsb - 1);
         }
-        // level-0 bounds of the first 64 superblocks, issued before the first superblock's
-        // work so that their latency overlaps it
+        double2 st_cur[8], st_prev[8];
+        if (sfirst >= 0) {  // (its bound would pass: it holds the bar's candidate)
+            ++nsup;
+            double d8, a8;
+            load8(sfirst, d8, a8);
+            const unsigned long long p = prep(sfirst, wave, W, d8, a8, st_cur);
+            if (p) finish(sfirst, p, st_cur);
+            exchange();
+            set_B();
+        }
+        // level-0 bounds of the first 64 superblocks
         double dm0, a0;
         auto load512 = [&](int g) __attribute__((always_inline)) {
             const int sbl = g + lane;
@@ -1094,20 +1138,30 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
             dm0 = oks ? A.Dm512[(size_t)i * A.nb512 + sbl] : -__builtin_inf();
             a0 = oks ? a[sbl << 9] : 0.0;
         };
-        load512(0);
-        if (sfirst >= 0) {  // (its bound would pass: it holds the bar's candidate)
-            ++nsup;
-            double d8, a8;
-            load8(sfirst, d8, a8);
-            superblock(sfirst, wave, W, d8, a8);
-            exchange();
-            set_B();
+        if (l0 == 0) {  // prefetched (lanes past nsb are masked by the bound counts below)
+            dm0 = dm0_pre;
+            a0 = a0_pre;
+        } else {
+            load512(0);
         }
-        for (int g = 0; g < nsb; g += 64) {
-            if (g > 0) load512(g);
-            const int ns = min(64, nsb - g);
-            for (int s8 = 0; s8 < ns; s8 += 8) {  // superblock bounds eight at a time
-                const int cnt = min(8, ns - s8);
+        // the passing superblocks in order: level-0 tests eight at a time, on demand
+        int g = 0, s8 = -8;
+        unsigned sm = 0;
+        auto next_sb = [&]() __attribute__((always_inline)) -> int {
+            for (;;) {
+                if (sm) {
+                    const int u = __builtin_ctz(sm);
+                    sm &= sm - 1;
+                    return g + s8 + u;
+                }
+                s8 += 8;
+                if (s8 >= min(64, nsb - g)) {
+                    g += 64;
+                    s8 = 0;
+                    if (g >= nsb) return -1;
+                    load512(g);
+                }
+                const int cnt = min(8, min(64, nsb - g) - s8);
                 unsigned own = 0;
                 for (int u = 0; u < cnt; ++u) {
                     const int sb = g + s8 + u;
@@ -1115,21 +1169,28 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
                 }
                 if (!own) continue;
                 nsup += __builtin_popcount(own);
-                unsigned sm = mask8(dm0, a0, s8, 1, cnt) & own;
-                if (!sm) continue;
-                // software pipeline: the next passing superblock's sub-block bounds load while
-                // this one's candidates are staged and screened
-                double pd, pa;
-                load8(g + s8 + __builtin_ctz(sm), pd, pa);
-                while (sm) {
-                    const int cur = g + s8 + __builtin_ctz(sm);
-                    sm &= sm - 1;
-                    const double d8 = pd, a8 = pa;
-                    if (sm) load8(g + s8 + __builtin_ctz(sm), pd, pa);
-                    superblock(cur, 0, 1, d8, a8);
-                }
+                sm = mask8(dm0, a0, s8, 1, cnt) & own;
             }
+        };
+        // software pipeline: load8 two superblocks ahead, the candidate loads one ahead
+        int cur = nsb > 0 ? next_sb() : -1;
+        double pd = 0.0, pa = 0.0;
+        if (cur >= 0) load8(cur, pd, pa);
+        unsigned long long pass_prev = 0;
+        int sb_prev = -1;
+        while (cur >= 0) {
+            const double d8 = pd, a8 = pa;
+            const int nxt = next_sb();
+            if (nxt >= 0) load8(nxt, pd, pa);
+            const unsigned long long pc = prep(cur, 0, 1, d8, a8, st_cur);
+            if (pass_prev) finish(sb_prev, pass_prev, st_prev);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) st_prev[b] = st_cur[b];
+            pass_prev = pc;
+            sb_prev = cur;
+            cur = nxt;
         }
+        if (pass_prev) finish(sb_prev, pass_prev, st_prev);
     }
 
     exchange();
@@ -1144,7 +1205,7 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
         const size_t t = (size_t)i * Na + jbase + r * 64 + lane;
         double b = best[r];
         int q = idx[r];
-        const double vo = A.v_old[t];
+        const double vo = vo_pre[r];
         if (!feas[r] && LAB) {
             b = A.keep_incoming ? A.v_new[t] : vo;
         } else {
