@@ -761,6 +761,8 @@ template <int NP, bool LAB, int R, int LB, int W>
 __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntile) {
     const int lane = threadIdx.x & 63;
     const int wave = readfirst(threadIdx.x >> 6);
+    const long long t_boot = A0.trace ? (long long)wall_clock64() : 0;  // (instrumentation)
+    const long long c_boot = A0.trace ? (long long)__builtin_amdgcn_s_memtime() : 0;
     int item = (A0.variant & 16) ? xcd_remap((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
     BellArgs A = A0;
     if (A0.C > 1) {  // batched candidates: blocks [c·N·ntile, (c+1)·N·ntile) are candidate c's
@@ -824,16 +826,36 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
                         return lexi_take(bell_val<NP, LAB>(coh - a[k], ev[k], A.sigma, dis),
                                          hl + Nl * k, best[r], idx[r]);
                     };
-                    for (int k = max(hk - 1, 0); k <= min(hk + 1, kf - 1); ++k) take(k);
-                    // Climb: when a neighbour of the hint beats it, the optimum has moved (early
-                    // sweeps; the sweep after a cold start moves it by thousands of candidates).
-                    // Doubling steps while the value improves, then halving steps around the
-                    // best point: for a unimodal objective this lands on the maximiser in
-                    // O(log distance) exact evaluations instead of the tree raising the bar
-                    // one passing candidate at a time.  Any candidate is a valid bar, so the
-                    // result does not depend on it (the tree below still proves the maximum).
+                    // Window: the hint and its wn neighbours on each side (wn = 1, 2, 4 or 8:
+                    // variant bits 7-8), all loads in flight together, then their exact values
+                    // (independent chains).  Indices are clamped into the feasible prefix; a
+                    // repeated candidate merges as a no-op.
+                    const int wn = 1 << ((A.variant >> 7) & 3);
+                    constexpr int WM = 8;
+                    double wa[2 * WM + 1], we[2 * WM + 1];
+#pragma unroll
+                    for (int d = -WM; d <= WM; ++d) {
+                        if (d < -wn || d > wn) continue;  // wave-uniform
+                        const int kc = min(max(hk + d, 0), kf - 1);
+                        wa[d + WM] = a[kc];
+                        we[d + WM] = ev[kc];
+                    }
+#pragma unroll
+                    for (int d = -WM; d <= WM; ++d) {
+                        if (d < -wn || d > wn) continue;
+                        const int kc = min(max(hk + d, 0), kf - 1);
+                        lexi_take(bell_val<NP, LAB>(coh - wa[d + WM], we[d + WM], A.sigma, dis),
+                                  hl + Nl * kc, best[r], idx[r]);
+                    }
+                    // Climb: when the best of the window sits on its edge, the optimum has moved
+                    // further (early sweeps; the sweep after a cold start moves it by thousands
+                    // of candidates).  Doubling steps while the value improves, then halving
+                    // steps around the best point: for a unimodal objective this lands on the
+                    // maximiser in O(log distance) exact evaluations instead of the tree raising
+                    // the bar one passing candidate at a time.  Any candidate is a valid bar, so
+                    // the result does not depend on it (the tree below still proves the maximum).
                     const int kb = idx[r] >= 0 ? idx[r] / Nl : hk;
-                    const int dir = kb > hk ? 1 : (kb < hk ? -1 : 0);
+                    const int dir = kb >= hk + wn ? 1 : (kb <= hk - wn ? -1 : 0);
                     if (dir != 0 && !(A.variant & 32)) {
                         int k = kb, step = 2;
                         for (;;) {
@@ -855,10 +877,11 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
             idx[r] = A.idx0[t] == -2 ? -1 : A.idx0[t];
         }
     }
-    unsigned nhits = 0, nsup = 0, nblk = 0, nfine = 0;
+    unsigned nhits = 0, nsup = 0, nblk = 0, nfine = 0, lane_pairs = 0;
     const long long t_start = A.trace ? (long long)wall_clock64() : 0;
     // phase cycle counters (trace mode): startup, superblock() calls, fine screens, exact paths
     long long cyc[4] = {0, 0, 0, 0}, c_mark = A.trace ? (long long)__builtin_amdgcn_s_memtime() : 0;
+    const long long c_mark0 = c_mark;
     auto stamp = [&](int ph) __attribute__((always_inline)) {
         if (A.trace) {
             const long long now = (long long)__builtin_amdgcn_s_memtime();
@@ -926,7 +949,7 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
         // overlap): lanes l0 + stride*u of (dv, av) hold (Dmax, a at the block start); bit u
         // of the result is set when some sub-state passes bound u (u < cnt)
         constexpr int RL = R * LB, G = StageGroup<RL>::G;
-        auto mask8 = [&](double dv, double av, int l0, int stride, int cnt)
+        auto mask8 = [&](double dv, double av, int l0, int stride, int cnt, bool sub = false)
                          __attribute__((always_inline)) {
             double dmax[8], a0[8];
 #pragma unroll
@@ -962,6 +985,9 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
             unsigned m = 0;
 #pragma unroll
             for (int u = 0; u < 8; ++u) m |= (__any(pu[u]) ? 1u : 0u) << u;
+            if (A.trace && sub)  // (instrumentation) this lane's own passing sub-blocks
+#pragma unroll
+                for (int u = 0; u < 8; ++u) lane_pairs += (u < cnt && pu[u]) ? 1u : 0u;
             return m & ((1u << cnt) - 1u);
         };
         // candidates [k0, k1), k1 - k0 <= 8, of superblock sbase staged in LDS.  The exact
@@ -1079,7 +1105,7 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
                 const int b = __builtin_ctz(bm);
                 const int nsub = min(8, (kg - (sbase + (b << 6)) + 7) >> 3);
                 if (A.hitcount || A.trace) nblk += nsub;
-                pass |= (unsigned long long)mask8(dm8, a8, 8 * b, 1, nsub) << (8 * b);
+                pass |= (unsigned long long)mask8(dm8, a8, 8 * b, 1, nsub, true) << (8 * b);
             }
 #pragma unroll
             for (int b = 0; b < 8; ++b)  // all loads issued before any is used
@@ -1194,6 +1220,7 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
     }
 
     exchange();
+    const long long c_end = A.trace ? (long long)__builtin_amdgcn_s_memtime() : 0;
 
     // final outputs, wave 0 (the merge kernel's rules: Aiyagari_VFI.m:79-81,
     // Labor_VFI.m:85,106-109)
@@ -1230,6 +1257,10 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
     block_max_to_slots(okd, dmax, A.diff);
     if (A.trace) {  // instrumentation (aiy_ws_set_timing bit 2): per-wave sums into wave 0
         __shared__ unsigned s_cnt[W][4];
+        __shared__ unsigned s_pairs;
+        if (threadIdx.x == 0) s_pairs = 0;
+        __syncthreads();
+        atomicAdd(&s_pairs, lane_pairs);
         if (lane == 0) {
             s_cnt[wave][0] = nsup; s_cnt[wave][1] = nblk; s_cnt[wave][2] = nfine; s_cnt[wave][3] = nhits;
         }
@@ -1246,6 +1277,10 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
             }
             tr[7] = blockIdx.x;
             for (int c = 0; c < 4; ++c) tr[8 + c] = cyc[c];
+            tr[12] = t_boot;                                   // kernel entry (wall clock)
+            tr[13] = c_mark0 - c_boot;                         // start-up cycles (hint, climb)
+            tr[14] = (long long)__builtin_amdgcn_s_memtime() - c_end;  // output cycles
+            tr[15] = s_pairs;  // (state, sub-block) pairs passing the 8-block bound
         }
     }
     if (A.hitcount) {  // instrumentation (aiy_ws_set_timing bit 1)

@@ -611,7 +611,7 @@ int aiy_ws_invalidate(aiy_ws* ws) {
 
 int aiy_ws_set_variant(aiy_ws* ws, int variant) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
-    if (variant < -1 || variant > 255) return fail(AIY_BAD_ARG, "variant in [-1, 255]");
+    if (variant < -1 || variant > 511) return fail(AIY_BAD_ARG, "variant in [-1, 511]");
     ws->variant = variant;
     return AIY_OK;
 }

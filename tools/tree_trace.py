@@ -50,6 +50,15 @@ def main():
                     x = T[:, col].astype(float)
                     c = np.corrcoef(x, dur)[0, 1] if x.std() > 0 else 0
                     print(f"  {name}: mean {x.mean():.1f} max {x.max():.0f} corr(dur) {c:.2f}")
+                boot = (T[:, 0] - T[:, 12]) / 100.0
+                print("  entry->start us p50/p90/max: %s; start-up cycles mean %.0f; output cycles "
+                      "mean %.0f; entry spread %.1f us" % (np.percentile(boot, [50, 90, 100]).round(1),
+                      T[:, 13].mean(), T[:, 14].mean(), (T[:, 12].max() - T[:, 12].min()) / 100.0))
+                pairs = T[:, 15].astype(float)
+                nsubpass = T[:, 5].astype(float) / 8.0  # candidate tests / 8 per passing sub-block
+                print("  (state, sub-block) pairs passing per wave: mean %.1f; passing sub-blocks "
+                      "x 64 lanes: mean %.1f (ratio %.3f)" % (pairs.mean(), (nsubpass * 64).mean(),
+                      pairs.sum() / max((nsubpass * 64).sum(), 1)))
                 cy = T[:, 8:12].astype(float)
                 print("  wave-0 cycles mean: top/sup-tests %.0f  block-tests %.0f  fine %.0f  exact %.0f"
                       % tuple(cy.mean(0)))
