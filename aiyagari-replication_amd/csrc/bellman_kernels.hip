@@ -757,12 +757,19 @@ __global__ __launch_bounds__(256, MINW) void bell_screen_kernel(BellArgs A, int 
 // then take the remaining superblocks round-robin; a last exchange folds the results.
 // The starting bar is the hint (last sweep's argmax) and its two neighbours, or — on a cold
 // start — the init kernel's candidate (best0/idx0).
-template <int NP, bool LAB, int R, int LB, int W>
+// INS: the instrumented build (per-state work counters, per-item trace); the production
+// instantiation compiles every counter and time stamp out
+template <int NP, bool LAB, int R, int LB, int W, bool INS>
 __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntile) {
     const int lane = threadIdx.x & 63;
     const int wave = readfirst(threadIdx.x >> 6);
-    const long long t_boot = A0.trace ? (long long)wall_clock64() : 0;  // (instrumentation)
-    const long long c_boot = A0.trace ? (long long)__builtin_amdgcn_s_memtime() : 0;
+    // every kernel argument the start-up reads, in one batch of scalar loads (otherwise the
+    // compiler fetches them in dependent rounds as the control flow reaches each use)
+    asm volatile("" ::"s"(A0.a), "s"(A0.Dt), "s"(A0.EV), "s"(A0.kf), "s"(A0.hint), "s"(A0.v_old),
+                 "s"(A0.Dm512), "s"(A0.s), "s"(A0.r), "s"(A0.w), "s"(A0.N), "s"(A0.Na),
+                 "s"(A0.variant), "s"(A0.C), "s"(A0.nb512), "s"(A0.sigma), "s"(A0.trace));
+    const long long t_boot = (INS && A0.trace) ? (long long)wall_clock64() : 0;  // (instrumentation)
+    const long long c_boot = (INS && A0.trace) ? (long long)__builtin_amdgcn_s_memtime() : 0;
     int item = (A0.variant & 16) ? xcd_remap((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
     BellArgs A = A0;
     if (A0.C > 1) {  // batched candidates: blocks [c·N·ntile, (c+1)·N·ntile) are candidate c's
@@ -878,12 +885,12 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
         }
     }
     unsigned nhits = 0, nsup = 0, nblk = 0, nfine = 0, lane_pairs = 0;
-    const long long t_start = A.trace ? (long long)wall_clock64() : 0;
+    const long long t_start = (INS && A.trace) ? (long long)wall_clock64() : 0;
     // phase cycle counters (trace mode): startup, superblock() calls, fine screens, exact paths
-    long long cyc[4] = {0, 0, 0, 0}, c_mark = A.trace ? (long long)__builtin_amdgcn_s_memtime() : 0;
+    long long cyc[4] = {0, 0, 0, 0}, c_mark = (INS && A.trace) ? (long long)__builtin_amdgcn_s_memtime() : 0;
     const long long c_mark0 = c_mark;
     auto stamp = [&](int ph) __attribute__((always_inline)) {
-        if (A.trace) {
+        if (INS && A.trace) {
             const long long now = (long long)__builtin_amdgcn_s_memtime();
             cyc[ph] += now - c_mark;
             c_mark = now;
@@ -985,7 +992,7 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
             unsigned m = 0;
 #pragma unroll
             for (int u = 0; u < 8; ++u) m |= (__any(pu[u]) ? 1u : 0u) << u;
-            if (A.trace && sub)  // (instrumentation) this lane's own passing sub-blocks
+            if (INS && A.trace && sub)  // (instrumentation) this lane's own passing sub-blocks
 #pragma unroll
                 for (int u = 0; u < 8; ++u) lane_pairs += (u < cnt && pu[u]) ? 1u : 0u;
             return m & ((1u << cnt) - 1u);
@@ -994,12 +1001,15 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
         // screen test on all of them without a branch (the current argmax itself is masked:
         // its value is known) gives one vote per candidate; only voted candidates take the
         // exact path: re-test per lane, exact value in the literal MATLAB order, merge
-        auto fine = [&](int sbase, int k0, int k1) __attribute__((always_inline)) {
-            if (A.hitcount || A.trace) nfine += k1 - k0;
-            double2 tk[8];
+        // the eight staged candidates of 8-block `bit` (broadcast LDS reads, all in flight);
+        // the whole 64-block is staged, candidates past the feasible range are masked by fine()
+        auto load_tk = [&](int bit, double2 (&tk)[8]) __attribute__((always_inline)) {
 #pragma unroll
-            for (int kk = 0; kk < 8; ++kk)  // broadcast reads, all in flight together
-                tk[kk] = s_cand[wave][k0 - sbase + kk];  // whole 64-block staged; kk >= k1 - k0 masked below
+            for (int kk = 0; kk < 8; ++kk) tk[kk] = s_cand[wave][(bit << 3) + kk];
+        };
+        auto fine = [&](int sbase, int k0, int k1, const double2 (&tk)[8])
+                        __attribute__((always_inline)) {
+            if (INS && (A.hitcount || A.trace)) nfine += k1 - k0;
             bool pk[8];
 #pragma unroll
             for (int g0 = 0; g0 < 8; g0 += G) {
@@ -1098,13 +1108,13 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
             const int nblock = min(8, (kg - sbase + 63) >> 6);
             unsigned own = 0;
             for (int b = bsel; b < nblock; b += bstep) own |= 1u << b;
-            if (A.hitcount || A.trace) nblk += __builtin_popcount(own);
+            if (INS && (A.hitcount || A.trace)) nblk += __builtin_popcount(own);
             const unsigned bpass = mask8(dm64, a8, 0, 8, nblock) & own;
             unsigned long long pass = 0;  // bit 8b+u: sub-block u of block b passes
             for (unsigned bm = bpass; bm; bm &= bm - 1) {
                 const int b = __builtin_ctz(bm);
                 const int nsub = min(8, (kg - (sbase + (b << 6)) + 7) >> 3);
-                if (A.hitcount || A.trace) nblk += nsub;
+                if (INS && (A.hitcount || A.trace)) nblk += nsub;
                 pass |= (unsigned long long)mask8(dm8, a8, 8 * b, 1, nsub, true) << (8 * b);
             }
 #pragma unroll
@@ -1125,10 +1135,21 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
             __builtin_amdgcn_wave_barrier();  // a wave reads only its own slice
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             stamp(1);
-            for (unsigned long long pm = pass; pm; pm &= pm - 1) {
-                const int bit = __builtin_ctzll(pm);
-                const int k0 = sbase + (bit << 3);
-                fine(sbase, k0, min(k0 + 8, kg));
+            // the next 8-block's candidates are read from LDS while this one is screened (two
+            // register sets, unrolled by two: no copies)
+            double2 tkA[8], tkB[8];
+            unsigned long long pm = pass;
+            if (pm) load_tk(__builtin_ctzll(pm), tkA);
+            while (pm) {
+                const int b0 = __builtin_ctzll(pm);
+                pm &= pm - 1;
+                if (pm) load_tk(__builtin_ctzll(pm), tkB);
+                fine(sbase, sbase + (b0 << 3), min(sbase + (b0 << 3) + 8, kg), tkA);
+                if (!pm) break;
+                const int b1 = __builtin_ctzll(pm);
+                pm &= pm - 1;
+                if (pm) load_tk(__builtin_ctzll(pm), tkA);
+                fine(sbase, sbase + (b1 << 3), min(sbase + (b1 << 3) + 8, kg), tkB);
             }
             stamp(2);
             __builtin_amdgcn_wave_barrier();  // reads done before the next superblock's writes
@@ -1148,7 +1169,7 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
         }
         double2 st_cur[8], st_prev[8];
         if (sfirst >= 0) {  // (its bound would pass: it holds the bar's candidate)
-            ++nsup;
+            if (INS) ++nsup;
             double d8, a8;
             load8(sfirst, d8, a8);
             const unsigned long long p = prep(sfirst, wave, W, d8, a8, st_cur);
@@ -1194,7 +1215,7 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
                     if (sb != sfirst && sb % W == wave) own |= 1u << u;
                 }
                 if (!own) continue;
-                nsup += __builtin_popcount(own);
+                if (INS) nsup += __builtin_popcount(own);
                 sm = mask8(dm0, a0, s8, 1, cnt) & own;
             }
         };
@@ -1220,7 +1241,7 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
     }
 
     exchange();
-    const long long c_end = A.trace ? (long long)__builtin_amdgcn_s_memtime() : 0;
+    const long long c_end = (INS && A.trace) ? (long long)__builtin_amdgcn_s_memtime() : 0;
 
     // final outputs, wave 0 (the merge kernel's rules: Aiyagari_VFI.m:79-81,
     // Labor_VFI.m:85,106-109)
@@ -1255,7 +1276,7 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
         }
     }
     block_max_to_slots(okd, dmax, A.diff);
-    if (A.trace) {  // instrumentation (aiy_ws_set_timing bit 2): per-wave sums into wave 0
+    if (INS && A.trace) {  // instrumentation (aiy_ws_set_timing bit 2): per-wave sums into wave 0
         __shared__ unsigned s_cnt[W][4];
         __shared__ unsigned s_pairs;
         if (threadIdx.x == 0) s_pairs = 0;
@@ -1283,7 +1304,7 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
             tr[15] = s_pairs;  // (state, sub-block) pairs passing the 8-block bound
         }
     }
-    if (A.hitcount) {  // instrumentation (aiy_ws_set_timing bit 1)
+    if (INS && A.hitcount) {  // instrumentation (aiy_ws_set_timing bit 1)
         unsigned long long* hc = A.hitcount + 4 * (blockIdx.x % kDiffSlots);
         if (nhits) atomicAdd(hc, (unsigned long long)nhits);
         if (lane == 0) {
@@ -1691,7 +1712,11 @@ template <int NP, bool LAB, int R, int W>
 static void tree_geo(const BellArgs& A, hipStream_t st) {
     constexpr int LB = LAB ? 5 : 1;
     const int ntile = cdiv(A.Na, 64 * R);
-    bell_tree_kernel<NP, LAB, R, LB, W><<<std::max(A.C, 1) * A.N * ntile, 64 * W, 0, st>>>(A, ntile);
+    const int grid = std::max(A.C, 1) * A.N * ntile;
+    if (A.trace || A.hitcount)
+        bell_tree_kernel<NP, LAB, R, LB, W, true><<<grid, 64 * W, 0, st>>>(A, ntile);
+    else
+        bell_tree_kernel<NP, LAB, R, LB, W, false><<<grid, 64 * W, 0, st>>>(A, ntile);
 }
 // variant bit 0: 2 states per lane (A1 only); bits 1-2: waves per tile 1 (default), 2, 4, 8
 template <int NP, bool LAB, int R>
