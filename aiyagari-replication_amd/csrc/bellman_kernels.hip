@@ -760,7 +760,7 @@ __global__ __launch_bounds__(256, MINW) void bell_screen_kernel(BellArgs A, int 
 // INS: the instrumented build (per-state work counters, per-item trace); the production
 // instantiation compiles every counter and time stamp out
 template <int NP, bool LAB, int R, int LB, int W, bool INS>
-__global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntile) {
+__global__ __launch_bounds__(64 * W, W >= 2 ? 5 : 1) void bell_tree_kernel(BellArgs A0, int ntile) {
     const int lane = threadIdx.x & 63;
     const int wave = readfirst(threadIdx.x >> 6);
     // every kernel argument the start-up reads, in one batch of scalar loads (otherwise the
@@ -788,8 +788,10 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
     const double y = A.w * A.s[i];
     const int jbase = tile * (64 * R);
     __shared__ double2 s_cand[W][512];  // each wave's current superblock: (a_k, D_k)
-    __shared__ double s_xb[W][64 * R];  // best exchange
-    __shared__ int s_xi[W][64 * R];
+    // W >= 2 (cooperating waves): registers are budgeted for 5 waves per SIMD, so the staging
+    // and fine-screen software pipelines (two register sets each) are off and the screen
+    // stages four chains at a time; the best exchange reuses each wave's idle s_cand slice
+    constexpr bool LEAN = W >= 2;
 
     // loads that do not depend on the start-up below, issued first so that their latency
     // overlaps it: the level-0 bounds of the first 64 superblocks (first labour group) and v_old
@@ -902,16 +904,15 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
     auto exchange = [&]() __attribute__((always_inline)) {
         if constexpr (W > 1) {
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                s_xb[wave][r * 64 + lane] = best[r];
-                s_xi[wave][r * 64 + lane] = idx[r];
-            }
+            for (int r = 0; r < R; ++r)  // (index exact as a double)
+                s_cand[wave][r * 64 + lane] = make_double2(best[r], (double)idx[r]);
             __syncthreads();
             for (int v = 0; v < W; ++v)
 #pragma unroll
-                for (int r = 0; r < R; ++r)
-                    if (v != wave && s_xi[v][r * 64 + lane] >= 0)
-                        lexi_take(s_xb[v][r * 64 + lane], s_xi[v][r * 64 + lane], best[r], idx[r]);
+                for (int r = 0; r < R; ++r) {
+                    const double2 e = s_cand[v][r * 64 + lane];
+                    if (v != wave && (int)e.y >= 0) lexi_take(e.x, (int)e.y, best[r], idx[r]);
+                }
             __syncthreads();
         }
     };
@@ -955,7 +956,7 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
         // eight block bounds at once (independent dependency chains, so their latencies
         // overlap): lanes l0 + stride*u of (dv, av) hold (Dmax, a at the block start); bit u
         // of the result is set when some sub-state passes bound u (u < cnt)
-        constexpr int RL = R * LB, G = StageGroup<RL>::G;
+        constexpr int RL = R * LB, G = LEAN ? (RL <= 2 ? 4 : 2) : StageGroup<RL>::G;
         auto mask8 = [&](double dv, double av, int l0, int stride, int cnt, bool sub = false)
                          __attribute__((always_inline)) {
             double dmax[8], a0[8];
@@ -1121,7 +1122,8 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
             for (int b = 0; b < 8; ++b)  // all loads issued before any is used
                 if ((pass >> (8 * b)) & 0xffull) {
                     const int k = min(sbase + (b << 6) + lane, Na - 1);
-                    st[b] = make_double2(a[k], Drow[k]);
+                    if constexpr (LEAN) s_cand[wave][(b << 6) + lane] = make_double2(a[k], Drow[k]);
+                    else st[b] = make_double2(a[k], Drow[k]);
                 }
             stamp(1);
             return pass;
@@ -1129,9 +1131,10 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
         auto finish = [&](int sb, unsigned long long pass, const double2 (&st)[8])
                           __attribute__((always_inline)) {
             const int sbase = sb << 9;
+            if constexpr (!LEAN)
 #pragma unroll
-            for (int b = 0; b < 8; ++b)
-                if ((pass >> (8 * b)) & 0xffull) s_cand[wave][(b << 6) + lane] = st[b];
+                for (int b = 0; b < 8; ++b)
+                    if ((pass >> (8 * b)) & 0xffull) s_cand[wave][(b << 6) + lane] = st[b];
             __builtin_amdgcn_wave_barrier();  // a wave reads only its own slice
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             stamp(1);
@@ -1139,6 +1142,13 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
             // register sets, unrolled by two: no copies)
             double2 tkA[8], tkB[8];
             unsigned long long pm = pass;
+            if constexpr (LEAN) {
+                for (; pm; pm &= pm - 1) {
+                    const int b0 = __builtin_ctzll(pm);
+                    load_tk(b0, tkA);
+                    fine(sbase, sbase + (b0 << 3), min(sbase + (b0 << 3) + 8, kg), tkA);
+                }
+            }
             if (pm) load_tk(__builtin_ctzll(pm), tkA);
             while (pm) {
                 const int b0 = __builtin_ctzll(pm);
@@ -1230,6 +1240,11 @@ __global__ __launch_bounds__(64 * W) void bell_tree_kernel(BellArgs A0, int ntil
             const int nxt = next_sb();
             if (nxt >= 0) load8(nxt, pd, pa);
             const unsigned long long pc = prep(cur, 0, 1, d8, a8, st_cur);
+            if constexpr (LEAN) {  // staged straight to LDS: screen it now
+                if (pc) finish(cur, pc, st_cur);
+                cur = nxt;
+                continue;
+            }
             if (pass_prev) finish(sb_prev, pass_prev, st_prev);
 #pragma unroll
             for (int b = 0; b < 8; ++b) st_prev[b] = st_cur[b];
