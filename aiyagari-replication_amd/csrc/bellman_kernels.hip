@@ -117,7 +117,7 @@ __device__ __forceinline__ void screen_t(double (&t)[M], const double (&cx)[M],
 // pairs per stage group: 8 candidates × the sub-states of a lane, at most ~16 chains
 template <int RL>
 struct StageGroup {
-    static constexpr int G = RL <= 2 ? 8 : (RL <= 4 ? 4 : 2);
+    static constexpr int G = RL <= 2 ? 8 : (RL <= 4 ? 4 : 1);
 };
 
 // (max value, first index) merge; NaN never enters (MATLAB max omits NaN)
@@ -760,7 +760,7 @@ __global__ __launch_bounds__(256, MINW) void bell_screen_kernel(BellArgs A, int 
 // INS: the instrumented build (per-state work counters, per-item trace); the production
 // instantiation compiles every counter and time stamp out
 template <int NP, bool LAB, int R, int LB, int W, bool INS>
-__global__ __launch_bounds__(64 * W, W >= 2 ? 5 : 1) void bell_tree_kernel(BellArgs A0, int ntile) {
+__global__ __launch_bounds__(64 * W, W >= 2 ? 5 : 3) void bell_tree_kernel(BellArgs A0, int ntile) {
     const int lane = threadIdx.x & 63;
     const int wave = readfirst(threadIdx.x >> 6);
     // every kernel argument the start-up reads, in one batch of scalar loads (otherwise the
@@ -791,7 +791,7 @@ __global__ __launch_bounds__(64 * W, W >= 2 ? 5 : 1) void bell_tree_kernel(BellA
     // W >= 2 (cooperating waves): registers are budgeted for 5 waves per SIMD, so the staging
     // and fine-screen software pipelines (two register sets each) are off and the screen
     // stages four chains at a time; the best exchange reuses each wave's idle s_cand slice
-    constexpr bool LEAN = W >= 2;
+    constexpr bool LEAN = W >= 2 || LAB;  // (labour: keeps 3 waves per SIMD)
 
     // loads that do not depend on the start-up below, issued first so that their latency
     // overlaps it: the level-0 bounds of the first 64 superblocks (first labour group) and v_old
@@ -956,7 +956,7 @@ __global__ __launch_bounds__(64 * W, W >= 2 ? 5 : 1) void bell_tree_kernel(BellA
         // eight block bounds at once (independent dependency chains, so their latencies
         // overlap): lanes l0 + stride*u of (dv, av) hold (Dmax, a at the block start); bit u
         // of the result is set when some sub-state passes bound u (u < cnt)
-        constexpr int RL = R * LB, G = LEAN ? (RL <= 2 ? 4 : 2) : StageGroup<RL>::G;
+        constexpr int RL = R * LB, G = LEAN ? (RL <= 2 ? 4 : 1) : StageGroup<RL>::G;
         auto mask8 = [&](double dv, double av, int l0, int stride, int cnt, bool sub = false)
                          __attribute__((always_inline)) {
             double dmax[8], a0[8];

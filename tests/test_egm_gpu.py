@@ -63,3 +63,36 @@ def test_egm_nonmonotone_grid_is_reported(pkg, gpu):
     with pytest.raises(pkg.AiyError) as e:
         pkg.egm_step(pc0, a, np.array([1.0, 1.2]), np.full((2, 2), 0.5), 0.02, 1.0, 0.96, 5.0, 0.0)
     assert e.value.status == "AIY_BAD_ARG"
+
+
+@pytest.mark.parametrize("tol,max_iter", [(1e-5, 7), (1e-3, 1000), (1e-5, 1), (2e-2, 1000),
+                                          (1e-5, 16), (1e-5, 17)])
+def test_egm_speculative_solve_matches_oracle(pkg, gpu, tol, max_iter):
+    """The host-tier solve enqueues up to 16 steps between dist reads (ring of policy_c buffers,
+    the stopping step re-run for its policy_k): iteration count, dist and both policies equal
+    the one-read-per-step C loop for stops inside a batch, on a batch edge and at max_iter."""
+    cal = no.calib_aiyagari(Na=400, shocks="tauchen")
+    a, s, P = cal["a_grid"], cal["s"], cal["P"]
+    w = no.wage(0.04, 0.36, 0.08)
+    pc0 = np.tile(((1.04) * a + w * np.mean(s))[:, None], (1, s.size))
+    R = pkg.egm_solve(pc0, a, s, P, 0.04, w, 0.96, 5.0, cal["amin"], tol, max_iter)
+    Ro = corc.egm_solve(pc0.T, a, s, P, 0.04, w, 0.96, 5.0, cal["amin"], tol, max_iter)
+    assert R["iters"] == Ro["iters"]
+    assert np.array_equal(R["policy_c"], Ro["policy_c"].T)
+    assert np.array_equal(R["policy_k"], Ro["policy_k"].T)
+    assert R["dist"] == Ro["dist"]
+    L = pkg.labor_egm_solve(pc0, a, s, P, 0.04, w, 0.96, 5.0, 1.0, 1.0, cal["amin"], tol, max_iter)
+    Lo = corc.labor_egm_solve(pc0.T, a, s, P, 0.04, w, 0.96, 5.0, 1.0, 1.0, cal["amin"], tol,
+                              max_iter)
+    assert L["iters"] == Lo["iters"]
+    for k in ("policy_c", "policy_k", "policy_l"):
+        assert np.array_equal(L[k], Lo[k].T), k
+
+
+def test_egm_solve_nonmonotone_grid_is_reported(pkg, gpu):
+    a = np.linspace(0, 10, 50)
+    pc0 = np.tile(np.linspace(50, 0.01, 50)[:, None], (1, 2))
+    with pytest.raises(pkg.AiyError) as e:
+        pkg.egm_solve(pc0, a, np.array([1.0, 1.2]), np.full((2, 2), 0.5), 0.02, 1.0, 0.96, 5.0,
+                      0.0, 1e-6, 50)
+    assert e.value.status == "AIY_BAD_ARG"
