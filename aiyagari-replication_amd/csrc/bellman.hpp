@@ -62,6 +62,14 @@ int launch_bell_kf(const BellArgs& A, hipStream_t st);
 int launch_bell_init(const BellArgs& A, hipStream_t st);
 int launch_bell_screen(const BellArgs& A, hipStream_t st);
 int launch_bell_tree(const BellArgs& A, hipStream_t st);
+// Timing of the dominant kernel: when set, the next tree-kernel launch on this host thread
+// records these events as part of its own dispatch (hipExtLaunchKernelGGL), so their elapsed
+// time is the kernel's execution — the figure rocprofv3 reports — without the scheduling gaps
+// of separate event records.  The launch clears them.
+struct DispatchEvents {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+extern thread_local DispatchEvents g_dispatch_ev;
 int launch_bell_plain(const BellArgs& A, hipStream_t st);
 int launch_bell_merge(const BellArgs& A, int use_partial, hipStream_t st);
 int launch_bell_table_batch(const BellArgs& A, unsigned long long* slots, int sweep, double tol,

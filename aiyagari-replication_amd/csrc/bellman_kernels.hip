@@ -29,6 +29,8 @@
 //              policy_l = L(l), policy_c = c(l,k), and max|v_new − v_old| ignoring NaN via an
 //              order-independent atomicMax on IEEE bits.
 // Non-integer σ (or σ > 9) runs a plain exhaustive kernel (device pow/log).
+#include <hip/hip_ext.h>
+
 #include <algorithm>
 #include <type_traits>
 
@@ -1667,6 +1669,18 @@ __global__ void bell_plain_kernel(BellArgs A) {
 // ------------------------------------------------------------------------------ launchers
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
+thread_local DispatchEvents g_dispatch_ev;
+template <class K, class... Args>
+static void launch_dispatch_timed(K kernel, int grid, int block, hipStream_t st, Args... args) {
+    if (g_dispatch_ev.start) {
+        hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(block), 0, st, g_dispatch_ev.start,
+                              g_dispatch_ev.stop, 0, args...);
+        g_dispatch_ev = DispatchEvents{};
+    } else {
+        kernel<<<grid, block, 0, st>>>(args...);
+    }
+}
+
 int launch_bell_table(const BellArgs& A, hipStream_t st) {
     static_assert(2 * kDiffSlots <= kTableBlock, "table block clears the diff slots");
     dim3 grid(cdiv(A.Na, kTableBlock), A.N);
@@ -1729,9 +1743,10 @@ static void tree_geo(const BellArgs& A, hipStream_t st) {
     const int ntile = cdiv(A.Na, 64 * R);
     const int grid = std::max(A.C, 1) * A.N * ntile;
     if (A.trace || A.hitcount)
-        bell_tree_kernel<NP, LAB, R, LB, W, true><<<grid, 64 * W, 0, st>>>(A, ntile);
+        launch_dispatch_timed(bell_tree_kernel<NP, LAB, R, LB, W, true>, grid, 64 * W, st, A, ntile);
     else
-        bell_tree_kernel<NP, LAB, R, LB, W, false><<<grid, 64 * W, 0, st>>>(A, ntile);
+        launch_dispatch_timed(bell_tree_kernel<NP, LAB, R, LB, W, false>, grid, 64 * W, st, A,
+                              ntile);
 }
 // variant bit 0: 2 states per lane (A1 only); bits 1-2: waves per tile 1 (default), 2, 4, 8
 template <int NP, bool LAB, int R>
@@ -1748,7 +1763,8 @@ static void run_tree(const BellArgs& A, hipStream_t st) {
     if constexpr (NP > 0 && !LAB) {
         if (A.variant & 64) {  // four lanes per state, 16 states per wave
             const int ntile = cdiv(A.Na, 16);
-            bell_quad_kernel<NP><<<std::max(A.C, 1) * A.N * ntile, 64, 0, st>>>(A, ntile);
+            launch_dispatch_timed(bell_quad_kernel<NP>, std::max(A.C, 1) * A.N * ntile, 64, st, A,
+                                  ntile);
             return;
         }
     }

@@ -203,9 +203,16 @@ int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
         // tree screen: the hint (or, cold, the init kernel's candidate) sets the first bar;
         // the tree kernel writes the outputs itself
         if (!A.hint) AIY_TRY(launch_bell_init(A, st));
-        AIY_TRY(ws_timing_begin(ws, st));
-        AIY_TRY(launch_bell_tree(A, st));
-        AIY_TRY(ws_timing_end(ws, st));
+        if (ws->timing) {  // events recorded by the dispatch itself (g_dispatch_ev)
+            if (ws->ev_used == (int)ws->ev_start.size()) AIY_TRY(ws_timing_drain(ws));
+            g_dispatch_ev = DispatchEvents{ws->ev_start[ws->ev_used], ws->ev_stop[ws->ev_used]};
+            const int rc = launch_bell_tree(A, st);
+            g_dispatch_ev = DispatchEvents{};
+            AIY_TRY(rc);
+            ws->ev_used++;
+        } else {
+            AIY_TRY(launch_bell_tree(A, st));
+        }
     } else {
         AIY_TRY(launch_bell_init(A, st));
         AIY_TRY(ws_timing_begin(ws, st));

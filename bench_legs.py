@@ -205,8 +205,27 @@ def egm_leg(pkg, dev, Na, labor=False, steps=50, reps=5, cpu_threads=1):
                                       *args) for _ in range(reps_cpu)], th)
         cpu_out[f"cores_{th}"] = {"value": reps_cpu * states / dt, "seconds": dt}
     name = "Aiyagari_Endogenous_Labor_EGM" if labor else "Aiyagari_EGM"
+    # the whole solve through the host tier (the MEX path: speculative batches of steps between
+    # dist reads, policy arrays copied in and out), to tol = 1e-5 from the same start
+    pc_host = pc0.T.copy()  # Na x N, the script's layout
+    walls, iters = [], 0
+    for _ in range(3):
+        t0 = time.perf_counter()
+        if labor:
+            R = pkg.labor_egm_solve(pc_host, a, cal["s"], cal["P"], r, w, cal["beta"], cal["sigma"],
+                                    1.0, 1.0, cal["amin"], 1e-5, 1000)
+        else:
+            R = pkg.egm_solve(pc_host, a, cal["s"], cal["P"], r, w, cal["beta"], cal["sigma"],
+                              cal["amin"], 1e-5, 1000)
+        walls.append(time.perf_counter() - t0)
+        iters = R["iters"]
+    solve_s = _median(walls)
     return {"workload": f"{name} steps, Na={Na} Nz={N} Rouwenhorst, device tier (2 launches "
                         f"per step: Euler RHS, interp1 inversion)",
+            "solve": {"iters": iters, "wall_ms": solve_s * 1e3,
+                      "us_per_iteration": solve_s / max(iters, 1) * 1e6,
+                      "path": "host tier (aiy_egm_solve / aiy_labor_egm_solve): speculative "
+                              "batches of up to 16 steps per dist read, H2D/D2H included"},
             "value": states / (step_ms * 1e-3), "unit": "state-iterations/s",
             "us_per_step": step_ms * 1e3, "repeats": reps,
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -6,7 +6,9 @@ FETCH_SIZE reports half the bytes of wide coalesced reads, so it is doubled; WRI
 taken as is.  Infinity-Cache hits are counted by these counters (they are L2 memory-side
 requests), so the figure is an upper bound on DRAM bytes.
 
-    python tools/pmc_traffic.py gpurun_out/pmc [kernel-prefix] [out.json]
+    python tools/pmc_traffic.py gpurun_out/pmc [kernel-prefix] [out.json] [skip] [take]
+
+skip/take: drop the first `skip` launches of the kernel (warm-up sweeps), keep the next `take`.
 """
 import collections
 import csv
@@ -15,23 +17,27 @@ import sys
 from pathlib import Path
 
 
-def per_launch(run_dir: Path, counter: str, prefix: str):
+def per_launch(run_dir: Path, counter: str, prefix: str, skip: int = 0, take: int = 0):
     vals = collections.defaultdict(float)
     for f in run_dir.rglob("*counter_collection.csv"):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] == counter and prefix in r["Kernel_Name"]:
-                vals[r["Dispatch_Id"]] += float(r["Counter_Value"])
+                vals[int(r["Dispatch_Id"])] += float(r["Counter_Value"])
     if not vals:
         raise SystemExit(f"no {counter} rows for {prefix!r} under {run_dir}")
-    return sum(vals.values()) / len(vals), len(vals)
+    ids = sorted(vals)
+    ids = ids[skip:skip + take] if take else ids[skip:]
+    return sum(vals[d] for d in ids) / len(ids), len(ids)
 
 
 def main():
     src = Path(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc")
     prefix = sys.argv[2] if len(sys.argv) > 2 else "bell_tree_kernel"
     out = Path(sys.argv[3] if len(sys.argv) > 3 else "profiles/traffic_vfi_tree.json")
-    fkb, nf = per_launch(src / "fetch", "FETCH_SIZE", prefix)
-    wkb, nw = per_launch(src / "write", "WRITE_SIZE", prefix)
+    skip = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+    take = int(sys.argv[5]) if len(sys.argv) > 5 else 0
+    fkb, nf = per_launch(src / "fetch", "FETCH_SIZE", prefix, skip, take)
+    wkb, nw = per_launch(src / "write", "WRITE_SIZE", prefix, skip, take)
     rec = {"kernel": prefix, "launches": {"fetch": nf, "write": nw},
            "fetch_size_kb_raw": fkb, "write_size_kb": wkb,
            "bytes_per_launch": 2 * fkb * 1024 + wkb * 1024,
