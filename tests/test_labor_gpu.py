@@ -83,3 +83,39 @@ def test_labor_screen_stress_noisy_value(pkg, gpu, scale):
     vo, (pko, plo, pco, lino) = corc.labor_vfi_sweep(V, a, s, P, L, 0.04, w, 0.96, 5.0, 1.0, 2.0)
     assert np.array_equal(v, vo) and np.array_equal(lin - 1, lino)
     assert np.array_equal(pk, pko) and np.array_equal(pl, plo) and np.array_equal(pc, pco)
+
+
+@pytest.mark.parametrize("max_iter", [40, 5])
+def test_labor_solve_infeasible_states_keep_incoming(pkg, gpu, max_iter):
+    """the host-tier labour solve runs speculative batches of sweeps on
+    ring buffers; states with no feasible choice (Labor_VFI.m:85) must still end with the
+    incoming v_new and policies, exactly as the literal loop (sweep, stop test, v_old = v_new)
+    over the C oracle's sweep — for a stop inside a batch and for max_iter exhaustion."""
+    a = np.array([0.5, 1.0, 2.0, 3.0, 4.5, 6.0, 8.0])
+    s = np.array([0.2, 0.6])
+    P = np.array([[0.7, 0.3], [0.4, 0.6]])
+    L = np.array([0.4, 1.0])
+    r, w, tol = -0.5, 1.0, 1e-6
+    v0 = np.zeros((2, 7))
+    v_in = np.full((2, 7), 42.0)
+    pol = (np.full((2, 7), 1.5), np.full((2, 7), 2.5), np.full((2, 7), 3.5),
+           np.full((2, 7), 3, np.int32))
+    R = pkg.labor_vfi_solve(v0, a, s, P, L, r, w, 0.9, 5.0, 1.0, 2.0, tol, max_iter,
+                            v_new=v_in, policies=pol)
+    # the literal loop on the C oracle's sweep (lin 0-based there)
+    v_old, v_new = v0.copy(), v_in.copy()
+    p = (pol[0], pol[1], pol[2], pol[3] - 1)
+    it = 0
+    for it in range(1, max_iter + 1):
+        v_new, p = corc.labor_vfi_sweep(v_old, a, s, P, L, r, w, 0.9, 5.0, 1.0, 2.0,
+                                        v_new=v_new, pol=p)
+        if np.nanmax(np.abs(v_new - v_old)) < tol:
+            break
+        v_old = v_new.copy()
+    feasible = (1 + r) * a[None, :] + w * s[:, None] * L.max() > a[0]
+    assert (~feasible).any() and feasible.any()
+    assert R["iters"] == it
+    assert np.array_equal(R["v_new"], v_new)
+    assert np.array_equal(R["policy_k"], p[0]) and np.array_equal(R["policy_l"], p[1])
+    assert np.array_equal(R["policy_c"], p[2]) and np.array_equal(R["lin"] - 1, p[3])
+    assert np.all(R["v_new"][~feasible] == 42.0) and np.all(R["lin"][~feasible] == 3)
