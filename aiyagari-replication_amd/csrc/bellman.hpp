@@ -76,4 +76,22 @@ int launch_bell_table_batch(const BellArgs& A, unsigned long long* slots, int sw
                             hipStream_t st);
 size_t bell_partial_slots(const BellArgs& A);
 
+// Persistent small-grid solve (A2 for A1 with the tree screen): sweeps g0+1 .. max_iter of the
+// plain loop in ONE cooperative launch — table phase, grid barrier, tree phase, grid barrier,
+// the stop test on the device — so no sweep pays a kernel boundary or a host round trip.
+// A holds the sweeps' common arguments (hint = idx); V[g & 1] is sweep g's output.
+struct PersistArgs {
+    BellArgs A;
+    double* V0;
+    double* V1;
+    const unsigned long long* first;  // [2*kDiffSlots] sweep g0's diff slots
+    unsigned long long* slots;        // [2][2*kDiffSlots]
+    unsigned* bar;                    // [4] barrier counter, generation, registrations, tickets (zeroed)
+    long long* result;                // [2] sweeps done (g*), status: 0 exhausted, 1 stop, 2 barrier timeout
+    double tol;
+    long long g0, max_iter;
+};
+int launch_bell_persist(const PersistArgs& PA, hipStream_t st);
+bool bell_persist_eligible(const BellArgs& A);
+
 }  // namespace aiy

@@ -761,8 +761,11 @@ __global__ __launch_bounds__(256, MINW) void bell_screen_kernel(BellArgs A, int 
 // start — the init kernel's candidate (best0/idx0).
 // INS: the instrumented build (per-state work counters, per-item trace); the production
 // instantiation compiles every counter and time stamp out
+// The body of one work item (tile of row i); block_id / nblocks are the launch coordinates (the
+// persistent solve calls it for several items per workgroup).
 template <int NP, bool LAB, int R, int LB, int W, bool INS>
-__global__ __launch_bounds__(64 * W, W >= 2 ? 5 : 3) void bell_tree_kernel(BellArgs A0, int ntile) {
+__device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, int block_id,
+                                               int nblocks) {
     const int lane = threadIdx.x & 63;
     const int wave = readfirst(threadIdx.x >> 6);
     // every kernel argument the start-up reads, in one batch of scalar loads (otherwise the
@@ -772,7 +775,7 @@ __global__ __launch_bounds__(64 * W, W >= 2 ? 5 : 3) void bell_tree_kernel(BellA
                  "s"(A0.variant), "s"(A0.C), "s"(A0.nb512), "s"(A0.sigma), "s"(A0.trace));
     const long long t_boot = (INS && A0.trace) ? (long long)wall_clock64() : 0;  // (instrumentation)
     const long long c_boot = (INS && A0.trace) ? (long long)__builtin_amdgcn_s_memtime() : 0;
-    int item = (A0.variant & 16) ? xcd_remap((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+    int item = (A0.variant & 16) ? xcd_remap(block_id, nblocks) : block_id;
     BellArgs A = A0;
     if (A0.C > 1) {  // batched candidates: blocks [c·N·ntile, (c+1)·N·ntile) are candidate c's
         const int c = item / (A0.N * ntile);
@@ -1313,7 +1316,7 @@ __global__ __launch_bounds__(64 * W, W >= 2 ? 5 : 3) void bell_tree_kernel(BellA
                 for (int v = 0; v < W; ++v) sum += s_cnt[v][c];
                 tr[3 + c] = sum;
             }
-            tr[7] = blockIdx.x;
+            tr[7] = block_id;
             for (int c = 0; c < 4; ++c) tr[8 + c] = cyc[c];
             tr[12] = t_boot;                                   // kernel entry (wall clock)
             tr[13] = c_mark0 - c_boot;                         // start-up cycles (hint, climb)
@@ -1330,6 +1333,173 @@ __global__ __launch_bounds__(64 * W, W >= 2 ? 5 : 3) void bell_tree_kernel(BellA
             atomicAdd(hc + 2, nblk * ns);
             if (nfine) atomicAdd(hc + 3, nfine * ns);
         }
+    }
+}
+
+template <int NP, bool LAB, int R, int LB, int W, bool INS>
+__global__ __launch_bounds__(64 * W, W >= 2 ? 5 : 3) void bell_tree_kernel(BellArgs A0, int ntile) {
+    bell_tree_item<NP, LAB, R, LB, W, INS>(A0, ntile, (int)blockIdx.x, (int)gridDim.x);
+}
+
+// ------------------------------------------------------------------------------ 3'''. persistent
+// A2 for small grids (the script's Na = 400 GE solves): at 2,800 states a sweep's two kernels
+// take ~5 + ~9 us, mostly launch ramp and the dependency gap between them, and the speculative
+// host loop still pays a read per batch.  Here one cooperative launch of one-wave workgroups
+// runs the sweeps itself: the table phase (EV, D, 8- and 512-block maxima: the table kernel's
+// values, 64 lanes x 8 passes per 512-candidate chunk), a grid barrier, the tree phase (the tree
+// kernel's item body, unchanged), a grid barrier, then every workgroup folds the same diff
+// slots and takes the same stop decision (Aiyagari_VFI.m:85-86).  Sweep g reads V[(g-1) & 1]
+// and writes V[g & 1], the plain loop's buffers; idx (= the next hint), pk and pc are
+// rewritten in place by each state's own lane.  The grid barrier: one counter and a
+// generation word, vector atomics, all working workgroups on one XCD (below); a waiter gives
+// up after ~2^25 short sleeps, reports status 2 and leaves the kernel, so a
+// lost workgroup cannot hang the device (co-residency itself is guaranteed by the cooperative
+// launch, which fails instead of running a grid that does not fit).
+// Barrier fences: agent scope (L2 write-back on release, invalidate on acquire), as a kernel
+// boundary does.  The workers all run on XCD 0 (below), so only its L2 is involved; lighter
+// same-XCD fences (vmcnt + L1 invalidate) were tried and were not sufficient on gfx950.
+// Measured at Na = 400: 31 us per sweep against 15 us for two ordinary launches per sweep in
+// the speculative loop — the barriers and the cold caches they leave cost more than the launch
+// gaps they remove — so the path is off by default (aiy_ws_set_persistent).
+__device__ __forceinline__ void xcd_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent"); }
+__device__ __forceinline__ void xcd_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); }
+// a coherent read of a word other workgroups update with atomics: an atomic RMW is performed
+// where the atomics are, never from a stale cache line
+__device__ __forceinline__ unsigned atomic_peek(unsigned* p) {
+    return __hip_atomic_fetch_or(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool grid_barrier(unsigned* bar, unsigned nblocks, long long* result) {
+    bool ok = true;
+    xcd_release();
+    if ((threadIdx.x & 63) == 0) {
+        const unsigned gen = atomic_peek(bar + 1);
+        if (__hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            nblocks - 1) {
+            __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            xcd_release();
+            __hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            unsigned spins = 0;
+            while (atomic_peek(bar + 1) == gen) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins == (1u << 25)) {
+                    __hip_atomic_store(result + 1, 2ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok = false;
+                    break;
+                }
+            }
+        }
+    }
+    xcd_acquire();
+    return __builtin_amdgcn_readfirstlane(ok ? 1 : 0) != 0;
+}
+
+// one 512-candidate chunk of row i: EV, Dt, Dm8 and Dm512 exactly as bell_table_kernel
+__device__ __forceinline__ void persist_table_chunk(const BellArgs& A,
+                                                    const double* __restrict__ V, int i,
+                                                    int chunk) {
+    const int lane = threadIdx.x & 63;
+    const int N = A.N, Na = A.Na;
+    double m512 = -__builtin_inf();
+    for (int u = 0; u < 8; ++u) {
+        const int k = chunk * 512 + u * 64 + lane;
+        const bool ok = k < Na;
+        double D = -__builtin_inf();
+        if (ok) {
+            const size_t t = (size_t)i * Na + k;
+            const double acc = table_ev(N, Na, A.P, V, A.beta, i, k);
+            A.EV[t] = acc;
+            D = table_D(acc, A.np);
+            A.Dt[t] = D;
+        }
+        double d8 = fmax(D, dpp_d<0xB1>(D));  // lane ^ 1
+        d8 = fmax(d8, dpp_d<0x4E>(d8));         // lane ^ 2
+        d8 = fmax(d8, dpp_d<0x104>(d8));        // lane + 4: the 8-block maximum at lanes 8j
+        if (ok && (k & 7) == 0) A.Dm8[(size_t)i * A.nb8 + (k >> 3)] = d8;
+        m512 = fmax(m512, D);
+    }
+    for (int off = 32; off > 0; off >>= 1) m512 = fmax(m512, __shfl_xor(m512, off));
+    if (lane == 0) A.Dm512[(size_t)i * A.nb512 + chunk] = m512;
+}
+
+template <int NP>
+__global__ __launch_bounds__(64) void bell_persist_kernel(PersistArgs PA) {
+    // The grid is 8x the working set.  Every workgroup registers; those running on XCD 0 (the
+    // hardware XCC id) draw tickets, the first gmax of them work and share XCD 0's L2, all others
+    // leave.  Workers wait until every workgroup has registered (the cooperative launch makes
+    // them all resident), so the worker count G is final before the first barrier.
+    const int lane = threadIdx.x & 63;
+    unsigned* reg = PA.bar + 2;  // [0] registered workgroups, [1] XCD-0 tickets
+    const unsigned gmax = gridDim.x / 8;
+    unsigned ticket = ~0u;
+    if (lane == 0) {
+        const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & 15;
+        if (xcc == 0) ticket = __hip_atomic_fetch_add(reg + 1, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+        xcd_release();
+        __hip_atomic_fetch_add(reg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    ticket = __builtin_amdgcn_readfirstlane(ticket);
+    if (ticket >= gmax) return;
+    if (lane == 0) {
+        unsigned spins = 0;
+        while (atomic_peek(reg) < gridDim.x) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins == (1u << 25)) {
+                __hip_atomic_store(PA.result + 1, 2ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+    }
+    const unsigned G = min(gmax, __builtin_amdgcn_readfirstlane(atomic_peek(reg + 1)));
+    const unsigned b = ticket;
+    xcd_acquire();
+    BellArgs A = PA.A;
+    const int ntile = (A.Na + 63) / 64, nitem = A.N * ntile, ntab = A.N * A.nb512;
+    // the stop test of a sweep from its diff slots (reduce_slots_kernel's fold)
+    auto stop_of = [&](const unsigned long long* sl) __attribute__((always_inline)) {
+        unsigned long long m = sl[2 * lane];
+        const bool any = __ballot(sl[2 * lane + 1] != 0ull) != 0ull;
+        for (int off = 32; off > 0; off >>= 1) {
+            const unsigned long long o = __shfl_xor(m, off);
+            m = o > m ? o : m;
+        }
+        return any && aiy_bitsd(m) < PA.tol;  // NaN-only: no stop (MATLAB max omits NaN)
+    };
+    long long g = PA.g0;
+    if (stop_of(PA.first)) {  // sweep g0 (the caller's ordinary launches) already stops
+        if (b == 0 && lane == 0) {
+            PA.result[0] = g;
+            PA.result[1] = 1;
+        }
+        return;
+    }
+    bool stopped = false;
+    for (g = PA.g0 + 1; g <= PA.max_iter; ++g) {
+        const double* Vold = (g & 1) ? PA.V0 : PA.V1;
+        double* Vnew = (g & 1) ? PA.V1 : PA.V0;
+        unsigned long long* sl = PA.slots + (size_t)(g & 1) * 2 * kDiffSlots;
+        if (b == 0) {  // (this set was last read by sweep g-2's stop test, two barriers ago)
+            sl[lane] = 0ull;
+            sl[64 + lane] = 0ull;
+        }
+        for (int q = (int)b; q < ntab; q += (int)G)
+            persist_table_chunk(A, Vold, q / A.nb512, q % A.nb512);
+        if (!grid_barrier(PA.bar, G, PA.result)) return;
+        A.v_old = Vold;
+        A.v_new = Vnew;
+        A.diff = sl;
+        for (int q = (int)b; q < nitem; q += (int)G)
+            bell_tree_item<NP, false, 1, 1, 1, false>(A, ntile, q, nitem);
+        if (!grid_barrier(PA.bar, G, PA.result)) return;
+        if (stop_of(sl)) {  // the same slots, the same decision in every workgroup
+            stopped = true;
+            break;
+        }
+    }
+    if (b == 0 && lane == 0) {
+        PA.result[0] = stopped ? g : PA.max_iter;
+        if (PA.result[1] != 2) PA.result[1] = stopped ? 1 : 0;
     }
 }
 
@@ -1704,6 +1874,41 @@ int launch_bell_kf(const BellArgs& A, hipStream_t st) {
 #ifndef AIY_BELL_R
 #define AIY_BELL_R 2
 #endif
+bool bell_persist_eligible(const BellArgs& A) {
+    return A.np >= 1 && A.np <= 8 && !A.labor && A.C <= 1 && A.tree && A.Na <= 4096 &&
+           A.Dt && A.Dm8 && A.Dm512 && !A.hitcount && !A.trace;
+}
+
+template <int NP>
+static int persist_go(const PersistArgs& PA, hipStream_t st) {
+    const int ntile = (PA.A.Na + 63) / 64;
+    const int items = std::max(PA.A.N * ntile, PA.A.N * PA.A.nb512);
+    int dev = 0, cus = 0, per_cu = 0;
+    AIY_HIP(hipGetDevice(&dev));
+    AIY_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    AIY_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bell_persist_kernel<NP>, 64, 0));
+    const int grid = std::min(items, std::max(1, per_cu * cus / 8));  // workgroups on XCD 0
+    PersistArgs a = PA;
+    void* args[] = {&a};
+    AIY_HIP(hipLaunchCooperativeKernel((const void*)bell_persist_kernel<NP>, dim3(8 * grid),
+                                       dim3(64), args, 0, st));
+    return AIY_OK;
+}
+
+int launch_bell_persist(const PersistArgs& PA, hipStream_t st) {
+    if (!bell_persist_eligible(PA.A)) return fail(AIY_BAD_ARG, "persistent solve: ineligible sweep");
+    switch (PA.A.np) {
+        case 1: return persist_go<1>(PA, st);
+        case 2: return persist_go<2>(PA, st);
+        case 3: return persist_go<3>(PA, st);
+        case 4: return persist_go<4>(PA, st);
+        case 5: return persist_go<5>(PA, st);
+        case 6: return persist_go<6>(PA, st);
+        case 7: return persist_go<7>(PA, st);
+        default: return persist_go<8>(PA, st);
+    }
+}
+
 template <int NP, bool LAB>
 struct Geo {
     static constexpr int R = LAB ? 1 : AIY_BELL_R;

@@ -106,7 +106,8 @@ int ws_timing_drain(aiy_ws* ws) {
 }
 
 // ---------------------------------------------------------------------------- Bellman sweep
-int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
+// validation, the kernel arguments of one sweep, and the cached feasible prefixes
+static int bell_args(aiy_ws* ws, const BellCall& c, BellArgs& A, hipStream_t st) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
     if (!c.v_old || !c.a || !c.s || !c.P || !c.v_new || !c.idx)
         return fail(AIY_BAD_ARG, "NULL device pointer");
@@ -114,7 +115,7 @@ int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
         return fail(AIY_BAD_ARG, "labour sweep needs labor_choice and 1 <= Nl <= workspace Nl");
     if (!(c.beta == c.beta) || !(c.r == c.r) || !(c.w == c.w) || !(c.sigma == c.sigma))
         return fail(AIY_NON_FINITE, "non-finite scalar argument");
-    BellArgs A{};
+    A = BellArgs{};
     A.N = (int)ws->N;
     A.Na = (int)ws->Na;
     A.Nl = c.labor ? (int)c.Nl : 1;
@@ -123,7 +124,6 @@ int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
     A.np = is_int_ge(c.sigma, 2.0) && c.sigma <= 9.0 ? (int)c.sigma - 1 : 0;
     if (c.mode == 1 && A.np == 0)
         return fail(AIY_BAD_ARG, "screened sweep (mode 1) needs integer sigma in [2, 9]");
-    bool screened = (c.mode != 2) && A.np > 0;
     A.coarse = ws->coarse;
     A.CK = ws->CK;
     // default geometry by size (measured at Na = 400: 2 cooperating waves per tile 10 % faster;
@@ -197,6 +197,13 @@ int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
         ws->kf_r = c.r; ws->kf_w = c.w; ws->kf_a = c.a; ws->kf_s = c.s; ws->kf_L = A.L;
         ws->kf_Nl = A.Nl; ws->kf_lab = A.labor;
     }
+    return AIY_OK;
+}
+
+int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
+    BellArgs A;
+    AIY_TRY(bell_args(ws, c, A, st));
+    const bool screened = (c.mode != 2) && A.np > 0;
     AIY_TRY(launch_bell_table(A, st));  // also clears the diff slots
     if (!screened) A.coarse = 0, A.hint = nullptr;
     if (screened && A.tree) {
@@ -343,10 +350,63 @@ static int bell_solve_spec(aiy_ws* ws, BellCall c, double* v_a, double* v_b, dou
     return AIY_OK;
 }
 
+// A2 on small grids: sweep 1 through the ordinary launches (cold start, cached feasible
+// prefixes), then sweeps 2..max_iter in one persistent cooperative launch that tests the stop
+// rule itself (bell_persist_kernel).  Same buffers and results as the plain loop: sweep g
+// writes buf[g & 1] (buf = {v_a, v_b}), idx/pk/pc hold the stopping sweep's policies, and on
+// exhaustion v_old = v_new.  Returns kNotApplicable when the sweep is not eligible.
+static constexpr int kNotApplicable = -1;
+static int bell_solve_persist(aiy_ws* ws, const BellCall& c, double* v_a, double* v_b,
+                              double tol, int64_t max_iter, int64_t* iters, int* out_new,
+                              hipStream_t st) {
+    BellCall c1 = c;
+    c1.keep_incoming = true;
+    c1.v_old = v_a;
+    c1.v_new = v_b;
+    BellArgs A;
+    AIY_TRY(bell_args(ws, c1, A, st));
+    if (c.mode == 2 || !bell_persist_eligible(A)) return kNotApplicable;
+    if (!ws->pers) AIY_TRY(dalloc(&ws->pers, 4 * (size_t)kDiffSlots + 8));
+    AIY_TRY(bell_sweep_dev(ws, c1, st));  // sweep 1
+    PersistArgs PA{};
+    PA.A = A;
+    PA.A.hint = c.idx;  // sweep g >= 2: the previous sweep's argmax
+    PA.A.keep_incoming = false;
+    PA.A.fold = nullptr;
+    PA.V0 = v_a;
+    PA.V1 = v_b;
+    PA.first = ws->diff;
+    PA.slots = ws->pers;
+    PA.bar = reinterpret_cast<unsigned*>(ws->pers + 4 * kDiffSlots);
+    PA.result = reinterpret_cast<long long*>(ws->pers + 4 * kDiffSlots + 2);
+    PA.tol = tol;
+    PA.g0 = 1;
+    PA.max_iter = max_iter;
+    AIY_HIP(hipMemsetAsync(ws->pers + 4 * kDiffSlots, 0, 8 * sizeof(unsigned long long), st));
+    AIY_TRY(launch_bell_persist(PA, st));
+    long long res[2] = {0, 0};
+    AIY_HIP(hipMemcpyAsync(res, PA.result, sizeof res, hipMemcpyDeviceToHost, st));
+    AIY_HIP(hipStreamSynchronize(st));
+    if (res[1] == 2) return fail(AIY_HIP_ERROR, "persistent solve: grid barrier timed out");
+    const int64_t g = res[0];
+    double* vnew = (g & 1) ? v_b : v_a;
+    if (res[1] == 0)  // exhausted: v_old = v_new after the last sweep (Aiyagari_VFI.m:88)
+        AIY_HIP(hipMemcpyAsync((g & 1) ? v_a : v_b, vnew, sizeof(double) * ws->N * ws->Na,
+                               hipMemcpyDeviceToDevice, st));
+    *iters = g;
+    *out_new = (g & 1) ? 1 : 0;
+    return AIY_OK;
+}
+
 int bell_solve_dev(aiy_ws* ws, BellCall c, double* v_a, double* v_b, double tol,
                    int64_t max_iter, int64_t* iters, int* out_new, hipStream_t st) {
     if (max_iter < 1) return fail(AIY_BAD_ARG, "max_iter must be >= 1");
     if (!c.idx) return fail(AIY_BAD_ARG, "NULL device pointer");
+    if (ws && ws->spec_max > 1 && !c.diff_out && ws->variant < 0 && ws->persist &&
+        !ws->timing && !ws->count_hits && !ws->tracing && !c.labor) {
+        const int rc = bell_solve_persist(ws, c, v_a, v_b, tol, max_iter, iters, out_new, st);
+        if (rc != kNotApplicable) return rc;
+    }
     if (ws && ws->spec_max > 1 && !c.diff_out) {
         // rings: (spec_max + 1) value buffers + spec_max sets of idx and 3 policies
         const size_t n = (size_t)ws->N * ws->Na;
@@ -620,6 +680,13 @@ int aiy_ws_set_variant(aiy_ws* ws, int variant) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
     if (variant < -1 || variant > 511) return fail(AIY_BAD_ARG, "variant in [-1, 511]");
     ws->variant = variant;
+    return AIY_OK;
+}
+
+int aiy_ws_set_persistent(aiy_ws* ws, int persistent) {
+    if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
+    if (persistent != 0 && persistent != 1) return fail(AIY_BAD_ARG, "persistent must be 0 or 1");
+    ws->persist = persistent != 0;
     return AIY_OK;
 }
 

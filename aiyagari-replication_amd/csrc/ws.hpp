@@ -64,6 +64,9 @@ struct aiy_ws {
     double* spec_pol = nullptr;                 // [spec_max][3][N*Na] (k, c, l)
     unsigned long long* spec_diff = nullptr;    // device [2*spec_max]
     unsigned long long* spec_hdiff = nullptr;   // pinned host [2*spec_max]
+    // persistent small-grid solve: diff slots [2][2*kDiffSlots], barrier words, result
+    unsigned long long* pers = nullptr;
+    bool persist = false;  // aiy_ws_set_persistent (measured slower: off by default)
     // speculative EGM solve: ring of spec_max + 1 policy_c buffers, per-step diff slots + flag
     size_t egm_spec_n = 0;
     int egm_spec_m = 0;
@@ -122,7 +125,7 @@ struct aiy_ws {
     }
     void free_all() {
         void* ps[] = {EV, T, T32, Dm, Dm8, Dt, Dm512, touched, best0, idx0, dis, kf, partial, diff, hitcount, trace, g0, g1, g2, gi,
-                      d_key, d_head, d_wr, d_mass, d_part};
+                      d_key, d_head, d_wr, d_mass, d_part, pers};
         for (void* p : ps)
             if (p) (void)hipFree(p);
         free_spec();
@@ -132,7 +135,7 @@ struct aiy_ws {
         EV = nullptr; T = nullptr; T32 = nullptr; Dm = nullptr; Dm8 = nullptr; Dt = nullptr; Dm512 = nullptr; touched = nullptr; best0 = nullptr; dis = nullptr; kf = nullptr; kf_cap = 0;
         kf_ok = false;
         idx0 = nullptr; partial = nullptr; diff = nullptr; hitcount = nullptr; trace = nullptr; trace_cap = 0; hdiff = nullptr;
-        g0 = g1 = g2 = nullptr; gi = nullptr;
+        g0 = g1 = g2 = nullptr; gi = nullptr; pers = nullptr;
         d_key = d_head = nullptr; d_wr = d_mass = d_part = nullptr;
         partial_cap = 0;
     }

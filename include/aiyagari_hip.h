@@ -235,6 +235,13 @@ int aiy_ws_set_search(aiy_ws* ws, int coarse_stride, int k_chunk);
  * discarded, so iteration count, v_new, v_old and policies do not depend on it; memory:
  * max_batch + 1 value buffers and max_batch policy sets per workspace. */
 int aiy_ws_set_speculation(aiy_ws* ws, int max_batch);
+/* A2 on small grids (Na <= 4096, A1 tree screen, integer sigma, default geometry): with
+ * persistent = 1 a solve runs sweep 1 with ordinary launches and every later sweep inside ONE
+ * cooperative launch that tests the stop rule on the device (no kernel boundary and no host
+ * read per sweep).  Results are identical either way.  Default 0 (the speculative loop): at
+ * Na = 400 the in-kernel grid barriers cost more than the launches they replace (31 vs 15 us
+ * per sweep). */
+int aiy_ws_set_persistent(aiy_ws* ws, int persistent);
 /* screen-kernel shape (tuning only; results are identical).  bit 3 clear (default): the bound
  * tree screen, bit 0 = 2 states per lane (else 1), bits 1-2 = 1, 2, 4 or 8 cooperating waves
  * per tile, bit 4 = XCD-aware tile order.  bit 3 set: the chunked screen + merge, with
