@@ -240,14 +240,22 @@ __global__ __launch_bounds__(kTableBlock) void bell_table_kernel(
         }
     }
     if (!T && !Dt) return;  // uniform per launch
-    // block maxima (NaN keys drop out of fmax: a NaN candidate is never a maximiser)
-    D = fmax(D, __shfl_xor(D, 1));
-    D = fmax(D, __shfl_xor(D, 2));
-    D = fmax(D, __shfl_xor(D, 4));
-    if (Dm8 && ok && (k & 7) == 0) Dm8[(size_t)i * nb8 + (k >> 3)] = D;
-    D = fmax(D, __shfl_xor(D, 8));
-    D = fmax(D, __shfl_xor(D, 16));
-    D = fmax(D, __shfl_xor(D, 32));
+    // block maxima (NaN keys drop out of fmax: a NaN candidate is never a maximiser), by DPP
+    // lane moves: lane ^ 1, lane ^ 2, lane + 4 give the 8-block maximum at lanes 8j; the
+    // reduction ladder gives the wave's 64-block maximum at lane 63
+    {
+        double d8 = fmax(D, dpp_d<0xB1>(D));
+        d8 = fmax(d8, dpp_d<0x4E>(d8));
+        d8 = fmax(d8, dpp_d<0x104>(d8));
+        if (Dm8 && ok && (k & 7) == 0) Dm8[(size_t)i * nb8 + (k >> 3)] = d8;
+    }
+    D = fmax(D, dpp_d<0xB1>(D));
+    D = fmax(D, dpp_d<0x4E>(D));
+    D = fmax(D, dpp_d<0x141>(D));         // row half-mirror: max of 8
+    D = fmax(D, dpp_d<0x140>(D));         // row mirror: max of 16
+    D = fmax(D, dpp_d<0x142, 0xa>(D));    // row_bcast:15: max of 32 in rows 1, 3
+    D = fmax(D, dpp_d<0x143, 0xc>(D));    // row_bcast:31: max of 64 in row 3
+    D = readlane_d(D, 63);
     if (Dm && ok && (k & 63) == 0) Dm[(size_t)i * nb + (k >> 6)] = D;
     if (Dm512) {
         if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = D;
@@ -307,14 +315,20 @@ __global__ __launch_bounds__(kTableBlock) void bell_table_batch_kernel(
         D = table_D(acc, np);
         Dt[t] = D;
     }
-    D = fmax(D, __shfl_xor(D, 1));
-    D = fmax(D, __shfl_xor(D, 2));
-    D = fmax(D, __shfl_xor(D, 4));
     const size_t rb8 = ((size_t)c * N + i) * nb8, rb512 = ((size_t)c * N + i) * nb512;
-    if (ok && (k & 7) == 0) Dm8[rb8 + (k >> 3)] = D;
-    D = fmax(D, __shfl_xor(D, 8));
-    D = fmax(D, __shfl_xor(D, 16));
-    D = fmax(D, __shfl_xor(D, 32));
+    {  // DPP maxima, as bell_table_kernel
+        double d8 = fmax(D, dpp_d<0xB1>(D));
+        d8 = fmax(d8, dpp_d<0x4E>(d8));
+        d8 = fmax(d8, dpp_d<0x104>(d8));
+        if (ok && (k & 7) == 0) Dm8[rb8 + (k >> 3)] = d8;
+    }
+    D = fmax(D, dpp_d<0xB1>(D));
+    D = fmax(D, dpp_d<0x4E>(D));
+    D = fmax(D, dpp_d<0x141>(D));
+    D = fmax(D, dpp_d<0x140>(D));
+    D = fmax(D, dpp_d<0x142, 0xa>(D));
+    D = fmax(D, dpp_d<0x143, 0xc>(D));
+    D = readlane_d(D, 63);
     if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = D;
     __syncthreads();
     if (threadIdx.x == 0) {
