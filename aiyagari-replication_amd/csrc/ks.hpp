@@ -45,6 +45,7 @@ int launch_ks_improve(const KsArgs& A, const double* V, const double* dV, double
                       int* nfev, hipStream_t st);
 int launch_ks_howard(const KsArgs& A, const double* V, const double* dV, const double* kopt,
                      double* Vn, hipStream_t st);
+int launch_ks_hints(const KsArgs& A, const double* kopt, hipStream_t st);
 int launch_ks_reldiff(const KsArgs& A, const double* V, const double* Vold,
                       unsigned long long* slots, hipStream_t st);
 }  // namespace aiy

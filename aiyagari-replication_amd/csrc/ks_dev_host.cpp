@@ -28,6 +28,7 @@ struct ks_dev {
     int ncols = 0;
     unsigned long long* slots = nullptr;
     int* seg = nullptr;    // [node] segment hints: improve writes them, Howard checks and uses them
+    ks_dev* seg_owner = nullptr;  // set: seg is that handle's array (ks_dev_share_hints)
 };
 
 namespace aiy {
@@ -57,7 +58,7 @@ extern "C" {
 
 int ks_dev_destroy(ks_dev* h) {
     if (!h) return AIY_OK;
-    void* ps[] = {h->kg, h->P, h->sl, h->dV, h->cols, h->slots, h->seg};
+    void* ps[] = {h->kg, h->P, h->sl, h->dV, h->cols, h->slots, h->seg_owner ? nullptr : h->seg};
     for (void* q : ps)
         if (q) (void)hipFree(q);
     delete h;
@@ -154,6 +155,29 @@ int ks_dev_reldiff(ks_dev* h, const double* V, const double* Vold, void* out, vo
     AIY_HIP(hipMemsetAsync(h->slots, 0, 2 * kDiffSlots * sizeof(unsigned long long), st));
     AIY_TRY(launch_ks_reldiff(shard_args(h), V, Vold, h->slots, st));
     AIY_TRY(launch_reduce_slots(h->slots, out, st));
+    return AIY_OK;
+}
+
+// Ghost shards (ks_dist.py, exchanges every m Howard sweeps): h reads and writes the segment
+// hints of `owner` (same grid), so the hints improve stores for the owner's nodes serve h's
+// sweeps over those nodes too.  owner must outlive h.
+int ks_dev_share_hints(ks_dev* h, ks_dev* owner) {
+    if (!h || !owner) return fail(AIY_BAD_ARG, "NULL argument");
+    if (h == owner) return AIY_OK;
+    if (owner->seg_owner) return fail(AIY_BAD_ARG, "owner shares another handle's hints");
+    if (h->nk != owner->nk || h->nK != owner->nK || h->dev != owner->dev)
+        return fail(AIY_BAD_SHAPE, "ks_dev_share_hints: handles of different grids or devices");
+    if (!h->seg_owner) AIY_HIP(hipFree(h->seg));
+    h->seg = owner->seg;
+    h->seg_owner = owner;
+    return AIY_OK;
+}
+
+// the segment hints of h's nodes from kopt (nodes whose k_opt another rank computed); a
+// hint only short-cuts Howard's search, so results never depend on it
+int ks_dev_hints(ks_dev* h, const double* kopt, void* stream) {
+    if (!h || !kopt) return fail(AIY_BAD_ARG, "NULL argument");
+    AIY_TRY(launch_ks_hints(shard_args(h), kopt, (hipStream_t)stream));
     return AIY_OK;
 }
 

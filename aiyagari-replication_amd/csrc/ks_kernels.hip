@@ -203,6 +203,16 @@ __global__ void ks_howard_kernel(KsArgs A, const double* __restrict__ V,
     Vn[n] = howard_node(A, W, n, k_opt[n]);
 }
 
+// the segment hints of the shard's nodes from k_opt (what ks_improve_kernel stores), for nodes
+// whose k_opt arrived from another rank (ks_dist.py ghost columns)
+__global__ void ks_hints_kernel(KsArgs A, const double* __restrict__ k_opt) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= A.n_local) return;
+    int n = A.node0 + blockIdx.y * A.sstride + t;
+    const double kp = k_opt[n];
+    A.seg_hint[n] = seg_of_dev(A.k_grid, A.nk, fmax(fmin(kp, A.k_grid[A.nk - 1]), A.k_grid[0]));
+}
+
 // max |v - v_old| / (|v_old| + 1e-10) ignoring NaN (:195)
 __global__ void ks_reldiff_kernel(KsArgs A, const double* __restrict__ V,
                                   const double* __restrict__ Vold,
@@ -362,6 +372,12 @@ int launch_ks_improve(const KsArgs& A, const double* V, const double* dV, double
 int launch_ks_howard(const KsArgs& A, const double* V, const double* dV, const double* kopt,
                      double* Vn, hipStream_t st) {
     ks_howard_kernel<<<dim3(cdiv(A.n_local, 256), std::max(A.ns, 1)), 256, 0, st>>>(A, V, dV, kopt, Vn);
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
+}
+int launch_ks_hints(const KsArgs& A, const double* kopt, hipStream_t st) {
+    if (!A.seg_hint) return AIY_OK;
+    ks_hints_kernel<<<dim3(cdiv(A.n_local, 256), std::max(A.ns, 1)), 256, 0, st>>>(A, kopt);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }

@@ -64,43 +64,87 @@ def forecast_index(K_grid, B, params):
     return out.reshape(4, Kg.size)
 
 
-def halo_plan(kp_idx, nK: int, world: int):
-    """plan[q][p] = sorted flat columns (s'·nK + K') rank q reads that rank p owns (p != q;
-    [] on the diagonal): for every node q owns, the forecast column K'_idx(s, K) of all four
-    s' (Krusell_Smith_VFI.m:343-349)."""
+def _need_plan(need, nK: int, world: int):
+    """plan[q][p] = sorted flat columns of need[q] that rank p owns (p != q; [] on the
+    diagonal)."""
     owner = np.empty(4 * nK, np.int64)
     for q in range(world):
         owner[owned_columns(nK, q, world)] = q
-    kp = np.asarray(kp_idx)
     plan = [[[] for _ in range(world)] for _ in range(world)]
     for q in range(world):
-        K0, K1, s0, s1 = shard_slices(nK, q, world)
-        targets = np.unique(kp[s0:s1, K0:K1])
-        need = sorted({sn * nK + int(t) for t in targets for sn in range(4)})
-        for c in need:
+        for c in sorted(set(int(c) for c in need[q])):
             if owner[c] != q:
                 plan[q][int(owner[c])].append(c)
     return plan
 
 
+def halo_plan(kp_idx, nK: int, world: int):
+    """plan[q][p] = sorted flat columns (s'·nK + K') rank q reads that rank p owns (p != q;
+    [] on the diagonal): for every node q owns, the forecast column K'_idx(s, K) of all four
+    s' (Krusell_Smith_VFI.m:343-349)."""
+    kp = np.asarray(kp_idx)
+    need = []
+    for q in range(world):
+        K0, K1, s0, s1 = shard_slices(nK, q, world)
+        targets = np.unique(kp[s0:s1, K0:K1])
+        need.append([sn * nK + int(t) for t in targets for sn in range(4)])
+    return _need_plan(need, nK, world)
+
+
+def ghost_rects(kp_idx, nK: int, K0: int, K1: int, s0: int, s1: int, depth: int):
+    """R_0 = the shard (K0, K1, s0, s1); R_j = the smallest rectangle (K range x all four s)
+    holding R_{j-1} and every column its nodes read (the forecast columns K'_idx(s, K) of all
+    s', Krusell_Smith_VFI.m:343-349).  A rank holding R_L current at sweep t can run sweep
+    t + i on R_{L-i} (its reads lie in R_{L-i+1}), so after L sweeps its own nodes are current
+    without any exchange in between: the communication-avoiding ("ghost zone") schedule."""
+    kp = np.asarray(kp_idx)
+    rects = [(K0, K1, s0, s1)]
+    for _ in range(depth):
+        Ka, Kb, sa, sb = rects[-1]
+        t = kp[sa:sb, Ka:Kb]
+        rects.append((min(Ka, int(t.min())), max(Kb, int(t.max()) + 1), 0, 4))
+    return rects
+
+
+def rect_columns(rect, nK: int):
+    Ka, Kb, sa, sb = rect
+    return [s * nK + K for s in range(sa, sb) for K in range(Ka, Kb)]
+
+
+def ghost_plan(kp_idx, nK: int, world: int, depth: int):
+    """Exchange plan for a block of `depth` sweeps: rank q receives every column of its
+    R_depth (ghost_rects) that another rank owns."""
+    need = [rect_columns(ghost_rects(kp_idx, nK, *shard_slices(nK, q, world), depth)[depth], nK)
+            for q in range(world)]
+    return _need_plan(need, nK, world)
+
+
+def _runs(cols):
+    """sorted columns -> [(c0, c1)) contiguous runs (rows of the flat (4·nK, k) view)"""
+    out = []
+    for c in cols:
+        if out and out[-1][1] == c:
+            out[-1][1] = c + 1
+        else:
+            out.append([c, c + 1])
+    return [(a, b) for a, b in out]
+
+
 class HaloExchange:
-    """Per-sweep exchange of the halo columns (rows of V viewed as (4·nK, k)) between ranks:
-    one batched set of point-to-point sends/receives (RCCL over xGMI on GPUs)."""
+    """Exchange of halo columns (rows of V viewed as (4·nK, k)) between ranks: one batched set
+    of point-to-point sends/receives (RCCL over xGMI on GPUs).  A column is contiguous in V and
+    a plan's columns from one peer are a few contiguous runs (one per s), so every send and
+    receive works on a view of V itself: no gather/scatter kernels on the exchange path."""
 
     def __init__(self, plan, rank: int, world: int, device, nk: int, dtype):
-        import torch
         self.rank, self.world = rank, world
         self.sends, self.recvs = [], []
         for p in range(world):
             if p == rank:
                 continue
-            if plan[p][rank]:   # what p reads from me
-                self.sends.append((p, torch.tensor(plan[p][rank], device=device)))
-            if plan[rank][p]:   # what I read from p
-                cols = torch.tensor(plan[rank][p], device=device)
-                self.recvs.append((p, cols, torch.empty((len(plan[rank][p]), nk),
-                                                        dtype=dtype, device=device)))
-        self.columns = sum(len(c) for _, c, _ in self.recvs)
+            self.sends += [(p, a, b) for a, b in _runs(plan[p][rank])]   # what p reads from me
+            self.recvs += [(p, a, b) for a, b in _runs(plan[rank][p])]   # what I read from p
+        self.columns = sum(b - a for _, a, b in self.recvs)
 
     def __call__(self, V):
         import torch
@@ -108,18 +152,18 @@ class HaloExchange:
         nccl = dist.get_backend() == "nccl"
         flat = V.view(-1, V.shape[-1])
         ops, staged = [], []
-        for p, cols in self.sends:
-            buf = flat.index_select(0, cols)
-            ops.append(dist.P2POp(dist.isend, buf if nccl else buf.cpu(), p))
-        for p, cols, buf in self.recvs:
-            rb = buf if nccl else torch.empty(buf.shape, dtype=buf.dtype)
-            staged.append((cols, rb))
+        for p, a, b in self.sends:
+            ops.append(dist.P2POp(dist.isend, flat[a:b] if nccl else flat[a:b].cpu(), p))
+        for p, a, b in self.recvs:
+            rb = flat[a:b] if nccl else torch.empty((b - a, flat.shape[1]), dtype=V.dtype)
+            if not nccl:
+                staged.append((a, b, rb))
             ops.append(dist.P2POp(dist.irecv, rb, p))
         if ops:
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
-        for cols, rb in staged:
-            flat.index_copy_(0, cols, rb.to(V.device))
+        for a, b, rb in staged:
+            flat[a:b].copy_(rb.to(V.device))
 
 
 class HipShard:
@@ -131,15 +175,19 @@ class HipShard:
         Kg = np.ascontiguousarray(K_grid, np.float64)
         self.K0, self.K1, self.s0, self.s1 = K0, K1, s0, s1
         self.kp_idx = forecast_index(Kg, B, params)
+        self._keep = (kg, Kg, np.ascontiguousarray(B, np.float64),
+                      np.asfortranarray(P, dtype=np.float64),
+                      np.ascontiguousarray(params, np.float64))
+        self._args = tuple(ptr(x) for x in self._keep) + (i64(kg.size), i64(Kg.size))
         h = vp()
-        check(lib().ks_dev_create_slice(ptr(kg), ptr(Kg), ptr(np.ascontiguousarray(B, np.float64)),
-                                        ptr(np.asfortranarray(P, dtype=np.float64)),
-                                        ptr(np.ascontiguousarray(params, np.float64)),
-                                        i64(kg.size), i64(Kg.size), i64(K0), i64(K1), i64(s0),
-                                        i64(s1), C.byref(h)))
+        check(lib().ks_dev_create_slice(*self._args, i64(K0), i64(K1), i64(s0), i64(s1),
+                                        C.byref(h)))
         self._h = h
+        self._ghosts = []
 
     def close(self):
+        for g in getattr(self, "_ghosts", []):  # they use this handle's hint array
+            g.close()
         if getattr(self, "_h", None):
             lib().ks_dev_destroy(self._h)
             self._h = None
@@ -155,6 +203,22 @@ class HipShard:
 
     def howard(self, V, kopt, Vout):
         check(lib().ks_dev_howard(self._h, ptr(V), ptr(kopt), ptr(Vout), stream_handle(None)))
+
+    def ghost(self, K0, K1, s0, s1):
+        """A shard over the rectangle (K0, K1, s0, s1) of other ranks' columns that shares this
+        shard's segment hints (ks_dev_share_hints; close it before this one)."""
+        g = HipShard.__new__(HipShard)
+        g.K0, g.K1, g.s0, g.s1, g.kp_idx = K0, K1, s0, s1, self.kp_idx
+        h = vp()
+        check(lib().ks_dev_create_slice(*self._args, i64(K0), i64(K1), i64(s0), i64(s1),
+                                        C.byref(h)))
+        g._h, g._args, g._keep, g._ghosts = h, self._args, self._keep, []
+        self._ghosts.append(g)
+        check(lib().ks_dev_share_hints(h, self._h))
+        return g
+
+    def hints(self, kopt):
+        check(lib().ks_dev_hints(self._h, ptr(kopt), stream_handle(None)))
 
     def reldiff(self, V, Vold):
         import torch
@@ -196,59 +260,150 @@ def _allreduce_max(x: float, device):
     return math.nan if v < 0 else v
 
 
+class HowardSweeps:
+    """The Jacobi Howard sweeps of one rank (Krusell_Smith_VFI.m:172-192) with their exchanges.
+
+    depth = 1: after every sweep the rank receives its halo (the forecast columns its nodes
+    read, `halo_plan`), one batched point-to-point exchange per sweep.
+    depth = m > 1 (communication-avoiding): before each block of L <= m sweeps the rank receives
+    every foreign column of its ghost rectangle R_L (`ghost_rects`), then sweep i of the block
+    runs on R_{L-i} — other ranks' columns are swept redundantly, with the same kernels on the
+    same inputs, so every value is bit-identical to the single-device solve — and only the
+    last sweep is confined to the rank's own nodes.  One exchange per block instead of per
+    sweep; after a policy improvement the rank also receives k_opt on R_{m-1} (the ghost
+    sweeps read it) and rebuilds the segment hints there.  After the last sweep the plain halo
+    is exchanged, so the state between calls is the depth-1 schedule's.
+    exchange = "allgather": every rank's owned slice to every rank after every sweep."""
+
+    def __init__(self, shard, nK, rank, world, V, depth=1, exchange="halo"):
+        self.shard, self.nK, self.rank, self.world = shard, nK, rank, world
+        self.depth = max(1, int(depth)) if (world > 1 and exchange == "halo") else 1
+        self.exchange = exchange
+        self.halo = None
+        self.blocks = {}     # L -> exchange before a block of L sweeps
+        self.rects = [(shard.K0, shard.K1, shard.s0, shard.s1)]
+        self.shards = [shard]
+        self.kx = None
+        nk = V.shape[-1]
+        self.nk = nk
+        if world > 1:
+            if exchange == "halo":
+                self.plan = halo_plan(shard.kp_idx, nK, world)
+                self.halo = HaloExchange(self.plan, rank, world, V.device, nk, V.dtype)
+                if self.depth > 1:
+                    self.rects = ghost_rects(shard.kp_idx, nK, *self.rects[0], self.depth)
+                    self.shards += [shard.ghost(*r) for r in self.rects[1:self.depth]]
+                    for L in range(1, self.depth + 1):
+                        self.blocks[L] = HaloExchange(ghost_plan(shard.kp_idx, nK, world, L),
+                                                      rank, world, V.device, nk, V.dtype)
+                    self.kx = self.blocks[self.depth - 1]   # k_opt on R_{m-1}
+            elif exchange != "allgather":
+                raise ValueError(f"exchange must be 'halo' or 'allgather', not {exchange!r}")
+        if exchange == "allgather" or world == 1:
+            import torch
+            self.own = torch.tensor(owned_columns(nK, rank, world), device=V.device)
+
+    def read_columns(self):
+        """Every column this rank ever reads or sweeps (own, halo and ghost columns)."""
+        cols = set(owned_columns(self.nK, self.rank, self.world))
+        if self.halo is not None:
+            cols |= {c for p in range(self.world) for c in self.plan[self.rank][p]}
+        if self.depth > 1:
+            cols |= set(rect_columns(self.rects[self.depth], self.nK))
+        return cols
+
+    def kopt_columns(self):
+        """Every column of k_opt this rank's sweeps read."""
+        cols = set(owned_columns(self.nK, self.rank, self.world))
+        if self.depth > 1:
+            cols |= set(rect_columns(self.rects[self.depth - 1], self.nK))
+        return cols
+
+    def improve(self, V, kopt):
+        """Policy improvement (:148-168) on the rank's nodes; with ghost sweeps, k_opt of the
+        ghost rectangle from its owners and the hints there."""
+        self.shard.improve(V, kopt)
+        if self.kx is not None:
+            self.kx(kopt)
+            self.shards[-1].hints(kopt)
+
+    def run(self, V, V2, kopt, n):
+        """n sweeps from V (current on the rank's nodes and halo); returns (V, V2) with V the
+        newest buffer, current on the rank's nodes and halo."""
+        if self.depth == 1:
+            for _ in range(n):
+                self.shard.howard(V, kopt, V2)
+                if self.halo is None and self.world > 1:  # allgather: carry the rest over
+                    fresh = V2.view(-1, self.nk).index_select(0, self.own)
+                    V2.copy_(V)
+                    V2.view(-1, self.nk).index_copy_(0, self.own, fresh)
+                V, V2 = V2, V
+                if self.halo is not None:
+                    self.halo(V)
+                elif self.world > 1:
+                    _exchange(V, self.rank, self.world, self.nK)
+            return V, V2
+        done = 0
+        while done < n:
+            L = min(self.depth, n - done)
+            self.blocks[L](V)                     # R_L current at this sweep
+            for i in range(1, L + 1):
+                self.shards[L - i].howard(V, kopt, V2)   # R_{L-i} at sweep + i
+                V, V2 = V2, V
+            done += L
+        if n:
+            self.halo(V)
+        return V, V2
+
+    def close(self):
+        for g in self.shards[1:]:
+            g.close()
+        self.shards = self.shards[:1]
+
+
 def ks_vfi_solve_dist(value, k_opt, shard, nK, howard_steps=50, tol=1e-6, max_vfi=10000,
-                      rank=0, world=1, exchange="halo", poison=False):
+                      rank=0, world=1, exchange="halo", poison=False, depth=1):
     """Krusell_Smith_VFI.m:141-204 for the current B.  value, k_opt: (4, K, k) tensors on this
-    rank's device, full arrays on every rank (in/out).  `shard` owns [K0, K1) (HipShard, or any
-    object with the same improve / howard / reldiff methods and a kp_idx table).  exchange:
-    "halo" (point-to-point, only the columns read) or "allgather".  poison (tests): NaN every
-    column this rank neither owns nor reads, proving the halo is sufficient.
+    rank's device, full arrays on every rank (in/out).  `shard` owns [K0, K1) of [s0, s1)
+    (HipShard, or any object with the same improve / howard / reldiff / ghost / hints methods
+    and a kp_idx table).  exchange: "halo" (point-to-point, only the columns read; `depth`
+    sweeps per exchange, HowardSweeps) or "allgather".  poison (tests): NaN every column this
+    rank neither owns nor reads, proving the exchanges are sufficient.
     Returns (iters, rel_diff)."""
     import torch
     import torch.distributed as dist
     V = value
     nk = V.shape[-1]
-    own = torch.tensor(owned_columns(nK, rank, world), device=V.device)
-    halo = None
     if world > 1:
         dist.barrier()   # first collective on every rank before any point-to-point
-        if exchange == "halo":
-            plan = halo_plan(shard.kp_idx, nK, world)
-            halo = HaloExchange(plan, rank, world, V.device, V.shape[2], V.dtype)
-            if poison:
-                keep = set(owned_columns(nK, rank, world)) | \
-                    {c for p in range(world) for c in plan[rank][p]}
-                flat = V.view(-1, nk)
-                for c in range(4 * nK):
-                    if c not in keep:
-                        flat[c] = math.nan
-        elif exchange != "allgather":
-            raise ValueError(f"exchange must be 'halo' or 'allgather', not {exchange!r}")
+    hs = HowardSweeps(shard, nK, rank, world, V, depth=depth, exchange=exchange)
+    if poison and world > 1 and exchange == "halo":
+        keep = hs.read_columns()
+        flat = V.view(-1, nk)
+        kkeep, kflat = hs.kopt_columns(), k_opt.view(-1, nk)
+        for c in range(4 * nK):
+            if c not in keep:
+                flat[c] = math.nan
+            if c not in kkeep:
+                kflat[c] = math.nan
     V2 = V.clone()
     rel, it = math.nan, 0
-    for it in range(1, max_vfi + 1):
-        Vold = V.clone()                                   # value_old = value (:145)
-        if (it - 1) % 5 == 0:                              # policy improvement (:148-168)
-            shard.improve(V, k_opt)
-        for _ in range(howard_steps):                      # Jacobi Howard sweeps (:172-192)
-            shard.howard(V, k_opt, V2)
-            if halo is None:  # V2 holds the shard's new nodes; carry the rest over, then gather
-                fresh = V2.view(-1, nk).index_select(0, own)
-                V2.copy_(V)
-                V2.view(-1, nk).index_copy_(0, own, fresh)
-            V, V2 = V2, V
-            if halo is not None:
-                halo(V)
-            elif world > 1:
-                _exchange(V, rank, world, nK)
-        rel = shard.reldiff(V, Vold)                       # :195
-        if world > 1:
-            rel = _allreduce_max(rel, V.device)
-        if rel < tol:
-            break
+    try:
+        for it in range(1, max_vfi + 1):
+            Vold = V.clone()                                   # value_old = value (:145)
+            if (it - 1) % 5 == 0:                              # policy improvement (:148-168)
+                hs.improve(V, k_opt)
+            V, V2 = hs.run(V, V2, k_opt, howard_steps)         # Jacobi Howard sweeps (:172-192)
+            rel = shard.reldiff(V, Vold)                       # :195
+            if world > 1:
+                rel = _allreduce_max(rel, V.device)
+            if rel < tol:
+                break
+    finally:
+        hs.close()
     if world > 1:                                          # every rank leaves with all of both
         _exchange(k_opt, rank, world, nK)
-        if halo is not None:
+        if exchange == "halo":
             _exchange(V, rank, world, nK)
     if V is not value:
         value.copy_(V)

@@ -153,6 +153,8 @@ def main():
     ap.add_argument("--no-solve", action="store_true", help="skip the solve-to-tol leg")
     ap.add_argument("--no-ks", action="store_true", help="skip the sharded Krusell-Smith leg")
     ap.add_argument("--no-panel", action="store_true", help="skip the KS panel (F2/F3) leg")
+    ap.add_argument("--ks-depth", type=int, default=None,
+                    help="KS Howard sweeps per halo exchange (default 4 on >1 rank)")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the labour/EGM/batch legs (D4, D5 per-GPU)")
     args = ap.parse_args()
@@ -253,7 +255,9 @@ def main():
     legs = {}
     if not args.no_ks:   # BASELINE configs[4]: KS VFI sharded over the same ranks (strong)
         import bench_ks
-        legs["ks_sharded"] = bench_ks.ks_leg(pkg, world, rank, dev)
+        legs["ks_sharded"] = bench_ks.ks_leg(pkg, world, rank, dev, depth=args.ks_depth)
+        if world == 1 and not args.no_extra:  # compute side of the N = 8 schedule, on this GPU
+            legs["ks_sharded"]["ghost_model"] = bench_ks.ghost_model(pkg, dev)
     if not args.no_ge:   # BASELINE configs[3]: multisection GE over the same ranks
         legs["ge_batch"] = BL.ge_batch_leg(pkg, world, rank, dev)
 

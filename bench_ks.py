@@ -23,42 +23,28 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 
-def ks_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, exchange="halo", reps=3):
+def ks_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, exchange="halo", reps=3,
+           depth=None):
     """Time one VFI iteration of the sharded solve (policy improvement + `howard` Jacobi
     sweeps with their exchanges, Krusell_Smith_VFI.m:148-192) at k = nk, K = nK, S = 4, max
-    over ranks, median of `reps`.  Every rank must call it (collectives inside)."""
+    over ranks, median of `reps`.  depth: Howard sweeps per exchange (ks_dist.HowardSweeps;
+    default 4 on more than one rank).  Every rank must call it (collectives inside)."""
     import numpy as np
     import torch
     import torch.distributed as dist
     kd = pkg.ks_dist
+    if depth is None:
+        depth = 4 if world > 1 else 1
     kg, Kg, P, V0 = pkg.calibration.krusell_smith(k_size=nk, K_size=nK)
     B = np.array([0.1, 0.97, 0.08, 0.975])
     K0, K1, s0, s1 = kd.shard_slices(nK, rank, world)
     sh = kd.HipShard(kg, Kg, B, P, pkg.ks_params(), K0, K1, s0, s1)
-    own = torch.tensor(kd.owned_columns(nK, rank, world), device=dev)
     V = torch.as_tensor(np.ascontiguousarray(V0.transpose(2, 1, 0)), device=dev)
     V2 = V.clone()
     ko = torch.ones_like(V)
-    halo = None
     if world > 1:
         dist.barrier()
-        if exchange == "halo":
-            halo = kd.HaloExchange(kd.halo_plan(sh.kp_idx, nK, world), rank, world, dev, nk,
-                                   V.dtype)
-
-    def sweeps(n):
-        nonlocal V, V2
-        for _ in range(n):
-            sh.howard(V, ko, V2)
-            if halo is None and world > 1:
-                fresh = V2.view(-1, nk).index_select(0, own)
-                V2.copy_(V)
-                V2.view(-1, nk).index_copy_(0, own, fresh)
-            V, V2 = V2, V
-            if halo is not None:
-                halo(V)
-            elif world > 1:
-                kd._exchange(V, rank, world, nK)
+    hs = kd.HowardSweeps(sh, nK, rank, world, V, depth=depth, exchange=exchange)
 
     def sync():
         torch.cuda.synchronize()
@@ -66,16 +52,16 @@ def ks_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, exchange="halo", r
             dist.barrier()
         torch.cuda.synchronize()
 
-    sh.improve(V, ko)  # warm-up (kernels, caches, communicators)
-    sweeps(2)
+    hs.improve(V, ko)  # warm-up (kernels, caches, communicators)
+    V, V2 = hs.run(V, V2, ko, 2 * hs.depth)
     samples = []
     for _ in range(reps):
         sync()
         t0 = time.perf_counter()
-        sh.improve(V, ko)
+        hs.improve(V, ko)
         sync()
         t1 = time.perf_counter()
-        sweeps(howard)
+        V, V2 = hs.run(V, V2, ko, howard)
         sync()
         t2 = time.perf_counter()
         samples.append((t1 - t0, t2 - t1))
@@ -86,7 +72,10 @@ def ks_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, exchange="halo", r
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ti, th = float(t[0]), float(t[1])
     nodes = nk * nK * 4
-    cols = halo.columns if halo is not None else (4 * nK - len(own) if world > 1 else 0)
+    cols = hs.halo.columns if hs.halo is not None else 0
+    gcols = hs.blocks[hs.depth].columns if hs.depth > 1 else cols
+    ghost = [(r[1] - r[0]) * (r[3] - r[2]) for r in hs.rects]
+    hs.close()
     sh.close()
     # Algorithmic bytes per node and Howard sweep (each array touched once): the slope rebuild
     # reads V and writes dV (16 B); the sweep reads k_opt and the segment hint (12 B), the V/dV
@@ -107,8 +96,61 @@ def ks_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, exchange="halo", r
                         f"configs[4] scaling size), ALM B={[float(b) for b in B]}, one VFI "
                         f"iteration = improvement + {howard} Howard sweeps, median of {reps}",
             "parallelism": f"(K, Z) shards over {world} ranks (rank 0: K [{K0}, {K1}), s "
-                           f"[{s0}, {s1})), {exchange} exchange per Howard sweep (rank 0 "
-                           f"receives {cols} (s, K) columns of {nk} values)"}
+                           f"[{s0}, {s1})), {exchange} exchange "
+                           + (f"every {hs.depth} Howard sweeps (ghost rectangles of rank 0: "
+                              f"{ghost} columns; {gcols} columns received per block)"
+                              if hs.depth > 1 else
+                              f"per Howard sweep (rank 0 receives {cols} (s, K) columns of "
+                              f"{nk} values)")}
+
+
+def ghost_model(pkg, dev, world=8, nk=32768, nK=64, depths=(1, 2, 3, 4, 6, 8), sweeps=24):
+    """Compute side of the communication-avoiding schedule on ONE GPU: for each emulated rank
+    of `world` (K-range shards of the scaling grid), the time of `sweeps` Howard sweeps run as
+    blocks of `depth` (ghost rectangles R_{L-1} .. R_0, ks_dist.HowardSweeps) without the
+    exchanges — what each rank's GPU does between exchanges at N = world.  Returns, per depth,
+    the slowest emulated rank's ms per sweep."""
+    import numpy as np
+    import torch
+    kd = pkg.ks_dist
+    kg, Kg, P, V0 = pkg.calibration.krusell_smith(k_size=nk, K_size=nK)
+    B = np.array([0.1, 0.97, 0.08, 0.975])
+    V = torch.as_tensor(np.ascontiguousarray(V0.transpose(2, 1, 0)), device=dev)
+    V2 = V.clone()
+    ko = torch.ones_like(V)
+    out = {}
+    for rank in range(world):
+        K0, K1, s0, s1 = kd.shard_slices(nK, rank, world)
+        sh = kd.HipShard(kg, Kg, B, P, pkg.ks_params(), K0, K1, s0, s1)
+        sh.improve(V, ko)
+        for d in depths:
+            rects = kd.ghost_rects(sh.kp_idx, nK, K0, K1, s0, s1, d)
+            shards = [sh] + [sh.ghost(*r) for r in rects[1:d]]
+            shards[-1].hints(ko)
+
+            def run(n):
+                nonlocal V, V2
+                done = 0
+                while done < n:
+                    L = min(d, n - done)
+                    for i in range(1, L + 1):
+                        shards[L - i].howard(V, ko, V2)
+                        V, V2 = V2, V
+                    done += L
+            run(d)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            run(sweeps)
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) / sweeps * 1e3
+            out[d] = max(out.get(d, 0.0), ms)
+            for g in shards[1:]:
+                g.close()
+            sh._ghosts.clear()
+        sh.close()
+    return {"world": world, "sweeps": sweeps,
+            "ms_per_sweep_by_depth": {str(d): out[d] for d in depths},
+            "note": "slowest emulated rank, compute only (no exchanges): ghost overhead vs depth"}
 
 
 def main():
@@ -117,6 +159,9 @@ def main():
     ap.add_argument("--nK", type=int, default=64)
     ap.add_argument("--howard", type=int, default=50)
     ap.add_argument("--exchange", default="halo", choices=("halo", "allgather"))
+    ap.add_argument("--depth", type=int, default=None, help="Howard sweeps per exchange")
+    ap.add_argument("--ghost-model", action="store_true",
+                    help="one GPU: compute time per sweep vs depth for emulated 8-rank shards")
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -128,8 +173,11 @@ def main():
         dist.init_process_group("nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    out = ks_leg(bench.load_pkg(), world, rank, dev, args.nk, args.nK, args.howard,
-                 args.exchange)
+    if args.ghost_model:
+        out = ghost_model(bench.load_pkg(), dev, nk=args.nk, nK=args.nK)
+    else:
+        out = ks_leg(bench.load_pkg(), world, rank, dev, args.nk, args.nK, args.howard,
+                     args.exchange, depth=args.depth)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -326,6 +326,13 @@ int ks_dev_howard(ks_dev* h, const double* V, const double* kopt, double* Vout, 
 /* :195 max relative change over the shard, NaN ignored; out = device uint64[2]
  * {IEEE bits of the max, nonzero if any node was not NaN} */
 int ks_dev_reldiff(ks_dev* h, const double* V, const double* Vold, void* out, void* stream);
+/* Ghost shards (ks_dist.py exchanges halos every m Howard sweeps and sweeps a widening
+ * rectangle of other ranks' columns redundantly in between — same kernels, so still bit-exact):
+ * h uses owner's segment-hint array (owner must outlive h; same grid and device), and
+ * ks_dev_hints recomputes the hints of h's nodes from kopt (for k_opt received from other
+ * ranks).  Hints only short-cut Howard's segment search: results never depend on them. */
+int ks_dev_share_hints(ks_dev* h, ks_dev* owner);
+int ks_dev_hints(ks_dev* h, const double* kopt, void* stream);
 /* Host-only (no device): the forecast column K'_idx(s, K) that bellman_value reads for every
  * node of slice (K, s) (Krusell_Smith_VFI.m:335-343, clamp + nearest index), 0-based,
  * out[s * nK + K].  The sharded driver builds its halo exchange from it: a rank needs, besides

@@ -47,6 +47,17 @@ class OracleShard:
         vt = torch.from_numpy(np.ascontiguousarray(Vn.transpose(2, 1, 0)))
         Vout[self.s0:self.s1, self.K0:self.K1, :] = vt[self.s0:self.s1, self.K0:self.K1, :]
 
+    def ghost(self, K0, K1, s0, s1):
+        g = OracleShard(self.p, self.kg, self.Kg, self.B, self.P, K0, K1, s0, s1)
+        g.kp_idx = self.kp_idx
+        return g
+
+    def hints(self, kopt):
+        pass
+
+    def close(self):
+        pass
+
     def reldiff(self, V, Vold):
         a = V[self.s0:self.s1, self.K0:self.K1, :].numpy()
         b = Vold[self.s0:self.s1, self.K0:self.K1, :].numpy()
@@ -54,17 +65,22 @@ class OracleShard:
         return float(np.nanmax(d)) if not np.all(np.isnan(d)) else math.nan
 
 
-def _setup(nK=4):
+# ALM whose forecast index moves by one to three K points: up below K* = 42.5 and down above it
+# in one aggregate state, down everywhere in the other, so shards read their neighbours' columns
+B_MIXED = np.array([0.6, 0.84, 0.1, 0.95])
+
+
+def _setup(nK=4, B_alm=None):
     from oracle import corc
     from oracle import np_oracle as no
     p, kg, Kg, P, V0, B = no.ks_setup(k_size=40, K_size=nK)
-    B = np.array([0.1, 0.97, 0.08, 0.975])  # non-identity ALM: shards read remote columns
+    B = np.array([0.1, 0.97, 0.08, 0.975]) if B_alm is None else np.asarray(B_alm)
     cp = corc.ks_params(**{k: p[k] for k in ("beta", "alpha", "delta", "k_min", "k_max", "ug",
                                               "ub", "l_bar", "mu", "z_grid", "eps_grid")})
     return cp, kg, Kg, P, V0, B
 
 
-def _worker(rank, world, port, outdir, nK, exchange="halo"):
+def _worker(rank, world, port, outdir, nK, exchange="halo", depth=1, howard=3, B_alm=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     from oracle import corc
     corc.num_threads(1)
@@ -72,15 +88,17 @@ def _worker(rank, world, port, outdir, nK, exchange="halo"):
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
     kd = _pkg().ks_dist
-    cp, kg, Kg, P, V0, B = _setup(nK)
+    cp, kg, Kg, P, V0, B = _setup(nK, B_alm)
     K0, K1, s0, s1 = kd.shard_slices(len(Kg), rank, world)
     V = torch.from_numpy(np.ascontiguousarray(V0.transpose(2, 1, 0)))
     ko = torch.ones_like(V)
     sh = OracleShard(cp, kg, Kg, B, P, K0, K1, s0, s1)
     sh.kp_idx = kd.forecast_index(Kg, B, _pkg().ks_params())  # host-only C ABI call
-    it, rel = kd.ks_vfi_solve_dist(V, ko, sh, len(Kg), howard_steps=3, tol=1e-6, max_vfi=6,
-                                   rank=rank, world=world, exchange=exchange,
-                                   poison=(exchange == "halo"))
+    if depth > 1 or B_alm is not None:  # the test's geometry must need remote columns
+        assert any(c for row in kd.halo_plan(sh.kp_idx, len(Kg), world) for c in row)
+    it, rel = kd.ks_vfi_solve_dist(V, ko, sh, len(Kg), howard_steps=howard, tol=1e-6,
+                                   max_vfi=6, rank=rank, world=world, exchange=exchange,
+                                   poison=(exchange == "halo"), depth=depth)
     np.save(Path(outdir, f"V{rank}.npy"), V.numpy())
     np.save(Path(outdir, f"k{rank}.npy"), ko.numpy())
     Path(outdir, f"m{rank}.json").write_text(json.dumps(dict(it=it, rel=rel)))
@@ -106,6 +124,47 @@ def test_gloo_sharded_equals_unsharded(tmp_path, world, nK, exchange):
         assert np.array_equal(np.load(Path(tmp_path, f"k{rank}.npy")), kr)
         m = json.loads(Path(tmp_path, f"m{rank}.json").read_text())
         assert m["it"] == R["iters"]
+
+
+@pytest.mark.parametrize("world,nK,depth,howard", [(2, 8, 1, 3), (3, 12, 1, 3), (2, 8, 2, 3),
+                                                   (3, 12, 3, 7), (4, 12, 4, 5), (5, 12, 2, 5),
+                                                   (2, 6, 6, 4), (8, 6, 3, 4)])
+def test_gloo_ghost_sweeps_equal_unsharded(tmp_path, world, nK, depth, howard):
+    """Communication-avoiding Howard (HowardSweeps depth > 1: one exchange per block of `depth`
+    sweeps, ghost rectangles swept redundantly) — bit-identical to the unsharded solve, with
+    every value column outside own ∪ R_depth and every k_opt column outside own ∪ R_{depth-1}
+    NaN-poisoned.  Blocks that do not divide the sweep count (7 = 3 + 3 + 1) and depth larger
+    than the sweep count are included; (8, 6) uses (K, Z) slices; depth 1 is the per-sweep halo on
+    the same geometry."""
+    import torch.multiprocessing as mp
+    from oracle import corc
+    port = 31200 + (os.getpid() % 1500) + 11 * world + 3 * nK + depth
+    mp.spawn(_worker, args=(world, port, str(tmp_path), nK, "halo", depth, howard, B_MIXED),
+             nprocs=world, join=True)
+    cp, kg, Kg, P, V0, B = _setup(nK, B_MIXED)
+    R = corc.ks_vfi_solve(cp, kg, Kg, V0, np.ones_like(V0), B, P, howard=howard, tol=1e-6,
+                          max_vfi=6)
+    Vr = np.ascontiguousarray(R["value"].transpose(2, 1, 0))
+    kr = np.ascontiguousarray(R["k_opt"].transpose(2, 1, 0))
+    for rank in range(world):
+        assert np.array_equal(np.load(Path(tmp_path, f"V{rank}.npy")), Vr)
+        assert np.array_equal(np.load(Path(tmp_path, f"k{rank}.npy")), kr)
+        assert json.loads(Path(tmp_path, f"m{rank}.json").read_text())["it"] == R["iters"]
+
+
+def test_ghost_rects_cover_reads():
+    """R_j holds R_{j-1} and every column R_{j-1}'s nodes read (the closure the schedule
+    needs), at the scaling grid's forecast map over 8 ranks."""
+    kd = _pkg().ks_dist
+    from oracle import np_oracle as no
+    p, kg, Kg, P, V0, B = no.ks_setup(k_size=8, K_size=64)
+    kp = kd.forecast_index(Kg, np.array([0.1, 0.97, 0.08, 0.975]), _pkg().ks_params())
+    for rank in range(8):
+        R = kd.ghost_rects(kp, 64, *kd.shard_slices(64, rank, 8), 6)
+        for j in range(1, 7):
+            prev, cur = set(kd.rect_columns(R[j - 1], 64)), set(kd.rect_columns(R[j], 64))
+            reads = {sn * 64 + int(kp[c // 64, c % 64]) for c in prev for sn in range(4)}
+            assert prev <= cur and reads <= cur
 
 
 def test_shard_ranges_cover():

@@ -20,32 +20,39 @@ def _pkg():
     return load_pkg()
 
 
-def _setup(nK):
+# forecast index moving by one to three K points (tests/test_ks_dist_cpu.py B_MIXED): shards
+# read their neighbours' columns and ghost rectangles grow with depth
+B_MIXED = np.array([0.6, 0.84, 0.1, 0.95])
+
+
+def _setup(nK, k_size=100):
     from oracle import np_oracle as no
-    p, kg, Kg, P, V0, B = no.ks_setup(k_size=100, K_size=nK)
+    p, kg, Kg, P, V0, B = no.ks_setup(k_size=k_size, K_size=nK)
     return kg, Kg, P, V0
 
 
-def _run(rank, world, nK, steps=8, vfi=7, exchange="halo"):
+def _run(rank, world, nK, steps=8, vfi=7, exchange="halo", depth=1, B_alm=B_ALM):
     import torch
     pkg = _pkg()
     kg, Kg, P, V0 = _setup(nK)
     prm = pkg.ks_params()
     K0, K1, s0, s1 = pkg.ks_dist.shard_slices(nK, rank, world)
-    sh = pkg.ks_dist.HipShard(kg, Kg, B_ALM, P, prm, K0, K1, s0, s1)
+    sh = pkg.ks_dist.HipShard(kg, Kg, B_alm, P, prm, K0, K1, s0, s1)
     V = torch.as_tensor(np.ascontiguousarray(V0.transpose(2, 1, 0)), device="cuda:0")
     ko = torch.ones_like(V)
     it, rel = pkg.ks_dist.ks_vfi_solve_dist(V, ko, sh, nK, howard_steps=steps, tol=1e-6,
                                             max_vfi=vfi, rank=rank, world=world,
-                                            exchange=exchange, poison=(exchange == "halo"))
+                                            exchange=exchange, poison=(exchange == "halo"),
+                                            depth=depth)
     torch.cuda.synchronize()
+    sh.close()
     return V.cpu().numpy(), ko.cpu().numpy(), it, rel
 
 
-def _reference(nK, steps=8, vfi=7):
+def _reference(nK, steps=8, vfi=7, B_alm=B_ALM):
     pkg = _pkg()
     kg, Kg, P, V0 = _setup(nK)
-    R = pkg.ks_vfi_solve(V0, np.ones_like(V0), kg, Kg, B_ALM, P, pkg.ks_params(),
+    R = pkg.ks_vfi_solve(V0, np.ones_like(V0), kg, Kg, B_alm, P, pkg.ks_params(),
                          howard_steps=steps, tol=1e-6, max_vfi=vfi)
     return (np.ascontiguousarray(R["value"].transpose(2, 1, 0)),
             np.ascontiguousarray(R["k_opt"].transpose(2, 1, 0)), R["iters"], R["rel_diff"])
@@ -57,12 +64,12 @@ def test_one_rank_equals_single_device(pkg, gpu):
     assert it == itr and np.array_equal(V, Vr) and np.array_equal(ko, kr) and rel == relr
 
 
-def _worker(rank, world, port, outdir, nK, exchange="halo"):
+def _worker(rank, world, port, outdir, nK, exchange="halo", depth=1, B_alm=B_ALM):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                       HSA_ENABLE_IPC_MODE_LEGACY="0")
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    V, ko, it, rel = _run(rank, world, nK, exchange=exchange)
+    V, ko, it, rel = _run(rank, world, nK, exchange=exchange, depth=depth, B_alm=B_alm)
     np.save(Path(outdir, f"V{rank}.npy"), V)
     np.save(Path(outdir, f"k{rank}.npy"), ko)
     Path(outdir, f"m{rank}.json").write_text(json.dumps(dict(it=it, rel=rel)))
@@ -90,6 +97,24 @@ def test_kz_slices_on_one_card(pkg, gpu, tmp_path, world, nK, exchange):
     port = 29900 + (os.getpid() % 1000) + world + 10 * (exchange == "halo")
     mp.spawn(_worker, args=(world, port, str(tmp_path), nK, exchange), nprocs=world, join=True)
     Vr, kr, itr, relr = _reference(nK)
+    for rank in range(world):
+        assert np.array_equal(np.load(Path(tmp_path, f"V{rank}.npy")), Vr)
+        assert np.array_equal(np.load(Path(tmp_path, f"k{rank}.npy")), kr)
+        assert json.loads(Path(tmp_path, f"m{rank}.json").read_text())["it"] == itr
+
+
+@pytest.mark.parametrize("world,nK,depth", [(3, 12, 1), (3, 12, 3), (4, 12, 5), (6, 6, 4)])
+def test_ghost_sweeps_on_one_card(pkg, gpu, tmp_path, world, nK, depth):
+    """Communication-avoiding Howard sweeps (ks_dist.HowardSweeps, depth > 1): HIP ghost shards
+    (ks_dev_share_hints / ks_dev_hints) sweep other ranks' columns redundantly between
+    exchanges; every value column outside own ∪ R_depth and k_opt column outside
+    own ∪ R_{depth-1} is NaN-poisoned; results equal the single-device solve bit for bit
+    (8 sweeps per block schedule: 3 + 3 + 2, 5 + 3, 4 + 4; (6, 6) uses (K, Z) slices)."""
+    import torch.multiprocessing as mp
+    port = 30300 + (os.getpid() % 1000) + 13 * world + nK + depth
+    mp.spawn(_worker, args=(world, port, str(tmp_path), nK, "halo", depth, B_MIXED),
+             nprocs=world, join=True)
+    Vr, kr, itr, relr = _reference(nK, B_alm=B_MIXED)
     for rank in range(world):
         assert np.array_equal(np.load(Path(tmp_path, f"V{rank}.npy")), Vr)
         assert np.array_equal(np.load(Path(tmp_path, f"k{rank}.npy")), kr)
