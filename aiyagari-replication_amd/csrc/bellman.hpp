@@ -21,6 +21,9 @@ struct BellArgs {
     const double* L;    // labour grid (A3) or nullptr
     const double* dis;  // psi*L^(1+eta)/(1+eta) per level (A3) or nullptr
     const int* hint;    // nullable: last sweep's linear index (l + Nl*k)
+    int* mom;           // nullable [N][Na]: the argmax's shift in k over the last hinted sweep
+                        // (tree kernel: read for an extrapolated start, rewritten; heuristic
+                        // only — any start is a valid screening bar)
     // scratch
     double* EV;
     double2* T;

@@ -165,6 +165,7 @@ __device__ __forceinline__ BellArgs bell_cand(const BellArgs& A, int c) {
     B.best0 += o;
     B.idx0 += o;
     if (B.hint) B.hint += o;
+    if (B.mom) B.mom += o;
     B.v_new += o;
     B.idx += o;
     if (B.pk) B.pk += o;
@@ -828,8 +829,13 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
     }
 
     double x[R], best[R];
-    int idx[R];
+    int idx[R], hk0[R];
     bool okr[R], feas[R];
+    // momentum (variant bit 9 clear): the argmax's shift over the last hinted sweep, so the
+    // start-up also tries hint + shift — in the early sweeps of a solve the optimum drifts by
+    // tens of candidates per sweep and a climb from the stale hint costs a dependent round
+    // trip per step.  Only the screening bar depends on it, never the result.
+    int* __restrict__ mom = (A.variant & 512) ? nullptr : A.mom;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int j = jbase + r * 64 + lane;
@@ -838,11 +844,13 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
         x[r] = okr[r] ? (1 + A.r) * a[j] : 0.0;
         best[r] = __builtin_nan("");
         idx[r] = -1;
+        hk0[r] = -1;
         feas[r] = false;
         if (!okr[r]) continue;
         for (int l = 0; l < Nl; ++l) feas[r] = feas[r] || A.kf[l * nall + t] > 0;
         if (A.hint) {
             const int h = A.hint[t];
+            const int mv = (mom && h >= 0) ? max(-Na, min(Na, mom[t])) : 0;
             if (h >= 0) {
                 const int hl = h % Nl;
                 const int kf = A.kf[hl * nall + t];
@@ -859,8 +867,13 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
                     // (independent chains).  Indices are clamped into the feasible prefix; a
                     // repeated candidate merges as a no-op.
                     const int wn = 1 << ((A.variant >> 7) & 3);
+                    hk0[r] = hk;
+                    // the extrapolated start hm = hint + last shift and its two neighbours,
+                    // when that window does not touch the hint's own
+                    const int hm = min(max(hk + mv, 0), kf - 1);
+                    const bool usem = hm > hk + wn + 1 || hm < hk - wn - 1;
                     constexpr int WM = 8;
-                    double wa[2 * WM + 1], we[2 * WM + 1];
+                    double wa[2 * WM + 1], we[2 * WM + 1], ma[3], me[3];
 #pragma unroll
                     for (int d = -WM; d <= WM; ++d) {
                         if (d < -wn || d > wn) continue;  // wave-uniform
@@ -868,12 +881,28 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
                         wa[d + WM] = a[kc];
                         we[d + WM] = ev[kc];
                     }
+                    if (usem) {
+#pragma unroll
+                        for (int d = -1; d <= 1; ++d) {
+                            const int kc = min(max(hm + d, 0), kf - 1);
+                            ma[d + 1] = a[kc];
+                            me[d + 1] = ev[kc];
+                        }
+                    }
 #pragma unroll
                     for (int d = -WM; d <= WM; ++d) {
                         if (d < -wn || d > wn) continue;
                         const int kc = min(max(hk + d, 0), kf - 1);
                         lexi_take(bell_val<NP, LAB>(coh - wa[d + WM], we[d + WM], A.sigma, dis),
                                   hl + Nl * kc, best[r], idx[r]);
+                    }
+                    if (usem) {
+#pragma unroll
+                        for (int d = -1; d <= 1; ++d) {
+                            const int kc = min(max(hm + d, 0), kf - 1);
+                            lexi_take(bell_val<NP, LAB>(coh - ma[d + 1], me[d + 1], A.sigma, dis),
+                                      hl + Nl * kc, best[r], idx[r]);
+                        }
                     }
                     // Climb: when the best of the window sits on its edge, the optimum has moved
                     // further (early sweeps; the sweep after a cold start moves it by thousands
@@ -883,7 +912,9 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
                     // the bar one passing candidate at a time.  Any candidate is a valid bar, so
                     // the result does not depend on it (the tree below still proves the maximum).
                     const int kb = idx[r] >= 0 ? idx[r] / Nl : hk;
-                    const int dir = kb >= hk + wn ? 1 : (kb <= hk - wn ? -1 : 0);
+                    int dir = kb >= hk + wn ? 1 : (kb <= hk - wn ? -1 : 0);
+                    if (usem && kb >= hm - 1 && kb <= hm + 1)  // best in the extrapolated window
+                        dir = kb == hm + 1 ? 1 : (kb == hm - 1 ? -1 : 0);
                     if (dir != 0 && !(A.variant & 32)) {
                         int k = kb, step = 2;
                         for (;;) {
@@ -1303,6 +1334,8 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
             if (LAB && A.pl) A.pl[t] = A.L[l];
         }
         A.v_new[t] = b;
+        if (mom && A.hint)  // this sweep's shift of the argmax, for the next sweep's start
+            mom[t] = (hk0[r] >= 0 && idx[r] >= 0) ? idx[r] / Nl - hk0[r] : 0;
         const double d = fabs(b - vo);
         if (d == d) {
             dmax = okd ? fmax(dmax, d) : d;

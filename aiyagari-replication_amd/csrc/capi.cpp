@@ -63,6 +63,10 @@ int ws_ensure_bell(aiy_ws* ws, size_t partial_slots) {
     AIY_TRY(dalloc(&ws->Dm512, (size_t)ws->N * ((ws->Na + 511) / 512)));
     AIY_TRY(dalloc(&ws->best0, n));
     AIY_TRY(dalloc(&ws->idx0, n));
+    if (!ws->mom) {
+        AIY_TRY(dalloc(&ws->mom, n));
+        AIY_HIP(hipMemset(ws->mom, 0, n * sizeof(int)));
+    }
     if (!ws->touched) {  // the merge kernel leaves touched = 0 and partial = -1 behind
         AIY_TRY(dalloc(&ws->touched, n));
         AIY_HIP(hipMemset(ws->touched, 0, n * sizeof(int)));
@@ -155,6 +159,7 @@ static int bell_args(aiy_ws* ws, const BellCall& c, BellArgs& A, hipStream_t st)
     A.nb512 = (int)((ws->Na + 511) / 512);
     A.best0 = ws->best0;
     A.idx0 = ws->idx0;
+    A.mom = ws->mom;
     A.partial = ws->partial;
     A.touched = ws->touched;
     A.hitcount = ws->count_hits ? ws->hitcount : nullptr;
@@ -488,6 +493,8 @@ int bell_solve_batch_dev(aiy_ws* ws, int64_t C, const double* r, const double* w
         AIY_TRY(dalloc(&ws->bDm512, (size_t)C * ws->N * nb512));
         AIY_TRY(dalloc(&ws->bbest0, C * n));
         AIY_TRY(dalloc(&ws->bidx0, C * n));
+        AIY_TRY(dalloc(&ws->bmom, C * n));
+        AIY_HIP(hipMemset(ws->bmom, 0, C * n * sizeof(int)));
         AIY_TRY(dalloc(&ws->bkf, C * n));
         AIY_TRY(dalloc(&ws->bstop, (size_t)C));
         AIY_TRY(dalloc(&ws->bslots, (size_t)C * 2 * 2 * kDiffSlots));
@@ -508,7 +515,7 @@ int bell_solve_batch_dev(aiy_ws* ws, int64_t C, const double* r, const double* w
     A.beta = beta; A.sigma = sigma; A.a = a; A.s = s; A.P = P;
     A.EV = ws->bEV; A.Dt = ws->bDt; A.Dm8 = ws->bDm8; A.Dm512 = ws->bDm512;
     A.nb = (int)((ws->Na + 63) / 64); A.nb8 = nb8; A.nb512 = nb512;
-    A.tree = true; A.best0 = ws->bbest0; A.idx0 = ws->bidx0; A.kf = ws->bkf;
+    A.tree = true; A.best0 = ws->bbest0; A.idx0 = ws->bidx0; A.kf = ws->bkf; A.mom = ws->bmom;
     A.hitcount = ws->count_hits ? ws->hitcount : nullptr;
     A.idx = idx; A.pk = pk; A.pc = pc; A.diff = ws->bslots;
     A.C = (int)C; A.rv = ws->brw; A.wv = ws->brw + C; A.stop = ws->bstop;
@@ -678,7 +685,7 @@ int aiy_ws_invalidate(aiy_ws* ws) {
 
 int aiy_ws_set_variant(aiy_ws* ws, int variant) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
-    if (variant < -1 || variant > 511) return fail(AIY_BAD_ARG, "variant in [-1, 511]");
+    if (variant < -1 || variant > 1023) return fail(AIY_BAD_ARG, "variant in [-1, 1023]");
     ws->variant = variant;
     return AIY_OK;
 }

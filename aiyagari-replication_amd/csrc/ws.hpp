@@ -24,6 +24,7 @@ struct aiy_ws {
     double* Dm512 = nullptr;
     double* best0 = nullptr;
     int* idx0 = nullptr;
+    int* mom = nullptr;  // [N][Na] last sweep's argmax shift (tree kernel start-up heuristic)
     int* touched = nullptr;
     double* dis = nullptr;
     int* kf = nullptr;
@@ -89,6 +90,7 @@ struct aiy_ws {
     double* bDm512 = nullptr;
     double* bbest0 = nullptr;
     int* bidx0 = nullptr;
+    int* bmom = nullptr;
     int* bkf = nullptr;
     int* bstop = nullptr;                  // device [bC]
     unsigned long long* bslots = nullptr;  // device [bC][2][2*kDiffSlots]
@@ -96,13 +98,13 @@ struct aiy_ws {
     int* hstop = nullptr;                  // pinned [bC]
     unsigned long long* hslots = nullptr;  // pinned [bC][2*kDiffSlots]
     void free_batch() {
-        void* ps[] = {bEV, bDt, bDm8, bDm512, bbest0, bidx0, bkf, bstop, bslots, brw};
+        void* ps[] = {bEV, bDt, bDm8, bDm512, bbest0, bidx0, bmom, bkf, bstop, bslots, brw};
         for (void* p : ps)
             if (p) (void)hipFree(p);
         if (hstop) (void)hipHostFree(hstop);
         if (hslots) (void)hipHostFree(hslots);
         bEV = bDt = bDm8 = bDm512 = bbest0 = brw = nullptr;
-        bidx0 = bkf = bstop = nullptr;
+        bidx0 = bkf = bstop = bmom = nullptr;
         bslots = nullptr;
         hstop = nullptr;
         hslots = nullptr;
@@ -124,7 +126,7 @@ struct aiy_ws {
         spec_hdiff = nullptr; spec_n = 0;
     }
     void free_all() {
-        void* ps[] = {EV, T, T32, Dm, Dm8, Dt, Dm512, touched, best0, idx0, dis, kf, partial, diff, hitcount, trace, g0, g1, g2, gi,
+        void* ps[] = {EV, T, T32, Dm, Dm8, Dt, Dm512, touched, best0, idx0, mom, dis, kf, partial, diff, hitcount, trace, g0, g1, g2, gi,
                       d_key, d_head, d_wr, d_mass, d_part, pers};
         for (void* p : ps)
             if (p) (void)hipFree(p);
@@ -134,7 +136,7 @@ struct aiy_ws {
         if (hdiff) (void)hipHostFree(hdiff);
         EV = nullptr; T = nullptr; T32 = nullptr; Dm = nullptr; Dm8 = nullptr; Dt = nullptr; Dm512 = nullptr; touched = nullptr; best0 = nullptr; dis = nullptr; kf = nullptr; kf_cap = 0;
         kf_ok = false;
-        idx0 = nullptr; partial = nullptr; diff = nullptr; hitcount = nullptr; trace = nullptr; trace_cap = 0; hdiff = nullptr;
+        idx0 = nullptr; mom = nullptr; partial = nullptr; diff = nullptr; hitcount = nullptr; trace = nullptr; trace_cap = 0; hdiff = nullptr;
         g0 = g1 = g2 = nullptr; gi = nullptr; pers = nullptr;
         d_key = d_head = nullptr; d_wr = d_mass = d_part = nullptr;
         partial_cap = 0;

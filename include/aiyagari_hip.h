@@ -247,7 +247,9 @@ int aiy_ws_set_persistent(aiy_ws* ws, int persistent);
  * per tile, bit 4 = XCD-aware tile order.  bit 3 set: the chunked screen + merge, with
  * bit 0 = 4 states per lane (else 2), bit 1 = registers capped for 8 waves per SIMD, bit 2 =
  * fp64-only screen (else the packed fp32 pre-screen with directed-rounding bounds first).
- * -1 (default): chosen by size — 2 cooperating waves per tile for Na <= 4096, else 0. */
+ * Tree screen extras: bit 5 = no hill-climb from the hint, bits 7-8 = hint window half-width
+ * 1, 2, 4 or 8, bit 9 = no extrapolated (hint + last shift) start, bit 6 = 4 lanes per state.
+ * -1 (default): chosen by size — 2 cooperating waves per tile for Na <= 4096, else 16. */
 int aiy_ws_set_variant(aiy_ws* ws, int variant);
 
 /* A1 on device.  hint (nullable, [N][Na] int32 0-based) = previous sweep's argmax; the result
