@@ -133,6 +133,14 @@ __device__ __forceinline__ bool lexi_take(double val, int q, double& best, int& 
     return false;
 }
 
+// the same rule without branches (selects only), so that independent evaluations ahead of a
+// run of merges stay in one basic block and their dependency chains interleave
+__device__ __forceinline__ void lexi_take_sel(double val, int q, double& best, int& idx) {
+    const bool take = (val == val) & ((idx < 0) | (val > best) | ((val == best) & (q < idx)));
+    best = take ? val : best;
+    idx = take ? q : idx;
+}
+
 // screening bar of (best, dis_l):  n·(best + dis) − τ·n·(|best| + |dis|)
 __device__ __forceinline__ double screen_B(double best, int idx, double dis, int np) {
     if (idx < 0) return -__builtin_inf();
@@ -1861,24 +1869,60 @@ __global__ void bell_merge_kernel(BellArgs A, int use_partial, int nlb, int nchu
 
 // ------------------------------------------------------------------------------ plain
 template <int NP, bool LAB>
-__global__ void bell_plain_kernel(BellArgs A) {
-    int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= A.N * A.Na) return;
-    if (A.idx0[t] == -2) return;
+__global__ __launch_bounds__(256) void bell_plain_kernel(BellArgs A) {
+    // The exhaustive scan (mode 2): every feasible candidate evaluated exactly, in the literal
+    // MATLAB order, merged with the (max value, first column-major index) rule.  A block owns
+    // 64 consecutive states of one row (one per lane) and its four waves split the candidate
+    // range into quarters (four times the waves of one wave per tile: the scan is bound by
+    // dependent fp64 divisions, so it needs the occupancy); the candidate index is
+    // wave-uniform, so a_k and EV_ik arrive by scalar loads, and each lane evaluates 8
+    // candidates per step as independent chains before merging them.  The quarters' partial
+    // maxima are merged through LDS; the merge rule is order-independent, so the result is the
+    // sequential scan's bit for bit.
+    constexpr int W = 4, U = 8;
+    __shared__ double s_best[W][64];
+    __shared__ int s_idx[W][64];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int Na = A.Na, Nl = A.Nl;
-    int i = t / Na, j = t - i * Na;
+    const int i = blockIdx.y;
+    const int j = blockIdx.x * 64 + lane;
+    const bool okj = j < Na;
+    const size_t t = (size_t)i * Na + (okj ? j : 0);
+    const bool live = okj && A.idx0[t] != -2;
     const double* __restrict__ a = A.a;
     const double* __restrict__ ev = A.EV + (size_t)i * Na;
-    double x = (1 + A.r) * a[j], y = A.w * A.s[i];
+    const double x = okj ? (1 + A.r) * a[j] : 0.0, y = A.w * A.s[i];
     double best = __builtin_nan("");
     int idx = -1;
     for (int l = 0; l < Nl; ++l) {
-        double coh = cash<LAB>(x, y, LAB ? A.L[l] : 1.0);
-        double dis = LAB ? A.dis[l] : 0.0;
-        int kf = A.kf[(size_t)l * A.N * Na + t];
-        for (int k = 0; k < kf; ++k)
-            lexi_take(bell_val<NP, LAB>(coh - a[k], ev[k], A.sigma, dis), l + Nl * k, best, idx);
+        const double coh = cash<LAB>(x, y, LAB ? A.L[l] : 1.0);
+        const double dis = LAB ? A.dis[l] : 0.0;
+        const int kf = live ? A.kf[(size_t)l * A.N * Na + t] : 0;
+        int km = kf;
+        for (int off = 32; off > 0; off >>= 1) km = max(km, __shfl_xor(km, off));
+        const int kmax = __builtin_amdgcn_readfirstlane(km);
+        const int kc = (kmax + W * U - 1) / (W * U) * U;  // quarter length, a multiple of U
+        const int k_lo = wave * kc, k_hi = min(kmax, k_lo + kc);
+        for (int k = k_lo; k < k_hi; k += U) {
+            double v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int kk = min(k + u, Na - 1);
+                const double val = bell_val<NP, LAB>(coh - a[kk], ev[kk], A.sigma, dis);
+                v[u] = (k + u < kf) ? val : __builtin_nan("");
+            }
+            AIY_SCHED_BARRIER();
+#pragma unroll
+            for (int u = 0; u < U; ++u) lexi_take_sel(v[u], l + Nl * (k + u), best, idx);
+        }
     }
+    s_best[wave][lane] = best;
+    s_idx[wave][lane] = idx;
+    __syncthreads();
+    if (wave != 0 || !live) return;
+#pragma unroll
+    for (int w = 1; w < W; ++w) lexi_take(s_best[w][lane], s_idx[w][lane], best, idx);
     A.best0[t] = best;
     A.idx0[t] = idx;
 }
@@ -2032,7 +2076,7 @@ static void run_tree(const BellArgs& A, hipStream_t st) {
 }
 template <int NP, bool LAB>
 static void run_plain(const BellArgs& A, hipStream_t st) {
-    bell_plain_kernel<NP, LAB><<<cdiv(A.N * A.Na, 128), 128, 0, st>>>(A);
+    bell_plain_kernel<NP, LAB><<<dim3(cdiv(A.Na, 64), A.N), 256, 0, st>>>(A);
 }
 template <int NP, bool LAB>
 static void run_merge(const BellArgs& A, int use_partial, hipStream_t st) {

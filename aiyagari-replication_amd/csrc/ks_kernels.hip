@@ -159,23 +159,28 @@ __device__ __forceinline__ double howard_node(const KsArgs& A, const KsView& W, 
 }
 
 // ------------------------------------------------------------------------------ tiled
+// Column-shaped launches (x: k tile, y: column, grid-stride): a node's column and row come from
+// the block indices, not from integer divisions of a flat node index per thread.
+__device__ __forceinline__ int ks_tile_k() { return blockIdx.x * blockDim.x + threadIdx.x; }
+
 __global__ void ks_slopes_kernel(KsArgs A, const double* __restrict__ V, double* __restrict__ dV) {
-    int t = blockIdx.x * blockDim.x + threadIdx.x;
-    int n = A.nk * A.nK * 4;
-    if (t >= n) return;
-    int q = t % A.nk;
-    size_t col = (size_t)(t / A.nk) * A.nk;
-    dV[t] = pchip_slope(A.k_grid, V + col, A.nk, q);
+    const int q = ks_tile_k();
+    if (q >= A.nk) return;
+    for (int c = blockIdx.y; c < 4 * A.nK; c += gridDim.y) {
+        const size_t col = (size_t)c * A.nk;
+        dV[col + q] = pchip_slope(A.k_grid, V + col, A.nk, q);
+    }
 }
 
 // slopes for a list of columns only (the columns a shard reads)
 __global__ void ks_slopes_cols_kernel(KsArgs A, const int* __restrict__ cols, int ncols,
                                       const double* __restrict__ V, double* __restrict__ dV) {
-    int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= ncols * A.nk) return;
-    int q = t % A.nk;
-    size_t col = (size_t)cols[t / A.nk] * A.nk;
-    dV[col + q] = pchip_slope(A.k_grid, V + col, A.nk, q);
+    const int q = ks_tile_k();
+    if (q >= A.nk) return;
+    for (int c = blockIdx.y; c < ncols; c += gridDim.y) {
+        const size_t col = (size_t)cols[c] * A.nk;
+        dV[col + q] = pchip_slope(A.k_grid, V + col, A.nk, q);
+    }
 }
 
 __global__ void ks_improve_kernel(KsArgs A, const double* __restrict__ V,
@@ -193,14 +198,25 @@ __global__ void ks_improve_kernel(KsArgs A, const double* __restrict__ V,
         A.seg_hint[n] = seg_of_dev(A.k_grid, A.nk, fmax(fmin(kp, A.k_grid[A.nk - 1]), A.k_grid[0]));
 }
 
+// Howard sweep over the launch's columns: x = k tile, y = column of an s block (grid-stride),
+// z = s block; node n = col·nk + ki with col = s·nK + K — the values of howard_node exactly
 __global__ void ks_howard_kernel(KsArgs A, const double* __restrict__ V,
                                  const double* __restrict__ dV, const double* __restrict__ k_opt,
                                  double* __restrict__ Vn) {
-    int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= A.n_local) return;
-    int n = A.node0 + blockIdx.y * A.sstride + t;
+    const int ki = ks_tile_k();
+    if (ki >= A.nk) return;
+    const int nk = A.nk;
+    const int col0 = A.node0 / nk + (int)blockIdx.z * (A.sstride / nk);  // block-uniform
+    const int ncl = A.n_local / nk;
     KsView W{A.k_grid, V, dV};
-    Vn[n] = howard_node(A, W, n, k_opt[n]);
+    const double k = W.kg[ki];
+    for (int y = blockIdx.y; y < ncl; y += gridDim.y) {
+        const int col = col0 + y;
+        const int si = col / A.nK;
+        const int n = col * nk + ki;
+        const KsSlice sl = A.slice[col];
+        Vn[n] = ks_bellman_dev(A, W, sl, si, k, k_opt[n], A.seg_hint ? A.seg_hint[n] : -1);
+    }
 }
 
 // the segment hints of the shard's nodes from k_opt (what ks_improve_kernel stores), for nodes
@@ -350,16 +366,22 @@ int launch_ks_fused(const KsArgs& A, double* V, double* kopt, int* nfev, KsOut* 
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }
+// column-shaped grid: block of 64·ceil(nk / 64) <= 256 lanes along k, columns along y
+static dim3 ks_col_block(int nk) { return dim3(std::min(256, (nk + 63) / 64 * 64)); }
+static dim3 ks_col_grid(int nk, long long ncols, int nz = 1) {
+    const int bx = (int)ks_col_block(nk).x;
+    return dim3(cdiv(nk, bx), (unsigned)std::max<long long>(1, std::min<long long>(ncols, 65535)),
+                std::max(nz, 1));
+}
 int launch_ks_slopes(const KsArgs& A, const double* V, double* dV, hipStream_t st) {
-    int n = A.nk * A.nK * 4;
-    ks_slopes_kernel<<<cdiv(n, 256), 256, 0, st>>>(A, V, dV);
+    ks_slopes_kernel<<<ks_col_grid(A.nk, 4ll * A.nK), ks_col_block(A.nk), 0, st>>>(A, V, dV);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }
 int launch_ks_slopes_cols(const KsArgs& A, const int* cols, int ncols, const double* V,
                           double* dV, hipStream_t st) {
     if (ncols <= 0) return AIY_OK;
-    ks_slopes_cols_kernel<<<cdiv((long long)ncols * A.nk, 256), 256, 0, st>>>(A, cols, ncols, V, dV);
+    ks_slopes_cols_kernel<<<ks_col_grid(A.nk, ncols), ks_col_block(A.nk), 0, st>>>(A, cols, ncols, V, dV);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }
@@ -371,7 +393,10 @@ int launch_ks_improve(const KsArgs& A, const double* V, const double* dV, double
 }
 int launch_ks_howard(const KsArgs& A, const double* V, const double* dV, const double* kopt,
                      double* Vn, hipStream_t st) {
-    ks_howard_kernel<<<dim3(cdiv(A.n_local, 256), std::max(A.ns, 1)), 256, 0, st>>>(A, V, dV, kopt, Vn);
+    if (A.node0 % A.nk || A.n_local % A.nk || (A.ns > 1 && A.sstride % A.nk))
+        return fail(AIY_BAD_SHAPE, "Howard launch: node range must be whole columns");
+    ks_howard_kernel<<<ks_col_grid(A.nk, A.n_local / A.nk, A.ns), ks_col_block(A.nk), 0, st>>>(
+        A, V, dV, kopt, Vn);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }

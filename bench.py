@@ -247,6 +247,21 @@ def main():
     torch.cuda.synchronize()
     counters = ws.counters()
     ws.set_timing(False)
+    exh = None
+    if not args.no_extra and args.mode == 1 and world == 1:
+        # SURVEY D3's exhaustive kernel (mode 2: table + plain scan + merge), same sweeps
+        restore()
+        exh_ms = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            ws.vfi_sweep(v[cur], a_t, s_t, P_t, r, w, cal["beta"], cal["sigma"], v[1 - cur],
+                         idx, pk, pc, hint=None, mode=2)
+            torch.cuda.synchronize()
+            exh_ms.append((time.perf_counter() - t0) * 1e3)
+            cur = 1 - cur
+        exh = sorted(exh_ms)[1]
+        restore()
     if world > 1:
         tt = torch.tensor([dt, kern_avg_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -334,6 +349,18 @@ def main():
                                        "tools/pmc.sh + tools/pmc_summary.py, same sweeps)"},
         }
         out.update(legs)
+        if exh is not None:  # the plain exhaustive scan's own roofline (mode 2)
+            fl = FLOPS_PER_CANDIDATE * feas / (exh * 1e-3) / 1e12
+            out["exhaustive"] = {
+                "workload": f"one exhaustive sweep at Na={Na} (mode 2: table + plain scan + merge; "
+                            f"every feasible candidate evaluated exactly), median of 3",
+                "ms_per_sweep": exh, "evals_per_s": evals_per_sweep / (exh * 1e-3),
+                "roofline": {"bound": "valu", "achieved": fl, "peak": 78.6, "unit": "TFLOP/s",
+                             "frac": fl / 78.6,
+                             "basis": f"8 fp64 flops x {feas} feasible candidates per sweep "
+                                      f"(the division counted as one flop; infeasible c <= 0 "
+                                      f"candidates are NaN in the reference and skipped)"},
+                "tree_speedup": exh / (dt / args.steps * 1e3)}
         if not args.no_solve:
             out["solve_to_tol"] = solve_wall(pkg, ws, cal, r, w, a_t, s_t, P_t, dev)
         if world == 1 and not args.no_extra:
