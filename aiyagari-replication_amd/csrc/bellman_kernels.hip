@@ -1870,7 +1870,8 @@ __global__ void bell_merge_kernel(BellArgs A, int use_partial, int nlb, int nchu
 // ------------------------------------------------------------------------------ plain
 template <int NP, bool LAB>
 __global__ __launch_bounds__(256) void bell_plain_kernel(BellArgs A) {
-    // The exhaustive scan (mode 2): every feasible candidate evaluated exactly, in the literal
+    // The exhaustive scan (mode 2, or variant bit 10): every feasible candidate evaluated
+    // exactly, writing the sweep's outputs itself (no init or merge launch), in the literal
     // MATLAB order, merged with the (max value, first column-major index) rule.  A block owns
     // 64 consecutive states of one row (one per lane) and its four waves split the candidate
     // range into quarters (four times the waves of one wave per tile: the scan is bound by
@@ -1889,16 +1890,17 @@ __global__ __launch_bounds__(256) void bell_plain_kernel(BellArgs A) {
     const int j = blockIdx.x * 64 + lane;
     const bool okj = j < Na;
     const size_t t = (size_t)i * Na + (okj ? j : 0);
-    const bool live = okj && A.idx0[t] != -2;
     const double* __restrict__ a = A.a;
     const double* __restrict__ ev = A.EV + (size_t)i * Na;
     const double x = okj ? (1 + A.r) * a[j] : 0.0, y = A.w * A.s[i];
     double best = __builtin_nan("");
     int idx = -1;
+    bool anyfeas = false;
     for (int l = 0; l < Nl; ++l) {
         const double coh = cash<LAB>(x, y, LAB ? A.L[l] : 1.0);
         const double dis = LAB ? A.dis[l] : 0.0;
-        const int kf = live ? A.kf[(size_t)l * A.N * Na + t] : 0;
+        const int kf = okj ? A.kf[(size_t)l * A.N * Na + t] : 0;
+        anyfeas = anyfeas || kf > 0;
         int km = kf;
         for (int off = 32; off > 0; off >>= 1) km = max(km, __shfl_xor(km, off));
         const int kmax = __builtin_amdgcn_readfirstlane(km);
@@ -1920,11 +1922,33 @@ __global__ __launch_bounds__(256) void bell_plain_kernel(BellArgs A) {
     s_best[wave][lane] = best;
     s_idx[wave][lane] = idx;
     __syncthreads();
-    if (wave != 0 || !live) return;
+    // wave 0 writes the sweep's outputs (the merge kernel's rules: Aiyagari_VFI.m:79-81,
+    // Labor_VFI.m:85,106-109) and the block's max|v_new - v_old|
+    bool okd = false;
+    double dd = 0.0;
+    if (wave == 0 && okj) {
 #pragma unroll
-    for (int w = 1; w < W; ++w) lexi_take(s_best[w][lane], s_idx[w][lane], best, idx);
-    A.best0[t] = best;
-    A.idx0[t] = idx;
+        for (int w = 1; w < W; ++w) lexi_take(s_best[w][lane], s_idx[w][lane], best, idx);
+        const double vo = A.v_old[t];
+        if (!anyfeas && LAB) {  // no feasible (l, a'): v_new keeps its value (:85)
+            best = A.keep_incoming ? A.v_new[t] : vo;
+        } else {
+            if (idx < 0) {  // all candidates NaN: max returns NaN at index 1
+                idx = 0;
+                best = __builtin_nan("");
+            }
+            const int l = idx % Nl, k = idx / Nl;
+            const double kp = a[k];
+            A.idx[t] = idx;
+            if (A.pk) A.pk[t] = kp;
+            if (A.pc) A.pc[t] = cash<LAB>(x, y, LAB ? A.L[l] : 1.0) - kp;
+            if (LAB && A.pl) A.pl[t] = A.L[l];
+        }
+        A.v_new[t] = best;
+        dd = fabs(best - vo);
+        okd = dd == dd;
+    }
+    block_max_to_slots(okd, dd, A.diff);
 }
 
 // ------------------------------------------------------------------------------ launchers
@@ -2069,6 +2093,8 @@ static void run_tree(const BellArgs& A, hipStream_t st) {
         if constexpr (!LAB && NP == 4) {
             if (A.variant & 1) tree_w<NP, LAB, 2>(A, st);
             else tree_w<NP, LAB, 1>(A, st);
+        } else if constexpr (LAB && NP == 4) {  // labour: cooperating waves per tile (bits 1-2)
+            tree_w<NP, LAB, 1>(A, st);
         } else {
             tree_geo<NP, LAB, 1, 1>(A, st);
         }

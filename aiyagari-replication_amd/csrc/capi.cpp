@@ -208,7 +208,10 @@ static int bell_args(aiy_ws* ws, const BellCall& c, BellArgs& A, hipStream_t st)
 int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
     BellArgs A;
     AIY_TRY(bell_args(ws, c, A, st));
-    const bool screened = (c.mode != 2) && A.np > 0;
+    // mode 2 / variant bit 10: the exhaustive scan (one launch after the table, outputs written
+    // by the scan itself); otherwise the bound tree (or the chunked screen, variant bit 3)
+    const bool exhaustive = c.mode == 2 || A.np == 0 || (A.variant & 1024);
+    const bool screened = !exhaustive;
     AIY_TRY(launch_bell_table(A, st));  // also clears the diff slots
     if (!screened) A.coarse = 0, A.hint = nullptr;
     if (screened && A.tree) {
@@ -225,13 +228,16 @@ int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
         } else {
             AIY_TRY(launch_bell_tree(A, st));
         }
-    } else {
+    } else if (screened) {
         AIY_TRY(launch_bell_init(A, st));
         AIY_TRY(ws_timing_begin(ws, st));
-        if (screened) AIY_TRY(launch_bell_screen(A, st));
-        else AIY_TRY(launch_bell_plain(A, st));
+        AIY_TRY(launch_bell_screen(A, st));
         AIY_TRY(ws_timing_end(ws, st));
-        AIY_TRY(launch_bell_merge(A, screened ? 1 : 0, st));
+        AIY_TRY(launch_bell_merge(A, 1, st));
+    } else {
+        AIY_TRY(ws_timing_begin(ws, st));
+        AIY_TRY(launch_bell_plain(A, st));
+        AIY_TRY(ws_timing_end(ws, st));
     }
     if (c.diff_out) AIY_TRY(launch_reduce_slots(ws->diff, c.diff_out, st));
     return AIY_OK;
@@ -685,7 +691,7 @@ int aiy_ws_invalidate(aiy_ws* ws) {
 
 int aiy_ws_set_variant(aiy_ws* ws, int variant) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
-    if (variant < -1 || variant > 1023) return fail(AIY_BAD_ARG, "variant in [-1, 1023]");
+    if (variant < -1 || variant > 2047) return fail(AIY_BAD_ARG, "variant in [-1, 2047]");
     ws->variant = variant;
     return AIY_OK;
 }

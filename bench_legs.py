@@ -61,7 +61,7 @@ def _median(x):
 
 
 # ----------------------------------------------------------------------------------- D4 labour
-def labor_leg(pkg, dev, Na, steps=10, warmup=5, reps=5, cpu=True, cpu_threads=1):
+def labor_leg(pkg, dev, Na, steps=10, warmup=5, reps=5, cpu=True, cpu_threads=1, variant=-1):
     """A3 at the labour script's calibration (rho .6, sigma_e .2, psi 1, eta 2, Nl = 10): device
     tier sweeps from v = 0 (warm-up sweeps, then `steps` timed, median of `reps` restarts from the
     same state).  Unit: Na·Na'·Nl·Nz candidates per sweep."""
@@ -76,6 +76,8 @@ def labor_leg(pkg, dev, Na, steps=10, warmup=5, reps=5, cpu=True, cpu_threads=1)
     t = lambda x: torch.as_tensor(np.ascontiguousarray(x), device=dev)
     a_t, s_t, P_t, L_t = t(cal["a_grid"]), t(cal["s"]), t(cal["P"]), t(L)
     ws = pkg.Workspace(N, Na, 10)
+    if variant >= 0:
+        ws.set_variant(variant)
     v = [torch.zeros((N, Na), dtype=torch.float64, device=dev) for _ in range(2)]
     lin = torch.zeros((N, Na), dtype=torch.int32, device=dev)
     pk, pl, pc = (torch.zeros((N, Na), dtype=torch.float64, device=dev) for _ in range(3))

@@ -119,3 +119,38 @@ def test_labor_solve_infeasible_states_keep_incoming(pkg, gpu, max_iter):
     assert np.array_equal(R["policy_k"], p[0]) and np.array_equal(R["policy_l"], p[1])
     assert np.array_equal(R["policy_c"], p[2]) and np.array_equal(R["lin"] - 1, p[3])
     assert np.all(R["v_new"][~feasible] == 42.0) and np.all(R["lin"][~feasible] == 3)
+
+
+@pytest.mark.parametrize("Na,variant", [(400, 16), (400, 2), (400, 4), (400, 6), (1100, 4),
+                                        (2000, 18), (2000, 6), (400, 1024), (1100, 1024)])
+def test_labor_cooperating_waves_vs_oracle(pkg, gpu, Na, variant):
+    """Labour tree kernel with 1, 2, 4 and 8 cooperating waves per tile (variant bits 1-2; the
+    Na <= 4096 default is 2 waves), and the exhaustive scan (bit 10): device-tier sweeps with the hint chain of a solve, then one
+    sweep compared with the C oracle bit for bit (values, linear index, all three policies)."""
+    import torch
+    cal = no.calib_aiyagari(Na=Na, rho=0.6, sigma_e=0.2)
+    a, s, P = cal["a_grid"], cal["s"], cal["P"]
+    L = 0.01 + (1.5 - 0.01) * no.matlab_linspace01(10)
+    r = 0.04
+    w = no.wage(r, 0.36, 0.08)
+    dev = torch.device("cuda", 0)
+    t = lambda x: torch.as_tensor(np.ascontiguousarray(x), device=dev)
+    a_t, s_t, P_t, L_t = t(a), t(s), t(P), t(L)
+    ws = pkg.Workspace(7, Na, 10)
+    ws.set_variant(variant)
+    v = [torch.zeros((7, Na), dtype=torch.float64, device=dev) for _ in range(2)]
+    lin = torch.zeros((7, Na), dtype=torch.int32, device=dev)
+    pk, pl, pc = (torch.zeros((7, Na), dtype=torch.float64, device=dev) for _ in range(3))
+    cur = 0
+    for q in range(7):
+        if q == 6:
+            V = v[cur].cpu().numpy()
+        ws.labor_vfi_sweep(v[cur], a_t, s_t, P_t, L_t, r, w, 0.96, 5.0, 1.0, 2.0, v[1 - cur], lin,
+                           pk, pl, pc, hint=None if q == 0 else lin)
+        cur = 1 - cur
+    torch.cuda.synchronize()
+    vo, (pko, plo, pco, lino) = corc.labor_vfi_sweep(V, a, s, P, L, r, w, 0.96, 5.0, 1.0, 2.0)
+    assert np.array_equal(v[cur].cpu().numpy(), vo)
+    assert np.array_equal(lin.cpu().numpy(), lino)
+    assert np.array_equal(pk.cpu().numpy(), pko) and np.array_equal(pl.cpu().numpy(), plo)
+    assert np.array_equal(pc.cpu().numpy(), pco)
