@@ -90,6 +90,7 @@ def ks_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, exchange="halo", r
                                   f"out; sweep: k_opt, segment hint, forecast V/dV columns in, V "
                                   f"out) x {nodes // world} nodes per GPU / sweep time; the "
                                   f"working set (V, dV, k_opt: 200 MB) is HBM-resident"},
+            "pmc": _ks_pmc(),
             "scaling": "strong", "vfi_iteration_ms": (ti + th) * 1e3,
             "howard_ms_per_sweep": th / howard * 1e3, "improve_ms": ti * 1e3,
             "workload": f"Krusell_Smith_VFI k={nk} K={nK} S=4 ({nodes} nodes, BASELINE "
@@ -102,6 +103,23 @@ def ks_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, exchange="halo", r
                               if hs.depth > 1 else
                               f"per Howard sweep (rank 0 receives {cols} (s, K) columns of "
                               f"{nk} values)")}
+
+
+def _ks_pmc():
+    """Counter summaries of the two Howard-sweep kernels at this size (rocprofv3 --pmc passes
+    over `bench_ks.py --howard 10`, tools/exp/exp_r02b_s10.sh), if committed under profiles/."""
+    out = {}
+    for name, f, t in (("ks_howard_kernel", "r02b_pmc_ks_howard.json", "r02b_traffic_ks_howard.json"),
+                       ("ks_slopes_cols_kernel", "r02b_pmc_ks_slopes.json",
+                        "r02b_traffic_ks_slopes.json")):
+        p, q = ROOT / "profiles" / f, ROOT / "profiles" / t
+        if p.exists():
+            d = json.loads(p.read_text())["derived"]
+            out[name] = {k: d[k] for k in ("valu_busy", "waves_per_simd", "valu_per_wave",
+                                           "wait_frac")}
+            if q.exists():
+                out[name]["hbm_bytes_per_launch"] = json.loads(q.read_text())["bytes_per_launch"]
+    return out or None
 
 
 def ghost_model(pkg, dev, world=8, nk=32768, nK=64, depths=(1, 2, 3, 4, 6, 8), sweeps=24):
