@@ -29,6 +29,7 @@ struct ks_dev {
     unsigned long long* slots = nullptr;
     int* seg = nullptr;    // [node] segment hints: improve writes them, Howard checks and uses them
     ks_dev* seg_owner = nullptr;  // set: seg is that handle's array (ks_dev_share_hints)
+    int sharers = 0;              // handles using this handle's seg array
 };
 
 namespace aiy {
@@ -58,6 +59,10 @@ extern "C" {
 
 int ks_dev_destroy(ks_dev* h) {
     if (!h) return AIY_OK;
+    if (h->sharers > 0)
+        return fail(AIY_BAD_ARG, "ks_dev_destroy: %d handle(s) still share this handle's hints; "
+                    "destroy them first", h->sharers);
+    if (h->seg_owner) h->seg_owner->sharers--;
     void* ps[] = {h->kg, h->P, h->sl, h->dV, h->cols, h->slots, h->seg_owner ? nullptr : h->seg};
     for (void* q : ps)
         if (q) (void)hipFree(q);
@@ -167,9 +172,13 @@ int ks_dev_share_hints(ks_dev* h, ks_dev* owner) {
     if (owner->seg_owner) return fail(AIY_BAD_ARG, "owner shares another handle's hints");
     if (h->nk != owner->nk || h->nK != owner->nK || h->dev != owner->dev)
         return fail(AIY_BAD_SHAPE, "ks_dev_share_hints: handles of different grids or devices");
-    if (!h->seg_owner) AIY_HIP(hipFree(h->seg));
+    if (h->sharers > 0) return fail(AIY_BAD_ARG, "other handles share h's hints");
+    if (h->seg_owner == owner) return AIY_OK;
+    if (h->seg_owner) h->seg_owner->sharers--;
+    else AIY_HIP(hipFree(h->seg));
     h->seg = owner->seg;
     h->seg_owner = owner;
+    owner->sharers++;
     return AIY_OK;
 }
 

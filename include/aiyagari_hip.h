@@ -330,7 +330,8 @@ int ks_dev_howard(ks_dev* h, const double* V, const double* kopt, double* Vout, 
 int ks_dev_reldiff(ks_dev* h, const double* V, const double* Vold, void* out, void* stream);
 /* Ghost shards (ks_dist.py exchanges halos every m Howard sweeps and sweeps a widening
  * rectangle of other ranks' columns redundantly in between — same kernels, so still bit-exact):
- * h uses owner's segment-hint array (owner must outlive h; same grid and device), and
+ * h uses owner's segment-hint array (same grid and device; destroying owner while a handle
+ * still shares it fails with AIY_BAD_ARG), and
  * ks_dev_hints recomputes the hints of h's nodes from kopt (for k_opt received from other
  * ranks).  Hints only short-cut Howard's segment search: results never depend on them. */
 int ks_dev_share_hints(ks_dev* h, ks_dev* owner);

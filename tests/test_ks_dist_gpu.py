@@ -119,3 +119,18 @@ def test_ghost_sweeps_on_one_card(pkg, gpu, tmp_path, world, nK, depth):
         assert np.array_equal(np.load(Path(tmp_path, f"V{rank}.npy")), Vr)
         assert np.array_equal(np.load(Path(tmp_path, f"k{rank}.npy")), kr)
         assert json.loads(Path(tmp_path, f"m{rank}.json").read_text())["it"] == itr
+
+
+def test_shared_hints_lifetime(pkg, gpu):
+    """ks_dev_share_hints: the owner cannot be destroyed while a ghost shard shares its hint
+    array (AIY_BAD_ARG), and can once the ghost is gone."""
+    kd = pkg.ks_dist
+    kg, Kg, P, V0 = _setup(6)
+    sh = kd.HipShard(kg, Kg, B_MIXED, P, pkg.ks_params(), 2, 4, 0, 4)
+    g = sh.ghost(0, 6, 0, 4)
+    lib = pkg.lib()
+    assert lib.ks_dev_destroy(sh._h) != 0          # refused: g still shares its hints
+    assert b"share" in lib.aiy_last_error()
+    g.close()
+    assert lib.ks_dev_destroy(sh._h) == 0
+    sh._h = None
