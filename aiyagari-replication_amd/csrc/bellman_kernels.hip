@@ -216,7 +216,7 @@ __global__ __launch_bounds__(kTableBlock) void bell_table_kernel(
         if (fold && threadIdx.x < 64) {  // same fold as reduce_slots_kernel
             const int l = threadIdx.x;
             unsigned long long m = diff[2 * l];
-            const int any = __ballot(diff[2 * l + 1] != 0ull) != 0ull;
+            const int any = __ballot((diff[2 * l + 1] & 1ull) != 0ull) != 0ull;
             for (int off = 32; off > 0; off >>= 1) {
                 unsigned long long o = __shfl_xor(m, off);
                 m = o > m ? o : m;
@@ -298,7 +298,7 @@ __global__ __launch_bounds__(kTableBlock) void bell_table_batch_kernel(
             const int l = threadIdx.x;
             const unsigned long long* sl = slots + ((size_t)c * 2 + ((sweep - 1) & 1)) * 2 * kDiffSlots;
             unsigned long long m = sl[2 * l];
-            const int any = __ballot(sl[2 * l + 1] != 0ull) != 0ull;
+            const int any = __ballot((sl[2 * l + 1] & 1ull) != 0ull) != 0ull;
             for (int off = 32; off > 0; off >>= 1) {
                 const unsigned long long o = __shfl_xor(m, off);
                 m = o > m ? o : m;
@@ -1514,7 +1514,7 @@ __global__ __launch_bounds__(64) void bell_persist_kernel(PersistArgs PA) {
     // the stop test of a sweep from its diff slots (reduce_slots_kernel's fold)
     auto stop_of = [&](const unsigned long long* sl) __attribute__((always_inline)) {
         unsigned long long m = sl[2 * lane];
-        const bool any = __ballot(sl[2 * lane + 1] != 0ull) != 0ull;
+        const bool any = __ballot((sl[2 * lane + 1] & 1ull) != 0ull) != 0ull;
         for (int off = 32; off > 0; off >>= 1) {
             const unsigned long long o = __shfl_xor(m, off);
             m = o > m ? o : m;
@@ -2186,7 +2186,7 @@ __global__ void reduce_slots_kernel(const unsigned long long* __restrict__ slots
                                    unsigned long long* __restrict__ out) {
     int l = threadIdx.x;
     unsigned long long k = slots[2 * l];
-    int any = __ballot(slots[2 * l + 1] != 0ull) != 0ull;
+    int any = __ballot((slots[2 * l + 1] & 1ull) != 0ull) != 0ull;
     for (int off = 32; off > 0; off >>= 1) {
         unsigned long long o = __shfl_xor(k, off);
         k = o > k ? o : k;
@@ -2207,7 +2207,7 @@ double fold_slots_host(const unsigned long long* h) {
     unsigned long long k = 0;
     bool any = false;
     for (int q = 0; q < kDiffSlots; ++q) {
-        if (h[2 * q + 1]) any = true;
+        if (h[2 * q + 1] & 1ull) any = true;  // (bit 1: EGM non-monotone flag)
         k = h[2 * q] > k ? h[2 * q] : k;
     }
     if (!any) return __builtin_nan("");

@@ -691,7 +691,7 @@ int aiy_ws_invalidate(aiy_ws* ws) {
 
 int aiy_ws_set_variant(aiy_ws* ws, int variant) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
-    if (variant < -1 || variant > 2047) return fail(AIY_BAD_ARG, "variant in [-1, 2047]");
+    if (variant < -1 || variant > 4095) return fail(AIY_BAD_ARG, "variant in [-1, 4095]");
     ws->variant = variant;
     return AIY_OK;
 }

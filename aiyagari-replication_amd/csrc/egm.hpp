@@ -18,7 +18,9 @@ struct EgmArgs {
     double* pk;
     double* pl;       // A5 (nullable)
     unsigned long long* diff;  // [2]
-    unsigned* flags;           // bit 0: a_hat not increasing
+    unsigned* flags;           // bit 0: a_hat not increasing (small-grid fused step: bit 1 of
+                               // the diff slots' second word instead, see egm_fused_kernel)
+    bool fused;                // Na <= 1024: one launch per step (egm_fused_kernel)
 };
 int launch_egm_step(const EgmArgs& A, hipStream_t st);
 }  // namespace aiy

@@ -19,6 +19,15 @@ static int fail_nonmonotone() {
                              "reference would sort it or fail (Aiyagari_EGM.m:95)");
 }
 
+// the non-monotone flag of a step from host copies of its diff slots and flag word: bit 0 of
+// the word (two-launch step) or bit 1 of a slot's second word (egm_fused_kernel)
+static bool egm_nonmonotone(const unsigned long long* slots, unsigned flag_word) {
+    if (flag_word & 1u) return true;
+    for (int q = 0; q < kDiffSlots; ++q)
+        if (slots[2 * q + 1] & 2ull) return true;
+    return false;
+}
+
 static int ensure_egm(aiy_ws* ws) {
     size_t n = (size_t)ws->N * ws->Na;
     if (!ws->g0) AIY_HIP(hipMalloc((void**)&ws->g0, n * sizeof(double)));
@@ -46,6 +55,8 @@ static EgmArgs egm_args(aiy_ws* ws, const double* c, const double* a, const doub
     A.ahat = ws->g0; A.cnext = ws->g1; A.cout = cout; A.pk = pk; A.pl = pl;
     A.diff = ws->diff;
     A.flags = (unsigned*)ws->gi;
+    // one launch per step on small grids unless the tuning variant sets bit 11 (A/B only)
+    A.fused = !(ws->variant >= 0 && (ws->variant & 2048));
     return A;
 }
 
@@ -73,7 +84,7 @@ static int read_egm(aiy_ws* ws, hipStream_t st, double* d) {
     AIY_HIP(hipMemcpyAsync(h + 2 * kDiffSlots, ws->gi, sizeof(int), hipMemcpyDeviceToHost, st));
     AIY_HIP(hipStreamSynchronize(st));
     *d = fold_slots_host(h);
-    if ((unsigned)h[2 * kDiffSlots] & 1u) return fail_nonmonotone();
+    if (egm_nonmonotone(h, (unsigned)h[2 * kDiffSlots])) return fail_nonmonotone();
     return AIY_OK;
 }
 
@@ -125,7 +136,7 @@ static int egm_solve_spec(aiy_ws* ws, const EgmArgs& A0, double* c0, double tol,
         AIY_HIP(hipStreamSynchronize(st));
         for (int64_t t = 0; t < m; ++t) {
             const unsigned long long* h = ws->egm_hslots + (size_t)t * SW;
-            if ((unsigned)h[2 * kDiffSlots] & 1u) return fail_nonmonotone();
+            if (egm_nonmonotone(h, (unsigned)h[2 * kDiffSlots])) return fail_nonmonotone();
             const double d = fold_slots_host(h);
             d_prev = d_last;
             d_last = d;

@@ -155,7 +155,7 @@ def labor_leg(pkg, dev, Na, steps=10, warmup=5, reps=5, cpu=True, cpu_threads=1,
 
 
 # ----------------------------------------------------------------------------------- D4 EGM
-def egm_leg(pkg, dev, Na, labor=False, steps=50, reps=5, cpu_threads=1):
+def egm_leg(pkg, dev, Na, labor=False, steps=50, reps=5, cpu_threads=1, variant=-1):
     """A4 (or A5) steps on device at r = 0.04 from the script's initial consumption guess
     (Aiyagari_EGM.m:64); unit = one (a, z) state per iteration; HBM roofline with the
     algorithmic bytes of SURVEY D4 (24 B: c in, c_next and policy_k out; +8 for policy_l)."""
@@ -170,6 +170,8 @@ def egm_leg(pkg, dev, Na, labor=False, steps=50, reps=5, cpu_threads=1):
     t = lambda x: torch.as_tensor(np.ascontiguousarray(x), device=dev)
     a_t, s_t, P_t = t(a), t(cal["s"]), t(cal["P"])
     ws = pkg.Workspace(N, Na)
+    if variant >= 0:  # (bit 11: the two-launch step even on small grids — A/B only)
+        ws.set_variant(variant)
     c = [t(pc0), torch.zeros((N, Na), dtype=torch.float64, device=dev)]
     pk = torch.zeros_like(c[0])
     pl = torch.zeros_like(c[0]) if labor else None
@@ -222,8 +224,10 @@ def egm_leg(pkg, dev, Na, labor=False, steps=50, reps=5, cpu_threads=1):
         walls.append(time.perf_counter() - t0)
         iters = R["iters"]
     solve_s = _median(walls)
-    return {"workload": f"{name} steps, Na={Na} Nz={N} Rouwenhorst, device tier (2 launches "
-                        f"per step: Euler RHS, interp1 inversion)",
+    fused = Na <= 1024 and not (variant >= 0 and variant & 2048)
+    return {"workload": f"{name} steps, Na={Na} Nz={N} Rouwenhorst, device tier (" +
+                        ("1 launch per step: egm_fused_kernel, a workgroup per z-state)" if fused
+                         else "2 launches per step: Euler RHS, interp1 inversion)"),
             "solve": {"iters": iters, "wall_ms": solve_s * 1e3,
                       "us_per_iteration": solve_s / max(iters, 1) * 1e6,
                       "path": "host tier (aiy_egm_solve / aiy_labor_egm_solve): speculative "

@@ -248,7 +248,10 @@ int aiy_ws_set_persistent(aiy_ws* ws, int persistent);
  * bit 0 = 4 states per lane (else 2), bit 1 = registers capped for 8 waves per SIMD, bit 2 =
  * fp64-only screen (else the packed fp32 pre-screen with directed-rounding bounds first).
  * Tree screen extras: bit 5 = no hill-climb from the hint, bits 7-8 = hint window half-width
- * 1, 2, 4 or 8, bit 9 = no extrapolated (hint + last shift) start, bit 6 = 4 lanes per state.
+ * 1, 2, 4 or 8, bit 9 = no extrapolated (hint + last shift) start, bit 6 = 4 lanes per state,
+ * bit 10 = the plain exhaustive scan.  EGM steps on this workspace: bit 11 = two launches per
+ * step even when Na <= 1024 (default there: one fused launch).  Results are identical for every
+ * value in [-1, 4095].
  * -1 (default): chosen by size — 2 cooperating waves per tile for Na <= 4096, else 16. */
 int aiy_ws_set_variant(aiy_ws* ws, int variant);
 

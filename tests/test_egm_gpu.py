@@ -96,3 +96,57 @@ def test_egm_solve_nonmonotone_grid_is_reported(pkg, gpu):
         pkg.egm_solve(pc0, a, np.array([1.0, 1.2]), np.full((2, 2), 0.5), 0.02, 1.0, 0.96, 5.0,
                       0.0, 1e-6, 50)
     assert e.value.status == "AIY_BAD_ARG"
+
+
+@pytest.mark.parametrize("Na", [2, 3, 65, 400, 1024, 1025])
+@pytest.mark.parametrize("labor", [False, True])
+def test_egm_fused_small_grid_equals_two_launches(pkg, gpu, Na, labor):
+    """Na <= 1024 runs a step as ONE launch (egm_fused_kernel, a workgroup per productivity
+    state); variant bit 11 forces the two-launch path.  Both, and the C restatement, agree bit
+    for bit over several steps (policy_c, policy_k, policy_l and the step's dist)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    cal = no.calib_aiyagari(Na=Na, shocks="rouwenhorst")
+    a, s, P = cal["a_grid"], cal["s"], cal["P"]
+    N = P.shape[0]
+    r = 0.03
+    w = no.wage(r, 0.36, 0.08)
+    t = lambda x: torch.as_tensor(np.ascontiguousarray(x), device=dev)
+    a_t, s_t, P_t = t(a), t(s), t(P)
+    pc = np.tile(((1 + r) * a + w * np.mean(s))[None, :], (N, 1))
+    runs = []
+    for var in (-1, 2048):
+        ws = pkg.Workspace(N, Na)
+        if var >= 0:
+            ws.set_variant(var)
+        c = t(pc)
+        outs = []
+        for _ in range(6):
+            o, k = torch.empty_like(c), torch.empty_like(c)
+            l = torch.empty_like(c) if labor else None
+            dd = torch.zeros(2, dtype=torch.int64, device=dev)
+            pkg.egm_step_dev(ws, c, a_t, s_t, P_t, r, w, 0.96, 5.0, cal["amin"], o, k,
+                             labor=labor, phi=1.0, theta=1.0, policy_l=l, diff=dd)
+            outs.append([x.cpu().numpy() for x in (c, o, k) + ((l,) if labor else ())] +
+                        [dd.cpu().numpy()])
+            c = o
+        runs.append(outs)
+    for step_f, step_t in zip(*runs):
+        for x, y in zip(step_f, step_t):
+            assert np.array_equal(x, y)
+    for cin, o, k, *rest in runs[0][:2]:
+        if labor:
+            co, ko, lo, _ = corc.labor_egm_step(cin, a, s, P, r, w, 0.96, 5.0, 1.0, 1.0, cal["amin"])
+            assert np.array_equal(rest[0], lo)
+        else:  # (corc works on [N][Na], the device layout)
+            co, ko, _ = corc.egm_step(cin, a, s, P, r, w, 0.96, 5.0, cal["amin"])
+        assert np.array_equal(o, co) and np.array_equal(k, ko)
+
+
+def test_egm_nonmonotone_grid_is_reported_two_launch_path(pkg, gpu):
+    """Na > 1024 takes the two-launch path (flag word) — reported like the fused path (slots)."""
+    a = np.linspace(0, 10, 5000)
+    pc0 = np.tile(np.linspace(50, 0.01, 5000)[:, None], (1, 2))
+    with pytest.raises(pkg.AiyError) as e:
+        pkg.egm_step(pc0, a, np.array([1.0, 1.2]), np.full((2, 2), 0.5), 0.02, 1.0, 0.96, 5.0, 0.0)
+    assert e.value.status == "AIY_BAD_ARG"
