@@ -152,6 +152,8 @@ def main():
     ap.add_argument("--no-ge", action="store_true", help="skip the GE wall-time legs")
     ap.add_argument("--no-solve", action="store_true", help="skip the solve-to-tol leg")
     ap.add_argument("--no-ks", action="store_true", help="skip the sharded Krusell-Smith leg")
+    ap.add_argument("--distinct-r", action="store_true",
+                    help="N > 1: one GE candidate r per rank instead of the same r on every rank")
     ap.add_argument("--no-panel", action="store_true", help="skip the KS panel (F2/F3) leg")
     ap.add_argument("--ks-depth", type=int, default=None,
                     help="KS Howard sweeps per halo exchange (default 4 on >1 rank)")
@@ -166,17 +168,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)  # before the process group: RCCL binds the current device
     if world > 1:
         dist.init_process_group("nccl")
-    torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
     pkg = load_pkg()
     cal = pkg.calibration.aiyagari(Na=args.na, shocks="rouwenhorst")
     N, Na = cal["N"], cal["Na"]
-    # candidate interest rates of the GE bracket [-0.05, 1/beta-1]: one per rank
+    # weak scaling: every rank sweeps the same problem (r = 0.04), so the work per GPU is fixed
+    # as N grows and the driver's efficiency compares like with like; --distinct-r gives each
+    # rank its own GE candidate of the bracket [-0.05, 1/beta-1] instead (per-rank cost varies
+    # with r: the feasible set shrinks as r falls)
     r_lo, r_hi = -0.05, 1 / cal["beta"] - 1
-    r = r_lo + (r_hi - r_lo) * (rank + 1) / (world + 1) if world > 1 else 0.04
+    r = r_lo + (r_hi - r_lo) * (rank + 1) / (world + 1) if (world > 1 and args.distinct_r) else 0.04
     w = pkg.calibration.wage(r, cal["alpha"], cal["delta"])
 
     t = lambda x: torch.as_tensor(np.ascontiguousarray(x), device=dev)
@@ -320,7 +325,10 @@ def main():
                                  else "exhaustive over a' (plain)",
                        "sweeps_timed": f"sweeps {args.warmup + 1}..{args.warmup + args.steps} of a "
                                        f"solve from v=0, hint = previous argmax",
-                       "parallelism": f"replicas: one GE candidate r per rank ({world})",
+                       "parallelism": (f"replicas: one GE candidate r per rank ({world})"
+                                       if world > 1 and args.distinct_r else
+                                       f"replicas: the same sweeps (r = 0.04) on each of {world} "
+                                       f"rank(s), no data-path collective"),
                        "feasible_fraction": feas / evals_per_sweep,
                        "tests_per_sweep": tests},
             "repeats": {"n": len(blocks), "median_ms_per_step": step_ms[len(blocks) // 2]

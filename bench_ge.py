@@ -35,9 +35,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)  # before the process group: RCCL binds the current device
     if world > 1:
         dist.init_process_group("nccl")
-    torch.cuda.set_device(local)
     pkg = bench.load_pkg()
     gb = pkg.ge_batch
     pkg.ge_batch.aiyagari_vfi_multisection(Na=args.na, levels=1, rank=0, world=1)  # warm-up

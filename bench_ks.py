@@ -187,9 +187,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)  # before the process group: RCCL binds the current device
     if world > 1:
         dist.init_process_group("nccl")
-    torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if args.ghost_model:
         out = ghost_model(bench.load_pkg(), dev, nk=args.nk, nK=args.nK)
