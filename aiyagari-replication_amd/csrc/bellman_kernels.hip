@@ -1154,7 +1154,8 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
         // prep of superblock n+1 before finish of superblock n, so the candidate loads of n+1
         // are in flight while n is screened (a bar raised by n's exact path only makes n+1's
         // bound tests, done against the older bar, pass more: never fewer candidates).
-        auto prep = [&](int sb, int bsel, int bstep, double dm8, double a8, double2 (&st)[8])
+        auto prep = [&](int sb, int bsel, int bstep, double dm8, double a8, double2 (&st)[8],
+                        bool subsplit = false)
                         __attribute__((always_inline)) -> unsigned long long {
             stamp(0);
             const int sbase = sb << 9;  // first candidate of the superblock
@@ -1163,10 +1164,13 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
             dm64 = fmax(dm64, dpp_d<0xB1>(dm64));
             dm64 = fmax(dm64, dpp_d<0x4E>(dm64));
             dm64 = fmax(dm64, dpp_d<0x104>(dm64));
-            // blocks inside the feasible range and owned by this wave
+            // blocks inside the feasible range and owned by this wave.  subsplit: every wave
+            // bound-tests every block and keeps the passing 8-blocks i with i % bstep == bsel —
+            // the passing 8-blocks cluster around the optima, so a split by 64-block leaves
+            // one wave with most of the fine screens and the others waiting at the exchange
             const int nblock = min(8, (kg - sbase + 63) >> 6);
             unsigned own = 0;
-            for (int b = bsel; b < nblock; b += bstep) own |= 1u << b;
+            for (int b = subsplit ? 0 : bsel; b < nblock; b += subsplit ? 1 : bstep) own |= 1u << b;
             if (INS && (A.hitcount || A.trace)) nblk += __builtin_popcount(own);
             const unsigned bpass = mask8(dm64, a8, 0, 8, nblock) & own;
             unsigned long long pass = 0;  // bit 8b+u: sub-block u of block b passes
@@ -1175,6 +1179,12 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
                 const int nsub = min(8, (kg - (sbase + (b << 6)) + 7) >> 3);
                 if (INS && (A.hitcount || A.trace)) nblk += nsub;
                 pass |= (unsigned long long)mask8(dm8, a8, 8 * b, 1, nsub, true) << (8 * b);
+            }
+            if (subsplit && bstep > 1) {  // 8-blocks bsel, bsel + bstep, ... (bstep = W: 2, 4, 8)
+                const unsigned long long pat = bstep == 2 ? 0x5555555555555555ull
+                                             : (bstep == 4 ? 0x1111111111111111ull
+                                                           : 0x0101010101010101ull);
+                pass &= pat << bsel;
             }
 #pragma unroll
             for (int b = 0; b < 8; ++b)  // all loads issued before any is used
@@ -1240,7 +1250,8 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
             if (INS) ++nsup;
             double d8, a8;
             load8(sfirst, d8, a8);
-            const unsigned long long p = prep(sfirst, wave, W, d8, a8, st_cur);
+            const unsigned long long p = prep(sfirst, wave, W, d8, a8, st_cur,
+                                              (A.variant & 4096) != 0);
             if (p) finish(sfirst, p, st_cur);
             exchange();
             set_B();

@@ -131,8 +131,12 @@ static int bell_args(aiy_ws* ws, const BellCall& c, BellArgs& A, hipStream_t st)
     A.coarse = ws->coarse;
     A.CK = ws->CK;
     // default geometry by size (measured at Na = 400: 2 cooperating waves per tile 10 % faster;
-    // at Na = 20,000 one wave per tile, XCD-aware tile order: 44.3 vs 45.9 us)
-    const int var = ws->variant >= 0 ? ws->variant : (ws->Na <= 4096 ? 2 : 16);
+    // at Na = 20,000 one wave per tile, XCD-aware tile order: 44.3 vs 45.9 us).  Labour at
+    // Na <= 4096: 4 waves per tile with the first superblock's passing 8-blocks dealt
+    // round-robin (bit 12) — Na = 400 sweep 58.1 -> 41.8 us, 1,000: 61.8 -> 54.8, 2,000:
+    // 81.5 -> 70.3 (profiles/r02c_s6_*); A1 is neutral to it (16.4 us either way)
+    const int var = ws->variant >= 0 ? ws->variant
+                                     : (ws->Na <= 4096 ? (c.labor ? 4 | 4096 : 2) : 16);
     A.variant = var;
     A.r = c.r;
     A.w = c.w;
@@ -691,7 +695,7 @@ int aiy_ws_invalidate(aiy_ws* ws) {
 
 int aiy_ws_set_variant(aiy_ws* ws, int variant) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
-    if (variant < -1 || variant > 4095) return fail(AIY_BAD_ARG, "variant in [-1, 4095]");
+    if (variant < -1 || variant > 8191) return fail(AIY_BAD_ARG, "variant in [-1, 8191]");
     ws->variant = variant;
     return AIY_OK;
 }

@@ -249,10 +249,12 @@ int aiy_ws_set_persistent(aiy_ws* ws, int persistent);
  * fp64-only screen (else the packed fp32 pre-screen with directed-rounding bounds first).
  * Tree screen extras: bit 5 = no hill-climb from the hint, bits 7-8 = hint window half-width
  * 1, 2, 4 or 8, bit 9 = no extrapolated (hint + last shift) start, bit 6 = 4 lanes per state,
- * bit 10 = the plain exhaustive scan.  EGM steps on this workspace: bit 11 = two launches per
- * step even when Na <= 1024 (default there: one fused launch).  Results are identical for every
- * value in [-1, 4095].
- * -1 (default): chosen by size — 2 cooperating waves per tile for Na <= 4096, else 16. */
+ * bit 10 = the plain exhaustive scan, bit 12 = cooperating waves deal the first superblock's
+ * passing 8-blocks round-robin (else by 64-block).  EGM steps on this workspace: bit 11 = two
+ * launches per step even when Na <= 1024 (default there: one fused launch).  Results are
+ * identical for every value in [-1, 8191].
+ * -1 (default): chosen by size — Na <= 4096: 2 cooperating waves per tile (A1), 4 with bit 12
+ * (labour); else 16. */
 int aiy_ws_set_variant(aiy_ws* ws, int variant);
 
 /* A1 on device.  hint (nullable, [N][Na] int32 0-based) = previous sweep's argmax; the result
