@@ -816,6 +816,7 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
     const double y = A.w * A.s[i];
     const int jbase = tile * (64 * R);
     __shared__ double2 s_cand[W][512];  // each wave's current superblock: (a_k, D_k)
+    __shared__ unsigned long long s_pass[W];  // (first superblock, bit 12) per-wave pass masks
     // W >= 2 (cooperating waves): registers are budgeted for 5 waves per SIMD, so the staging
     // and fine-screen software pipelines (two register sets each) are off and the screen
     // stages four chains at a time; the best exchange reuses each wave's idle s_cand slice
@@ -1174,17 +1175,28 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
             if (INS && (A.hitcount || A.trace)) nblk += __builtin_popcount(own);
             const unsigned bpass = mask8(dm64, a8, 0, 8, nblock) & own;
             unsigned long long pass = 0;  // bit 8b+u: sub-block u of block b passes
-            for (unsigned bm = bpass; bm; bm &= bm - 1) {
+            const bool deal = subsplit && bstep > 1;
+            int ord = 0;
+            for (unsigned bm = bpass; bm; bm &= bm - 1, ++ord) {
+                // deal: the passing 64-blocks' 8-block tests go round-robin over the waves too
+                if (deal && ord % bstep != bsel) continue;
                 const int b = __builtin_ctz(bm);
                 const int nsub = min(8, (kg - (sbase + (b << 6)) + 7) >> 3);
                 if (INS && (A.hitcount || A.trace)) nblk += nsub;
                 pass |= (unsigned long long)mask8(dm8, a8, 8 * b, 1, nsub, true) << (8 * b);
             }
-            if (subsplit && bstep > 1) {  // 8-blocks bsel, bsel + bstep, ... (bstep = W: 2, 4, 8)
-                const unsigned long long pat = bstep == 2 ? 0x5555555555555555ull
-                                             : (bstep == 4 ? 0x1111111111111111ull
-                                                           : 0x0101010101010101ull);
-                pass &= pat << bsel;
+            if constexpr (W > 1) {
+                if (deal) {  // the union of the waves' masks, then 8-blocks bsel, bsel + W, ...
+                    s_pass[bsel] = pass;
+                    __syncthreads();
+                    unsigned long long all = 0;
+                    for (int v = 0; v < bstep; ++v) all |= s_pass[v];
+                    __syncthreads();
+                    const unsigned long long pat = bstep == 2 ? 0x5555555555555555ull
+                                                 : (bstep == 4 ? 0x1111111111111111ull
+                                                               : 0x0101010101010101ull);
+                    pass = all & (pat << bsel);
+                }
             }
 #pragma unroll
             for (int b = 0; b < 8; ++b)  // all loads issued before any is used
