@@ -799,6 +799,13 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
     const long long t_boot = (INS && A0.trace) ? (long long)wall_clock64() : 0;  // (instrumentation)
     const long long c_boot = (INS && A0.trace) ? (long long)__builtin_amdgcn_s_memtime() : 0;
     int item = (A0.variant & 16) ? xcd_remap(block_id, nblocks) : block_id;
+    if ((A0.variant & 8192) && A0.C <= 1) {
+        // descending j: a launch larger than two waves per SIMD places its last workgroups as
+        // third waves on a SIMD; with this order those are the lowest-asset tiles, whose short
+        // feasible prefixes make them the cheapest
+        const int q = block_id / A0.N;
+        item = (block_id - q * A0.N) * ntile + (ntile - 1 - q);
+    }
     BellArgs A = A0;
     if (A0.C > 1) {  // batched candidates: blocks [c·N·ntile, (c+1)·N·ntile) are candidate c's
         const int c = item / (A0.N * ntile);

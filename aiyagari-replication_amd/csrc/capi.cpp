@@ -135,8 +135,11 @@ static int bell_args(aiy_ws* ws, const BellCall& c, BellArgs& A, hipStream_t st)
     // Na <= 4096: 4 waves per tile with the first superblock's passing 8-blocks dealt
     // round-robin (bit 12) — Na = 400 sweep 58.1 -> 41.8 us, 1,000: 61.8 -> 54.8, 2,000:
     // 81.5 -> 70.3 (profiles/r02c_s6_*); A1 is neutral to it (16.4 us either way)
+    // A1 at Na > 4096: tiles in descending j (bit 13) — the launch's third waves per SIMD get
+    // the cheap low-asset tiles: headline kernel 34.8 -> 32.9 us (profiles/r02c_s11_*)
     const int var = ws->variant >= 0 ? ws->variant
-                                     : (ws->Na <= 4096 ? (c.labor ? 4 | 4096 : 2) : 16);
+                                     : (ws->Na <= 4096 ? (c.labor ? 4 | 4096 : 2)
+                                                       : (c.labor ? 16 : 8192));
     A.variant = var;
     A.r = c.r;
     A.w = c.w;
@@ -695,7 +698,7 @@ int aiy_ws_invalidate(aiy_ws* ws) {
 
 int aiy_ws_set_variant(aiy_ws* ws, int variant) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
-    if (variant < -1 || variant > 8191) return fail(AIY_BAD_ARG, "variant in [-1, 8191]");
+    if (variant < -1 || variant > 16383) return fail(AIY_BAD_ARG, "variant in [-1, 16383]");
     ws->variant = variant;
     return AIY_OK;
 }

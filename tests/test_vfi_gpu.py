@@ -146,7 +146,7 @@ def test_full_size_bitwise_vs_oracle(pkg, gpu):
     assert (pcs > 0).all()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 6, 8, 12, 64, 96, 4098, 4100, 4102])
+@pytest.mark.parametrize("variant", [0, 1, 2, 6, 8, 12, 64, 96, 4098, 4100, 4102, 8192, 8194])
 def test_screen_stress_noisy_value(pkg, gpu, variant):
     """Rough value functions put many candidates within rounding distance of the running best
     (near-ties everywhere, multi-modal objectives): the fp32 pre-screen, the fp64 screen and
