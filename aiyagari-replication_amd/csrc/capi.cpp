@@ -135,11 +135,11 @@ static int bell_args(aiy_ws* ws, const BellCall& c, BellArgs& A, hipStream_t st)
     // Na <= 4096: 4 waves per tile with the first superblock's passing 8-blocks dealt
     // round-robin (bit 12) — Na = 400 sweep 58.1 -> 41.8 us, 1,000: 61.8 -> 54.8, 2,000:
     // 81.5 -> 70.3 (profiles/r02c_s6_*); A1 is neutral to it (16.4 us either way)
-    // A1 at Na > 4096: tiles in descending j (bit 13) — the launch's third waves per SIMD get
-    // the cheap low-asset tiles: headline kernel 34.8 -> 32.9 us (profiles/r02c_s11_*)
+    // (Na > 4096: bit 13, tiles in descending j, is faster in a solve's early sweeps — sweep 25:
+    // 34.9 vs 35.8 us — and slower once the policy has settled — sweep 100: 33.6 vs 32.8 us,
+    // whole solve to tol 9.37 vs 8.99 ms — so the default stays row-major, XCD-contiguous (16))
     const int var = ws->variant >= 0 ? ws->variant
-                                     : (ws->Na <= 4096 ? (c.labor ? 4 | 4096 : 2)
-                                                       : (c.labor ? 16 : 8192));
+                                     : (ws->Na <= 4096 ? (c.labor ? 4 | 4096 : 2) : 16);
     A.variant = var;
     A.r = c.r;
     A.w = c.w;

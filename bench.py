@@ -299,12 +299,10 @@ def main():
         # result is bit-identical to -- the rate an exhaustive kernel would need to match it
         effective = FLOPS_PER_CANDIDATE * evals_per_sweep / (kern_avg_ms * 1e-3) / 1e12
         traffic = None
-        tf = (_json_profile("r02c_traffic_vfi_tree.json") or _json_profile("r02b_traffic_vfi_tree.json")
-              or _json_profile("traffic_vfi_tree.json"))
+        tf = _json_profile("r02b_traffic_vfi_tree.json") or _json_profile("traffic_vfi_tree.json")
         if tf:
             traffic = tf.get("bytes_per_launch")
-        pmc = (_json_profile("r02c_pmc_tree_final.json") or _json_profile("r02b_pmc_tree_final.json")
-               or _json_profile("r02_pmc_tree_final.json")
+        pmc = (_json_profile("r02b_pmc_tree_final.json") or _json_profile("r02_pmc_tree_final.json")
                or _json_profile("r02_pmc_tree_climb.json"))
         step_ms = sorted(blocks)
         out = {
@@ -356,7 +354,7 @@ def main():
                                             f"{evals_per_sweep} candidates per launch, the exhaustive "
                                             f"scan this kernel reproduces bit for bit",
                          "pmc": (pmc or {}).get("derived"),
-                         "pmc_source": "profiles/r02c_pmc_tree_final.json (rocprofv3 --pmc, "
+                         "pmc_source": "profiles/r02b_pmc_tree_final.json (rocprofv3 --pmc, "
                                        "tools/pmc.sh + tools/pmc_summary.py, same sweeps)"},
         }
         out.update(legs)

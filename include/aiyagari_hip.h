@@ -255,7 +255,7 @@ int aiy_ws_set_persistent(aiy_ws* ws, int persistent);
  * descending asset order (one wave per tile).  Results are identical for every value in
  * [-1, 16383].
  * -1 (default): chosen by size — Na <= 4096: 2 cooperating waves per tile (A1), 4 with bit 12
- * (labour); else 8192 (A1) or 16 (labour). */
+ * (labour); else 16. */
 int aiy_ws_set_variant(aiy_ws* ws, int variant);
 
 /* A1 on device.  hint (nullable, [N][Na] int32 0-based) = previous sweep's argmax; the result
