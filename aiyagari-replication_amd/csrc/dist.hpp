@@ -3,6 +3,13 @@
 #include <hip/hip_runtime.h>
 
 namespace aiy {
+// Summation order of a destination's mass (the A10 definition, restated by the C oracle
+// orc_dist_*): the terms landing in (i, k), in ascending source j, are summed sequentially in
+// chunks of kDistChunk consecutive terms and the chunk sums are summed sequentially.  A run of
+// at most kDistChunk terms is the plain sequential sum; a long run (the borrowing constraint,
+// the top of the grid) has a dependent chain of ≈ L/G + G additions instead of L.
+constexpr int kDistChunk = 32;
+
 struct DistArgs {
     int N, Na;
     bool lottery;        // off-grid policy (kp) split between bracketing nodes
@@ -12,14 +19,18 @@ struct DistArgs {
     const double* P;     // row-major
     const double* lam;   // [N][Na]
     double* out;         // λ' [N][Na]
-    int* key;            // scratch [N][Na]
-    int* head;           // scratch [N][Na]
-    double* wr;          // scratch [N][Na]
-    double* mass;        // scratch [N][Na]
+    int* key;            // plan [N][Na]: destination key of source j
+    int* off;            // plan [N][Na+1]: off(i,k) = #{j : key(i,j) < k} (monotone keys)
+    double* wr;          // plan [N][Na]: lottery weight of the upper node
+    double* mass;        // scratch [N][Na] (non-monotone fallback only)
     unsigned long long* diff;  // [2*kDiffSlots]
     unsigned* flags;     // bit 0 non-monotone policy, bit 1 index out of range
 };
-int launch_dist_update(const DistArgs& A, bool fallback, hipStream_t st);
+// the policy's plan (keys, lottery weights, run offsets, flags) — once per policy
+int launch_dist_prepare(const DistArgs& A, hipStream_t st);
+// one push λ → λ' with max|λ'−λ| into A.diff (which the caller has cleared): one fused launch
+// on a monotone plan, the ordered-scan gather + projection otherwise
+int launch_dist_push(const DistArgs& A, bool fallback, hipStream_t st);
 int launch_dist_capital(const double* lam, const double* a, int N, int Na, double* part,
                         double* out, hipStream_t st);
 }  // namespace aiy

@@ -1,7 +1,17 @@
-// A10 entry points: aiy_dist_update_dev (one histogram push on device) and
-// aiy_dist_stationary (MATLAB layouts, iterate to the fixed point, K = Σ λ·a).
+// A10 entry points: aiy_dist_update_dev (one histogram push on device),
+// aiy_dist_stationary_dev (iterate to the fixed point on device) and aiy_dist_stationary
+// (MATLAB layouts, K = Σ λ·a).
+//
+// The policy is fixed across the fixed-point iteration, so its plan (keys, lottery weights,
+// run offsets, the monotonicity flag) is built ONCE per call and read back once; every push is
+// then one launch (dist_push_kernel).  The iteration runs in speculative batches as the VFI
+// and EGM solves do: m pushes are enqueued between reads — push g reads ring slot (g−1) mod R
+// and writes slot g mod R, its max|Δλ| lands in its own slot set — and one D2H read per batch
+// finds the first push with max|Δλ| < tol.  Pushes are deterministic, so the iteration count,
+// the returned λ and dist are exactly the one-read-per-push loop's.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <mutex>
@@ -14,10 +24,12 @@
 
 namespace aiy {
 
+constexpr int kDistSpecMax = 32;  // pushes per convergence read
+
 static int ensure_dist(aiy_ws* ws) {
-    size_t n = (size_t)ws->N * ws->Na;
+    const size_t n = (size_t)ws->N * ws->Na;
     if (!ws->d_key) AIY_HIP(hipMalloc((void**)&ws->d_key, n * sizeof(int)));
-    if (!ws->d_head) AIY_HIP(hipMalloc((void**)&ws->d_head, n * sizeof(int)));
+    if (!ws->d_off) AIY_HIP(hipMalloc((void**)&ws->d_off, (n + ws->N) * sizeof(int)));
     if (!ws->d_wr) AIY_HIP(hipMalloc((void**)&ws->d_wr, n * sizeof(double)));
     if (!ws->d_mass) AIY_HIP(hipMalloc((void**)&ws->d_mass, n * sizeof(double)));
     if (!ws->d_part) AIY_HIP(hipMalloc((void**)&ws->d_part, 260 * sizeof(double)));
@@ -29,33 +41,43 @@ static int ensure_dist(aiy_ws* ws) {
     return AIY_OK;
 }
 
-// one push λ → λ'; *d_out = max|λ'−λ| (host, synchronising) when d_out != nullptr
+// the policy's plan; *fallback = the policy is not monotone (ordered-scan gather).
+// Synchronises once to read the flags.
+static int dist_plan(aiy_ws* ws, const int* idx, const double* kp, const double* a,
+                     const double* P, DistArgs* A, bool* fallback, hipStream_t st) {
+    if (!ws || !a || !P || (!idx && !kp))
+        return fail(AIY_BAD_ARG, "NULL argument (need policy_idx or policy_k)");
+    if (ws->N > 16) return fail(AIY_BAD_SHAPE, "histogram kernels support N <= 16");
+    AIY_TRY(ensure_dist(ws));
+    *A = DistArgs{};
+    A->N = (int)ws->N; A->Na = (int)ws->Na; A->lottery = (idx == nullptr);
+    A->idx = idx; A->kp = kp; A->a = a; A->P = P;
+    A->key = ws->d_key; A->off = ws->d_off; A->wr = ws->d_wr; A->mass = ws->d_mass;
+    A->diff = ws->diff; A->flags = (unsigned*)ws->gi;
+    AIY_HIP(hipMemsetAsync(ws->gi, 0, sizeof(int), st));
+    AIY_TRY(launch_dist_prepare(*A, st));
+    AIY_HIP(hipMemcpyAsync(&ws->hdiff[2 * kDiffSlots], ws->gi, sizeof(int), hipMemcpyDeviceToHost, st));
+    AIY_HIP(hipStreamSynchronize(st));
+    const unsigned flags = (unsigned)ws->hdiff[2 * kDiffSlots];
+    if (flags & 2u) return fail(AIY_BAD_ARG, "policy index outside [1, Na]");
+    *fallback = (flags & 1u) != 0;
+    return AIY_OK;
+}
+
+// one push λ → λ'; *d_host = max|λ'−λ| (synchronising) when d_host != nullptr
 int dist_update_dev(aiy_ws* ws, const double* lam, const int* idx, const double* kp,
                     const double* a, const double* P, double* out, double* diff_dev,
                     double* d_host, hipStream_t st) {
-    if (!ws || !lam || !a || !P || !out || (!idx && !kp))
-        return fail(AIY_BAD_ARG, "NULL argument (need policy_idx or policy_k)");
-    AIY_TRY(ensure_dist(ws));
-    DistArgs A{};
-    A.N = (int)ws->N; A.Na = (int)ws->Na; A.lottery = (idx == nullptr);
-    A.idx = idx; A.kp = kp; A.a = a; A.P = P; A.lam = lam; A.out = out;
-    A.key = ws->d_key; A.head = ws->d_head; A.wr = ws->d_wr; A.mass = ws->d_mass;
-    A.diff = ws->diff; A.flags = (unsigned*)ws->gi;
+    if (!lam || !out) return fail(AIY_BAD_ARG, "NULL argument");
+    DistArgs A;
+    bool fb = false;
+    AIY_TRY(dist_plan(ws, idx, kp, a, P, &A, &fb, st));
+    A.lam = lam;
+    A.out = out;
     AIY_HIP(hipMemsetAsync(ws->diff, 0, 2 * kDiffSlots * sizeof(unsigned long long), st));
-    AIY_HIP(hipMemsetAsync(ws->gi, 0, sizeof(int), st));
     AIY_TRY(ws_timing_begin(ws, st));
-    AIY_TRY(launch_dist_update(A, false, st));
+    AIY_TRY(launch_dist_push(A, fb, st));
     AIY_TRY(ws_timing_end(ws, st));
-    // flags decide whether the exact fallback must run: read them (synchronises)
-    unsigned flags = 0;
-    AIY_HIP(hipMemcpyAsync(&ws->hdiff[2 * kDiffSlots], ws->gi, sizeof(int), hipMemcpyDeviceToHost, st));
-    AIY_HIP(hipStreamSynchronize(st));
-    flags = (unsigned)ws->hdiff[2 * kDiffSlots];
-    if (flags & 2u) return fail(AIY_BAD_ARG, "policy index outside [1, Na]");
-    if (flags & 1u) {  // non-monotone policy: redo the gather by exhaustive ordered scans
-        AIY_HIP(hipMemsetAsync(ws->diff, 0, 2 * kDiffSlots * sizeof(unsigned long long), st));
-        AIY_TRY(launch_dist_update(A, true, st));
-    }
     if (diff_dev) AIY_TRY(launch_reduce_slots(ws->diff, diff_dev, st));
     if (d_host) {
         AIY_HIP(hipMemcpyAsync(ws->hdiff, ws->diff, 2 * kDiffSlots * sizeof(unsigned long long),
@@ -63,6 +85,74 @@ int dist_update_dev(aiy_ws* ws, const double* lam, const int* idx, const double*
         AIY_HIP(hipStreamSynchronize(st));
         *d_host = fold_slots_host(ws->hdiff);
     }
+    return AIY_OK;
+}
+
+// the fixed-point loop of aiy_dist_stationary on device:  for it = 1..max_iter: push; stop
+// when max|Δλ| < tol.  lam_out receives the last push; k_dev (nullable) = Σ λ·a.
+int dist_stationary_dev(aiy_ws* ws, const double* lam0, const int* idx, const double* kp,
+                        const double* a, const double* P, double tol, int64_t max_iter,
+                        double* lam_out, double* k_dev, int64_t* iters, double* dist,
+                        hipStream_t st) {
+    if (!lam0 || !lam_out || !iters || !dist) return fail(AIY_BAD_ARG, "NULL argument");
+    if (max_iter < 1) return fail(AIY_BAD_ARG, "max_iter must be >= 1");
+    DistArgs A0;
+    bool fb = false;
+    AIY_TRY(dist_plan(ws, idx, kp, a, P, &A0, &fb, st));
+    const int M = kDistSpecMax, R = M + 1;
+    const size_t n = (size_t)ws->N * ws->Na, nb = n * sizeof(double);
+    const int SW = 2 * kDiffSlots;
+    if (ws->dist_n != n || ws->dist_m != M) {
+        ws->free_dist_spec();
+        AIY_HIP(hipMalloc((void**)&ws->dist_ring, (size_t)R * nb));
+        AIY_HIP(hipMalloc((void**)&ws->dist_slots, (size_t)M * SW * sizeof(unsigned long long)));
+        AIY_HIP(hipHostMalloc((void**)&ws->dist_hslots, (size_t)M * SW * sizeof(unsigned long long)));
+        ws->dist_n = n;
+        ws->dist_m = M;
+    }
+    auto slot = [&](int64_t g) { return ws->dist_ring + (size_t)(g % R) * n; };
+    AIY_HIP(hipMemcpyAsync(slot(0), lam0, nb, hipMemcpyDeviceToDevice, st));
+    int64_t done = 0, stop = 0;
+    double d_prev = NAN, d_last = NAN, d_stop = NAN;
+    while (!stop && done < max_iter) {
+        int64_t m = M;
+        if (d_last == d_last && d_prev == d_prev && d_last < d_prev && d_last > 0 && tol > 0) {
+            const double need = std::ceil(std::log(tol / d_last) / std::log(d_last / d_prev));
+            if (need >= 1 && need < (double)m) m = (int64_t)need;
+        }
+        m = std::min<int64_t>(std::max<int64_t>(m, 1), max_iter - done);
+        AIY_HIP(hipMemsetAsync(ws->dist_slots, 0, (size_t)m * SW * sizeof(unsigned long long), st));
+        for (int64_t t = 0; t < m; ++t) {
+            DistArgs A = A0;
+            A.lam = slot(done + t);
+            A.out = slot(done + t + 1);
+            A.diff = ws->dist_slots + (size_t)t * SW;
+            AIY_TRY(ws_timing_begin(ws, st));
+            AIY_TRY(launch_dist_push(A, fb, st));
+            AIY_TRY(ws_timing_end(ws, st));
+        }
+        AIY_HIP(hipMemcpyAsync(ws->dist_hslots, ws->dist_slots,
+                               (size_t)m * SW * sizeof(unsigned long long),
+                               hipMemcpyDeviceToHost, st));
+        AIY_HIP(hipStreamSynchronize(st));
+        for (int64_t t = 0; t < m; ++t) {
+            const double d = fold_slots_host(ws->dist_hslots + (size_t)t * SW);
+            d_prev = d_last;
+            d_last = d;
+            d_stop = d;
+            if (d < tol) {
+                stop = done + 1 + t;
+                break;
+            }
+        }
+        if (!stop) done += m;
+    }
+    const int64_t g = stop ? stop : done;
+    AIY_HIP(hipMemcpyAsync(lam_out, slot(g), nb, hipMemcpyDeviceToDevice, st));
+    if (k_dev)
+        AIY_TRY(launch_dist_capital(lam_out, a, (int)ws->N, (int)ws->Na, ws->d_part, k_dev, st));
+    *iters = g;
+    *dist = d_stop;
     return AIY_OK;
 }
 
@@ -77,6 +167,14 @@ int aiy_dist_update_dev(aiy_ws* ws, const double* lambda, const int32_t* policy_
                         double* lambda_out, double* diff, void* stream) {
     return dist_update_dev(ws, lambda, policy_idx, policy_k, a_grid, P, lambda_out, diff,
                            nullptr, (hipStream_t)stream);
+}
+
+int aiy_dist_stationary_dev(aiy_ws* ws, const double* lambda, const int32_t* policy_idx,
+                            const double* policy_k, const double* a_grid, const double* P,
+                            double tol, int64_t max_iter, double* lambda_out,
+                            double* k_supply, int64_t* iters, double* dist, void* stream) {
+    return dist_stationary_dev(ws, lambda, policy_idx, policy_k, a_grid, P, tol, max_iter,
+                               lambda_out, k_supply, iters, dist, (hipStream_t)stream);
 }
 
 int aiy_dist_stationary(const int32_t* policy_idx, const double* policy_k, int vfi_layout,
@@ -123,18 +221,10 @@ int aiy_dist_stationary(const int32_t* policy_idx, const double* policy_k, int v
     to_rows(lambda);
     AIY_HIP(hipMemcpyAsync(dl0, rows.data(), nb, hipMemcpyHostToDevice, c->st));
     double d = NAN;
-    int64_t it;
-    double* cur = dl0;
-    double* nxt = dl1;
-    for (it = 1; it <= max_iter; ++it) {
-        AIY_TRY(dist_update_dev(c->ws, cur, didx, dkp, da, dP, nxt, nullptr, &d, c->st));
-        std::swap(cur, nxt);
-        if (d < tol) break;
-    }
-    if (it > max_iter) it = max_iter;
-    AIY_TRY(ensure_dist(c->ws));
-    AIY_TRY(launch_dist_capital(cur, da, (int)N, (int)Na, c->ws->d_part, dK, c->st));
-    AIY_HIP(hipMemcpyAsync(rows.data(), cur, nb, hipMemcpyDeviceToHost, c->st));
+    int64_t it = 0;
+    AIY_TRY(dist_stationary_dev(c->ws, dl0, didx, dkp, da, dP, tol, max_iter, dl1, dK, &it, &d,
+                                c->st));
+    AIY_HIP(hipMemcpyAsync(rows.data(), dl1, nb, hipMemcpyDeviceToHost, c->st));
     AIY_HIP(hipMemcpyAsync(k_supply, dK, sizeof(double), hipMemcpyDeviceToHost, c->st));
     AIY_HIP(hipStreamSynchronize(c->st));
     if (vfi_layout) rows_to_cm(rows.data(), N, Na, lambda);

@@ -4,25 +4,29 @@
 // Scatter-free transpose-gather.  The policy maps j to a destination key k(j) (the grid index
 // for a VFI policy; the bracket of a' for an off-grid EGM policy, whose mass is split between
 // k and k+1 as a lottery).  Optimal policies are monotone in j (increasing differences,
-// Topkis), so each key's preimage is ONE contiguous run of j.  Then:
-//   heads   (per (i,j))  the first j of every run records itself in head[i][k]; a decrease of
-//                        k(j) raises a flag (non-monotone policy → exact fallback kernel).
-//   gather  (per (i,k))  one thread walks the run(s) ending in slot k in ascending j and
-//                        accumulates — the same additions, in the same order, as the
-//                        sequential scatter `mass[k(j)] += λ_j` of the C oracle, so the result
-//                        is bit-identical, with no atomics and no cancellation.
-//   project (per (m,k))  λ'(m,k) = Σ_i P(i,m)·mass(i,k) in i order, plus max|λ'−λ| (slots).
-// Fallback (per (i,k), only when the flag is set): scan every j of the row in order.
+// Topkis), so each key's preimage is ONE contiguous run of j, and the runs of consecutive keys
+// are adjacent: the whole policy is a CSR offset row per productivity state,
+// off(i,k) = #{j : k(i,j) < k}.
+//   prepare (once per policy)  keys, lottery weights, offsets (binary search of the key row),
+//                              flags: non-monotone keys, index out of range.
+//   push (one launch per push) a workgroup owns 64 destinations k and all N states: wave i
+//                              gathers mass(i,k) from its run(s) (no atomics), LDS, then wave
+//                              m projects λ'(m,k) = Σ_i P(i,m)·mass(i,k) in i order and folds
+//                              max|λ'−λ| into the diff slots.
+// The terms of a destination are summed in the order dist.hpp defines (ascending j, chunks of
+// kDistChunk): runs of ≤ 32 terms are summed by their own lane; a longer run is split over the
+// wave, one chunk per lane, and its chunk sums are folded in order — so the borrowing-
+// constraint run does not serialise a lane for hundreds of dependent additions.
+// Fallback (non-monotone policy): one thread per (i,k) scans the row in order, same chunking.
 #include "aiy_common.hpp"
 #include "dist.hpp"
 
 namespace aiy {
 
 __global__ void dist_keys_kernel(DistArgs A) {
-    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= A.N * A.Na) return;
     const int Na = A.Na;
-    int i = t / Na, j = t - i * Na;
     int key;
     if (A.lottery) {
         double x = A.kp[t];
@@ -39,81 +43,141 @@ __global__ void dist_keys_kernel(DistArgs A) {
         }
     }
     A.key[t] = key;
-    (void)i;
-    (void)j;
 }
 
-__global__ void dist_heads_kernel(DistArgs A) {
-    int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= A.N * A.Na) return;
-    const int Na = A.Na;
-    int i = t / Na, j = t - i * Na;
-    int key = A.key[t];
-    int prev = j > 0 ? A.key[t - 1] : -1;
-    if (key != prev) {
-        if (key < prev) atomicOr(A.flags, 1u);  // not monotone: a key may have several runs
-        A.head[(size_t)i * Na + key] = j;
+// off(i,k) for k = 0..Na (lower bound of k in the key row) + the monotonicity check
+__global__ void dist_offsets_kernel(DistArgs A) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int Na = A.Na, W = Na + 1;
+    if (t >= A.N * W) return;
+    const int i = t / W, k = t - i * W;
+    const int* __restrict__ row = A.key + (size_t)i * Na;
+    if (k >= 1 && k < Na && row[k - 1] > row[k]) atomicOr(A.flags, 1u);
+    int lo = 0, hi = Na;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (row[mid] < k) lo = mid + 1;
+        else hi = mid;
     }
+    A.off[t] = lo;
 }
 
-// one thread per (i, k): accumulate the run(s) that land in slot k, ascending j
-__global__ void dist_gather_kernel(DistArgs A) {
-    int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= A.N * A.Na) return;
-    const int Na = A.Na;
-    int i = t / Na, k = t - i * Na;
-    const int* __restrict__ key = A.key + (size_t)i * Na;
+// term of source j for a destination whose lottery run of the node below ends at js
+template <bool LOT>
+__device__ __forceinline__ double dist_term(const double* __restrict__ lam,
+                                            const double* __restrict__ wr, int j, int js) {
+    if (!LOT) return lam[j];
+    const double w = wr[j];
+    return j < js ? lam[j] * w : lam[j] * (1 - w);
+}
+
+// sequential sum of the terms of sources [b, e) (e − b ≤ kDistChunk), 8 loads in flight
+template <bool LOT>
+__device__ __forceinline__ double dist_chunk(const double* __restrict__ lam,
+                                             const double* __restrict__ wr, int b, int e,
+                                             int js) {
+    double part = 0.0;
+    for (int t0 = b; __ballot(t0 < e) != 0ull; t0 += 8) {  // wave-uniform trip count
+        double x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = (t0 + u < e) ? dist_term<LOT>(lam, wr, t0 + u, js) : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (t0 + u < e) part = part + x[u];
+    }
+    return part;
+}
+
+template <bool LOT>
+__global__ __launch_bounds__(1024) void dist_push_kernel(DistArgs A) {
+    __shared__ double s_mass[16][64];
+    const int lane = threadIdx.x & 63, i = threadIdx.x >> 6;  // blockDim = 64·N
+    const int N = A.N, Na = A.Na;
+    const int k = blockIdx.x * 64 + lane;
+    const bool ok = k < Na;
+    const int* __restrict__ off = A.off + (size_t)i * (Na + 1);
     const double* __restrict__ lam = A.lam + (size_t)i * Na;
-    const int* __restrict__ head = A.head + (size_t)i * Na;
-    double acc = 0.0;
-    if (A.lottery) {
-        const double* __restrict__ wr = A.wr + (size_t)i * Na;
-        if (k >= 1) {
-            int h = head[k - 1];
-            if (h >= 0)
-                for (int j = h; j < Na && key[j] == k - 1; ++j) acc = acc + lam[j] * wr[j];
-        }
-        int h = head[k];
-        if (h >= 0)
-            for (int j = h; j < Na && key[j] == k; ++j) acc = acc + lam[j] * (1 - wr[j]);
-    } else {
-        int h = head[k];
-        if (h >= 0)
-            for (int j = h; j < Na && key[j] == k; ++j) acc = acc + lam[j];
+    const double* __restrict__ wr = LOT ? A.wr + (size_t)i * Na : nullptr;
+    int jb = 0, js = 0, je = 0;
+    if (ok) {
+        js = off[k];
+        je = off[k + 1];
+        jb = (LOT && k > 0) ? off[k - 1] : js;
     }
-    A.mass[t] = acc;
+    const int L = je - jb;
+    constexpr int G = kDistChunk;
+    // short runs: the lane's own sequential sum (== the chunked sum for L <= G)
+    double tot = dist_chunk<LOT>(lam, wr, jb, L <= G ? je : jb, js);
+    // long runs, one at a time: lane c sums chunks c, c + 64, ...; the chunk sums are folded
+    // in chunk order with wave-uniform reads
+    unsigned long long lm = __ballot(L > G);
+    while (lm) {
+        const int q = __builtin_ctzll(lm);
+        lm &= lm - 1;
+        const int qb = readlane_i(jb, q), qs = readlane_i(js, q), qL = readlane_i(L, q);
+        const int nch = (qL + G - 1) / G;
+        double total = 0.0;
+        for (int c0 = 0; c0 < nch; c0 += 64) {
+            const int c = c0 + lane;
+            const int b = qb + c * G;
+            const int e = c < nch ? min(b + G, qb + qL) : b;
+            const double part = dist_chunk<LOT>(lam, wr, b, e, qs);
+            const int nc = min(64, nch - c0);
+            for (int u = 0; u < nc; ++u) total = total + readlane_d(part, u);
+        }
+        if (lane == q) tot = total;
+    }
+    s_mass[i][lane] = tot;
+    __syncthreads();
+    const int m = i;
+    double d = 0.0;
+    bool okd = false;
+    if (ok) {
+        double acc = 0.0;
+        for (int q = 0; q < N; ++q) acc = acc + A.P[q * N + m] * s_mass[q][lane];
+        const size_t t = (size_t)m * Na + k;
+        A.out[t] = acc;
+        d = fabs(acc - A.lam[t]);
+        okd = (d == d);
+    }
+    block_max_to_slots(okd, d, A.diff);
 }
 
-// exact fallback for non-monotone policies: every j of the row, in order
+// exact fallback for non-monotone policies: every j of the row, in order, chunked as above
 __global__ void dist_gather_scan_kernel(DistArgs A) {
-    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= A.N * A.Na) return;
     const int Na = A.Na;
-    int i = t / Na, k = t - i * Na;
+    const int i = t / Na, k = t - i * Na;
     const int* __restrict__ key = A.key + (size_t)i * Na;
     const double* __restrict__ lam = A.lam + (size_t)i * Na;
-    double acc = 0.0;
-    if (A.lottery) {
-        const double* __restrict__ wr = A.wr + (size_t)i * Na;
-        for (int j = 0; j < Na; ++j) {
-            int q = key[j];
-            if (q == k) acc = acc + lam[j] * (1 - wr[j]);
-            else if (q + 1 == k) acc = acc + lam[j] * wr[j];
+    const double* __restrict__ wr = A.lottery ? A.wr + (size_t)i * Na : nullptr;
+    double total = 0.0, part = 0.0;
+    int n = 0;
+    for (int j = 0; j < Na; ++j) {
+        const int q = key[j];
+        double x;
+        if (q == k) x = A.lottery ? lam[j] * (1 - wr[j]) : lam[j];
+        else if (A.lottery && q + 1 == k) x = lam[j] * wr[j];
+        else continue;
+        part = part + x;
+        if (++n == kDistChunk) {
+            total = total + part;
+            part = 0.0;
+            n = 0;
         }
-    } else {
-        for (int j = 0; j < Na; ++j)
-            if (key[j] == k) acc = acc + lam[j];
     }
-    A.mass[t] = acc;
+    if (n) total = total + part;
+    A.mass[t] = total;
 }
 
 __global__ void dist_project_kernel(DistArgs A) {
-    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
     bool ok = false;
     double d = 0.0;
     if (t < A.N * A.Na) {
         const int N = A.N, Na = A.Na;
-        int m = t / Na, k = t - m * Na;
+        const int m = t / Na, k = t - m * Na;
         double acc = 0.0;
         for (int i = 0; i < N; ++i) acc = acc + A.P[i * N + m] * A.mass[(size_t)i * Na + k];
         A.out[t] = acc;
@@ -128,7 +192,7 @@ __global__ void dist_capital_kernel(const double* __restrict__ lam, const double
                                     int N, int Na, double* __restrict__ part) {
     __shared__ double sh[256];
     double acc = 0.0;
-    int n = N * Na;
+    const int n = N * Na;
     for (int t = blockIdx.x * 256 + threadIdx.x; t < n; t += gridDim.x * 256)
         acc = acc + lam[t] * a[t % Na];
     sh[threadIdx.x] = acc;
@@ -147,18 +211,26 @@ __global__ void fold_kernel(const double* __restrict__ part, int n, double* __re
     }
 }
 
-int launch_dist_update(const DistArgs& A, bool fallback, hipStream_t st) {
-    int n = A.N * A.Na;
-    int g = (n + 255) / 256;
+int launch_dist_prepare(const DistArgs& A, hipStream_t st) {
+    const int n = A.N * A.Na, nw = A.N * (A.Na + 1);
+    dist_keys_kernel<<<(n + 255) / 256, 256, 0, st>>>(A);
+    dist_offsets_kernel<<<(nw + 255) / 256, 256, 0, st>>>(A);
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
+}
+
+int launch_dist_push(const DistArgs& A, bool fallback, hipStream_t st) {
+    if (A.N < 1 || A.N > 16) return fail(AIY_BAD_SHAPE, "histogram kernels support N <= 16");
+    const int n = A.N * A.Na;
     if (!fallback) {
-        AIY_HIP(hipMemsetAsync(A.head, 0xff, sizeof(int) * (size_t)n, st));
-        dist_keys_kernel<<<g, 256, 0, st>>>(A);
-        dist_heads_kernel<<<g, 256, 0, st>>>(A);
-        dist_gather_kernel<<<g, 256, 0, st>>>(A);
+        const int g = (A.Na + 63) / 64;
+        if (A.lottery) dist_push_kernel<true><<<g, 64 * A.N, 0, st>>>(A);
+        else dist_push_kernel<false><<<g, 64 * A.N, 0, st>>>(A);
     } else {
+        const int g = (n + 255) / 256;
         dist_gather_scan_kernel<<<g, 256, 0, st>>>(A);
+        dist_project_kernel<<<g, 256, 0, st>>>(A);
     }
-    dist_project_kernel<<<g, 256, 0, st>>>(A);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }

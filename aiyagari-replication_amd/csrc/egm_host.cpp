@@ -185,7 +185,7 @@ static int egm_host(double* pc, const double* a, const double* s, const double* 
         AIY_TRY(read_egm(c->ws, c->st, &d));
         cur = nxt;
         it = 1;
-    } else if (c->ws->spec_max > 1 && max_iter > 0) {
+    } else if (c->ws->spec_max > 1 && max_iter > 0 && d > tol) {  // :74 tests dist = 1 first
         AIY_TRY(ensure_egm(c->ws));
         const EgmArgs A = egm_args(c->ws, cur, da, ds, dP, r, w, beta, sigma, amin, labor, phi,
                                    theta, nxt, dpk, labor ? dpl : nullptr);

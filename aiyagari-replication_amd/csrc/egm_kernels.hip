@@ -39,8 +39,8 @@ __global__ __launch_bounds__(1024) void egm_rhs_kernel(EgmArgs A) {
     const int N = A.N, Na = A.Na;
     const int a_i = blockIdx.x * 64 + lane;
     const bool ok = a_i < Na;
-    if (blockIdx.x == 0) {
-        if (threadIdx.x < 2 * kDiffSlots) A.diff[threadIdx.x] = 0ull;
+    if (blockIdx.x == 0) {  // blockDim = 64·N may be smaller than the 2·kDiffSlots words
+        for (int q = threadIdx.x; q < 2 * kDiffSlots; q += blockDim.x) A.diff[q] = 0ull;
         if (threadIdx.x == 0) *A.flags = 0u;
     }
     s_up[m][lane] = ok ? uprime_dev(A.c[(size_t)m * Na + a_i], A.sigma, A.ns) : 0.0;

@@ -45,6 +45,10 @@ int launch_ks_improve(const KsArgs& A, const double* V, const double* dV, double
                       int* nfev, hipStream_t st);
 int launch_ks_howard(const KsArgs& A, const double* V, const double* dV, const double* kopt,
                      double* Vn, hipStream_t st);
+// Howard sweep writing the next sweep's slopes too (dV must hold the slopes of V on every
+// column the launch reads; Vn and dVn are written on the launch's nodes)
+int launch_ks_howard_slopes(const KsArgs& A, const double* V, const double* dV,
+                            const double* kopt, double* Vn, double* dVn, hipStream_t st);
 int launch_ks_hints(const KsArgs& A, const double* kopt, hipStream_t st);
 int launch_ks_reldiff(const KsArgs& A, const double* V, const double* Vold,
                       unsigned long long* slots, hipStream_t st);

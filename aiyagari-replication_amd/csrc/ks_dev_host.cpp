@@ -152,6 +152,23 @@ int ks_dev_howard(ks_dev* h, const double* V, const double* kopt, double* Vout, 
     return AIY_OK;
 }
 
+// the pchip slopes of every column h's sweep reads (own columns and forecast targets) into
+// the caller's dV (full k x K x S); what a fused sweep needs before its first launch
+int ks_dev_slopes(ks_dev* h, const double* V, double* dV, void* stream) {
+    if (!h || !V || !dV) return fail(AIY_BAD_ARG, "NULL argument");
+    return launch_ks_slopes_cols(shard_args(h), h->cols, h->ncols, V, dV, (hipStream_t)stream);
+}
+
+// one Jacobi Howard sweep on h's nodes that also writes the next sweep's slopes: reads V and
+// dV (slopes of V on every column h reads), writes Vout and dVout on h's nodes
+int ks_dev_howard_fused(ks_dev* h, const double* V, const double* dV, const double* kopt,
+                        double* Vout, double* dVout, void* stream) {
+    if (!h || !V || !dV || !kopt || !Vout || !dVout) return fail(AIY_BAD_ARG, "NULL argument");
+    if (V == Vout || dV == dVout)
+        return fail(AIY_BAD_ARG, "Howard sweeps are Jacobi: V/Vout and dV/dVout must differ");
+    return launch_ks_howard_slopes(shard_args(h), V, dV, kopt, Vout, dVout, (hipStream_t)stream);
+}
+
 // max over the shard's nodes of |V - Vold| / (|Vold| + 1e-10), NaN ignored (:195).
 // out (device, 2 x uint64): {IEEE bits of the max, nonzero if any node was not NaN}
 int ks_dev_reldiff(ks_dev* h, const double* V, const double* Vold, void* out, void* stream) {

@@ -219,6 +219,51 @@ __global__ void ks_howard_kernel(KsArgs A, const double* __restrict__ V,
     }
 }
 
+// Howard sweep + the NEXT sweep's pchip slopes in one launch (the .Values refresh of
+// :186-191 fused into the sweep that produces the values).  A block owns O consecutive k
+// nodes of a column and evaluates the sweep on [q0 − 2, q0 + O + 2) (the neighbours the
+// slopes of its own nodes read, end rules included), stages those values in LDS and writes
+// value and slope of its own nodes — the same formulas on the same values as
+// ks_howard_kernel + ks_slopes_kernel, so bit for bit the two-launch sweep.  Columns of
+// length <= blockDim are one block each (O = nk: nothing evaluated twice); longer columns
+// evaluate 4 of every 256 nodes twice.
+__global__ __launch_bounds__(256) void ks_howard_slopes_kernel(KsArgs A, const double* __restrict__ V,
+                                                               const double* __restrict__ dV,
+                                                               const double* __restrict__ k_opt,
+                                                               double* __restrict__ Vn,
+                                                               double* __restrict__ dVn, int O) {
+    __shared__ double s_v[256];
+    const int nk = A.nk;
+    const int q0 = blockIdx.x * O;
+    const int lo = q0 >= 2 ? q0 - 2 : 0;
+    const int own_hi = min(nk, q0 + O);
+    const int hi = min(nk, q0 + O + 2);
+    const int q = lo + (int)threadIdx.x;
+    const bool comp = q < hi, mine = q >= q0 && q < own_hi;
+    const int col0 = A.node0 / nk + (int)blockIdx.z * (A.sstride / nk);  // block-uniform
+    const int ncl = A.n_local / nk;
+    KsView W{A.k_grid, V, dV};
+    const double k = comp ? W.kg[q] : 0.0;
+    const LdsCol yl{s_v, lo};
+    for (int y = blockIdx.y; y < ncl; y += gridDim.y) {  // block-uniform trip count
+        const int col = col0 + y;
+        const int si = col / A.nK;
+        const size_t n = (size_t)col * nk + q;
+        double v = 0.0;
+        if (comp) {
+            const KsSlice sl = A.slice[col];
+            v = ks_bellman_dev(A, W, sl, si, k, k_opt[n], A.seg_hint ? A.seg_hint[n] : -1);
+        }
+        s_v[threadIdx.x] = v;
+        __syncthreads();
+        if (mine) {
+            Vn[n] = v;
+            dVn[n] = pchip_slope_t(A.k_grid, yl, nk, q);
+        }
+        __syncthreads();
+    }
+}
+
 // the segment hints of the shard's nodes from k_opt (what ks_improve_kernel stores), for nodes
 // whose k_opt arrived from another rank (ks_dist.py ghost columns)
 __global__ void ks_hints_kernel(KsArgs A, const double* __restrict__ k_opt) {
@@ -397,6 +442,18 @@ int launch_ks_howard(const KsArgs& A, const double* V, const double* dV, const d
         return fail(AIY_BAD_SHAPE, "Howard launch: node range must be whole columns");
     ks_howard_kernel<<<ks_col_grid(A.nk, A.n_local / A.nk, A.ns), ks_col_block(A.nk), 0, st>>>(
         A, V, dV, kopt, Vn);
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
+}
+int launch_ks_howard_slopes(const KsArgs& A, const double* V, const double* dV,
+                            const double* kopt, double* Vn, double* dVn, hipStream_t st) {
+    if (A.node0 % A.nk || A.n_local % A.nk || (A.ns > 1 && A.sstride % A.nk))
+        return fail(AIY_BAD_SHAPE, "Howard launch: node range must be whole columns");
+    const int B = (int)ks_col_block(A.nk).x;  // 64 .. 256
+    const int O = A.nk <= B ? A.nk : B - 4;
+    const dim3 g(cdiv(A.nk, O), (unsigned)std::max(1, std::min(A.n_local / A.nk, 65535)),
+                 std::max(A.ns, 1));
+    ks_howard_slopes_kernel<<<g, B, 0, st>>>(A, V, dV, kopt, Vn, dVn, O);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }

@@ -8,9 +8,10 @@ namespace aiy {
 
 __device__ __forceinline__ int sgn_dev(double x) { return (x > 0) - (x < 0); }
 
-// pchip slope at point q of a column (x = k_grid), MATLAB pchipslopes
-__device__ inline double pchip_slope(const double* __restrict__ x, const double* __restrict__ y, int n,
-                              int q) {
+// pchip slope at point q of a column (x = k_grid), MATLAB pchipslopes.  y is anything
+// indexable by the column's node index: a column pointer, or a window staged in LDS (LdsCol).
+template <class Y>
+__device__ inline double pchip_slope_t(const double* __restrict__ x, const Y& y, int n, int q) {
     if (q == 0 || q == n - 1) {
         double h0, h1, e0, e1;
         if (q == 0) {
@@ -42,6 +43,16 @@ __device__ inline double pchip_slope(const double* __restrict__ x, const double*
     }
     return 0.0;
 }
+__device__ inline double pchip_slope(const double* __restrict__ x, const double* __restrict__ y,
+                                     int n, int q) {
+    return pchip_slope_t(x, y, n, q);
+}
+// nodes [lo, lo + len) of a column staged in LDS, indexed by node
+struct LdsCol {
+    const double* p;
+    int lo;
+    __device__ double operator[](int i) const { return p[i - lo]; }
+};
 
 // pwch coefficients + ppval Horner on segment i
 __device__ __forceinline__ double pchip_at(const double* __restrict__ x,

@@ -47,10 +47,23 @@ struct aiy_ws {
     unsigned long long* hdiff = nullptr;     // pinned host [2*kDiffSlots + 4]
     // histogram scratch (A10)
     int* d_key = nullptr;
-    int* d_head = nullptr;
+    int* d_off = nullptr;   // [N][Na+1] run offsets of the policy (the plan)
     double* d_wr = nullptr;
     double* d_mass = nullptr;
     double* d_part = nullptr;
+    // speculative histogram iteration: ring of dist_m + 1 λ buffers, per-push diff slots
+    size_t dist_n = 0;
+    int dist_m = 0;
+    double* dist_ring = nullptr;
+    unsigned long long* dist_slots = nullptr;   // device [dist_m][2*kDiffSlots]
+    unsigned long long* dist_hslots = nullptr;  // pinned host, same shape
+    void free_dist_spec() {
+        if (dist_ring) (void)hipFree(dist_ring);
+        if (dist_slots) (void)hipFree(dist_slots);
+        if (dist_hslots) (void)hipHostFree(dist_hslots);
+        dist_ring = nullptr; dist_slots = nullptr; dist_hslots = nullptr;
+        dist_n = 0; dist_m = 0;
+    }
     // generic scratch used by the EGM / distribution / simulation kernels
     double* g0 = nullptr;
     double* g1 = nullptr;
@@ -127,18 +140,19 @@ struct aiy_ws {
     }
     void free_all() {
         void* ps[] = {EV, T, T32, Dm, Dm8, Dt, Dm512, touched, best0, idx0, mom, dis, kf, partial, diff, hitcount, trace, g0, g1, g2, gi,
-                      d_key, d_head, d_wr, d_mass, d_part, pers};
+                      d_key, d_off, d_wr, d_mass, d_part, pers};
         for (void* p : ps)
             if (p) (void)hipFree(p);
         free_spec();
         free_batch();
         free_egm_spec();
+        free_dist_spec();
         if (hdiff) (void)hipHostFree(hdiff);
         EV = nullptr; T = nullptr; T32 = nullptr; Dm = nullptr; Dm8 = nullptr; Dt = nullptr; Dm512 = nullptr; touched = nullptr; best0 = nullptr; dis = nullptr; kf = nullptr; kf_cap = 0;
         kf_ok = false;
         idx0 = nullptr; mom = nullptr; partial = nullptr; diff = nullptr; hitcount = nullptr; trace = nullptr; trace_cap = 0; hdiff = nullptr;
         g0 = g1 = g2 = nullptr; gi = nullptr; pers = nullptr;
-        d_key = d_head = nullptr; d_wr = d_mass = d_part = nullptr;
+        d_key = d_off = nullptr; d_wr = d_mass = d_part = nullptr;
         partial_cap = 0;
     }
 };

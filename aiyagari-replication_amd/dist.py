@@ -35,3 +35,16 @@ def dist_update_dev(ws, lam, a_grid, P, out, policy_idx=None, policy_k=None, dif
     check(lib().aiy_dist_update_dev(ws.handle, ptr(lam), ptr(policy_idx), ptr(policy_k),
                                     ptr(a_grid), ptr(P), ptr(out), ptr(diff),
                                     stream_handle(stream)))
+
+
+def dist_stationary_dev(ws, lam0, a_grid, P, out, policy_idx=None, policy_k=None, tol=1e-12,
+                        max_iter=10000, k_supply=None, stream=None):
+    """aiy_dist_stationary_dev: the fixed point on device ([N][Na] torch tensors; policy_idx
+    0-based).  `out` receives λ; k_supply (optional 1-element device tensor) Σ λ·a.
+    Returns (iters, dist)."""
+    it, dist = C.c_int64(), C.c_double()
+    check(lib().aiy_dist_stationary_dev(ws.handle, ptr(lam0), ptr(policy_idx), ptr(policy_k),
+                                        ptr(a_grid), ptr(P), d(tol), i64(max_iter), ptr(out),
+                                        ptr(k_supply), C.byref(it), C.byref(dist),
+                                        stream_handle(stream)))
+    return it.value, dist.value

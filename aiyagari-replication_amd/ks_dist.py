@@ -356,8 +356,11 @@ class HowardSweeps:
         return V, V2
 
     def close(self):
+        owned = getattr(self.shard, "_ghosts", None)
         for g in self.shards[1:]:
             g.close()
+            if owned is not None and g in owned:  # one solve per ALM step: do not accumulate
+                owned.remove(g)
         self.shards = self.shards[:1]
 
 

@@ -34,7 +34,8 @@ labor = s * pi_stat;
 
 kmax = delta^(1 / (alpha - 1));
 amax = kmax^alpha + (1 - delta) * kmax;
-amin = -b;
+wmin = (1 - alpha) * (alpha / ((1 / beta - 1) + delta))^(alpha / (1 - alpha));
+amin = min(b, wmin * s(1));           % the borrowing limit of Aiyagari_VFI.m:53-54
 a_grid = amin + (amax - amin) * linspace(0, 1, Na).^2;
 
 wage = @(r) (1 - alpha) * (alpha / (r + delta))^(alpha / (1 - alpha));
@@ -58,7 +59,7 @@ r_history = zeros(n_steps, 1); k_supply = zeros(n_steps, 1); k_demand = zeros(n_
 for step = 1:n_steps
     r = (r_low + r_high) / 2;
     % warm start from the previous solve's v_old (the reference's chained warm start)
-    [v_new, v_old, policy_k, policy_c, iter] = ...
+    [v_new, v_old, policy_k, policy_c, iter, idx] = ...
         aiy_vfi_solve_mex(v_old, a_grid, s, P, r, wage(r), beta, sigma, tol, max_iter);
     [K_s, sim_k] = aiy_sim_capital_mex(policy_k, a_grid, P, z1, k1, rand(T - 1, 1), 1);
     K_d = kdemand(r);
@@ -76,8 +77,8 @@ fprintf('equilibrium r = %.10f after %.3f s\n', r, toc);
 
 % ---------------------------------------------------------------- stationary histogram (A10)
 % the on-grid policy's fixed point on the (z, a) grid: a deterministic alternative to the
-% Monte-Carlo mean (new; the reference has no histogram update)
-[~, idx] = min(abs(policy_k(:, :, 1) - reshape(a_grid, 1, 1, [])), [], 3);
+% Monte-Carlo mean (new; the reference has no histogram update).  idx is the last solve's
+% 1-based argmax, returned by the gateway (policy_k == a_grid(idx)).
 [lambda, K_hist] = aiy_dist_stationary_mex(idx, a_grid, P, ones(N, Na) / (N * Na), 1e-12, ...
                                            10000, 1);
 fprintf('histogram K = %.6f, Monte-Carlo K = %.6f\n', K_hist, K_s);

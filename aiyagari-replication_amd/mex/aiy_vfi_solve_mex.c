@@ -1,10 +1,12 @@
-/* [v_new, v_old, policy_k, policy_c, iter] =
+/* [v_new, v_old, policy_k, policy_c, iter, idx] =
  *     aiy_vfi_solve_mex(v_old, a_grid, s, P, r, w, beta, sigma, tol, max_iter)
  * Replaces Aiyagari_VFI.m:65-90 (and the GE copy :147-171).  Break semantics kept: v_new is
- * the converged iterate, v_old the previous one (the GE loop warm-starts from it). */
+ * the converged iterate, v_old the previous one (the GE loop warm-starts from it).  idx
+ * (optional) is the last sweep's argmax, 1-based as `max` returns it (:79-80), so
+ * policy_k == a_grid(idx). */
 #include "mexcommon.h"
 void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
-    aiy_nargs(nrhs, 10, 10, nlhs, 5, "[v_new,v_old,policy_k,policy_c,iter] = aiy_vfi_solve_mex(v_old,a_grid,s,P,r,w,beta,sigma,tol,max_iter)");
+    aiy_nargs(nrhs, 10, 10, nlhs, 6, "[v_new,v_old,policy_k,policy_c,iter,idx] = aiy_vfi_solve_mex(v_old,a_grid,s,P,r,w,beta,sigma,tol,max_iter)");
     mwSize N = mxGetM(prhs[0]), Na = mxGetN(prhs[0]);
     aiy_in(prhs[0], "v_old", 0, 0);
     const double* a = aiy_vec(prhs[1], "a_grid", Na, NULL);
@@ -19,9 +21,16 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     mxArray* pk = aiy_out(N, Na);
     mxArray* pc = aiy_out(N, Na);
     int64_t it = 0;
+    int32_t* idx = nlhs > 5 ? (int32_t*)malloc(sizeof(int32_t) * N * Na) : NULL;
     aiy_begin();
     int rc = aiy_vfi_solve(mxGetPr(vo), a, s, P, (int64_t)N, (int64_t)Na, r, w, beta, sigma, tol,
-                           max_iter, mxGetPr(plhs[0]), mxGetPr(pk), mxGetPr(pc), NULL, &it);
+                           max_iter, mxGetPr(plhs[0]), mxGetPr(pk), mxGetPr(pc), idx, &it);
+    if (rc == AIY_OK && idx) {
+        plhs[5] = aiy_out(N, Na);
+        double* o = mxGetPr(plhs[5]);
+        for (mwSize q = 0; q < N * Na; ++q) o[q] = idx[q];
+    }
+    free(idx);
     aiy_check(rc);
     if (nlhs > 1) plhs[1] = vo; else mxDestroyArray(vo);
     if (nlhs > 2) plhs[2] = pk; else mxDestroyArray(pk);

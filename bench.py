@@ -374,6 +374,7 @@ def main():
             out["solve_to_tol"] = solve_wall(pkg, ws, cal, r, w, a_t, s_t, P_t, dev)
         if world == 1 and not args.no_extra:
             out["batch_config4_share"] = BL.batch_leg(pkg, dev)
+            out["dist"] = BL.dist_leg(pkg, dev)
             out["labor_vfi"] = {"Na400": BL.labor_leg(pkg, dev, 400, cpu_threads=threads,
                                                       cpu=not args.no_cpu_baseline),
                                 "Na20000": BL.labor_leg(pkg, dev, 20000, steps=5, reps=3, cpu=False)}
@@ -390,6 +391,14 @@ def main():
                 out["ks_sharded"]["cpu_baseline"] = BL.ks_cpu_baseline(pkg, threads=threads)
         if not args.no_ge and world == 1:
             out["ge_equilibrium"] = ge_wall(pkg, threads)
+            if "ge_batch" in out:  # config 4's CPU baseline: the sequential C bisection
+                g = out["ge_equilibrium"]
+                out["ge_batch"]["cpu_baseline"] = {
+                    "value": g["wall_s_cpu"], "unit": "s to equilibrium r", "cores": threads,
+                    "kind": "port", "value_1core": g["wall_s_cpu_1core"],
+                    "sample": "the whole sequential bisection of Aiyagari_VFI.m at its defaults "
+                              "(C restatement oracle/aiy_oracle.c, OpenMP over states), the "
+                              "same r trace"}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -4,6 +4,7 @@
   labor_leg()       D4: A3 labour VFI sweeps (Aiyagari_Endogenous_Labor_VFI.m:69-112)
   egm_leg()         D4: A4/A5 EGM steps (Aiyagari_EGM.m:74-110, ..._Labor_EGM.m:67-107)
   batch_leg()       D5: the batched multi-rate solve (config 4's per-GPU share) vs one rate
+  dist_leg()        A10: histogram pushes at Na = 20,000 (HBM roofline)
   ge_batch_leg()    D5: config 4's multisection GE (64 candidates / round over the ranks)
   ks_cpu_baseline() D6: the C restatement's Krusell-Smith evals/s (bounded sample)
 
@@ -245,7 +246,11 @@ def egm_leg(pkg, dev, Na, labor=False, steps=50, reps=5, cpu_threads=1, variant=
 def batch_leg(pkg, dev, Na=20000, C=8, sweeps=25):
     """The per-GPU share of config 4 at the headline grid: C rates solved as one batch (one
     table + one tree launch per sweep over all C) against one rate alone, both running exactly
-    `sweeps` sweeps from v = 0 (tol = 0: no early stop).  Unit: Na·Na'·Nz per candidate-sweep."""
+    `sweeps` sweeps from v = 0 (tol = 0: no early stop).  Unit: Na·Na'·Nz per candidate-sweep.
+    Roofline: the batched tree launch's executed work (bound/candidate tests and exact
+    evaluations counted by the instrumented instantiation over the same sweeps, all C
+    candidates) ÷ its average launch duration (HIP events around every tree launch).  The same
+    path is pinned bit for bit by tests/test_pinned_gpu.py::test_batch_config4_share_sweep25."""
     import torch
     cal = pkg.calibration.aiyagari(Na=Na, shocks="rouwenhorst")
     N = cal["N"]
@@ -255,12 +260,14 @@ def batch_leg(pkg, dev, Na=20000, C=8, sweeps=25):
     w = [pkg.calibration.wage(r, cal["alpha"], cal["delta"]) for r in rs]
     ws = pkg.Workspace(N, Na)
     res = {}
+    bufs = {}
     for n in (C, 1):
         va = torch.zeros((n, N, Na), dtype=torch.float64, device=dev)
         vb = torch.zeros_like(va)
         idx = torch.zeros((n, N, Na), dtype=torch.int32, device=dev)
         pk = torch.zeros_like(va)
         pc = torch.zeros_like(va)
+        bufs[n] = (va, vb, idx, pk, pc)
         pkg.vfi.solve_batch_dev(ws, rs[:n], w[:n], va, vb, a_t, s_t, P_t, cal["beta"],
                                 cal["sigma"], 0.0, 3, idx, pk, pc)  # warm-up
         ms = []
@@ -273,13 +280,120 @@ def batch_leg(pkg, dev, Na=20000, C=8, sweeps=25):
             torch.cuda.synchronize()
             ms.append((time.perf_counter() - t0) * 1e3)
         res[n] = _median(ms)
+    va, vb, idx, pk, pc = bufs[C]
+
+    def run(flags):
+        ws.set_timing(**flags)
+        va.zero_()
+        pkg.vfi.solve_batch_dev(ws, rs, w, va, vb, a_t, s_t, P_t, cal["beta"], cal["sigma"], 0.0,
+                                sweeps, idx, pk, pc)
+        torch.cuda.synchronize()
+
+    run({"on": True})
+    km, nl, _ = ws.timing()
+    kern_ms = km / max(nl, 1)
+    run({"on": False, "count": True})
+    ex, sup, blk, cand = ws.counters()
+    ws.set_timing(False)
+    executed = (FLOPS_PER_TEST * (sup + blk + cand) + FLOPS_PER_CANDIDATE * ex) / sweeps
+    ach = executed / (kern_ms * 1e-3) / 1e12
     per = N * Na * Na * sweeps
     return {"workload": f"Aiyagari VFI at Na={Na} Nz={N} Rouwenhorst: {C} candidate rates as one "
                         f"batched solve, {sweeps} sweeps each from v=0 (config 4 per-GPU share)",
             "value": C * per / (res[C] * 1e-3), "unit": "evals/s",
             "batch_ms": res[C], "single_rate_ms": res[1],
             "single_rate_evals_per_s": per / (res[1] * 1e-3),
-            "speedup_vs_sequential_rates": C * res[1] / res[C]}
+            "speedup_vs_sequential_rates": C * res[1] / res[C],
+            "roofline": {"bound": "valu", "achieved": ach, "peak": PEAK_FP64_TFLOPS,
+                         "unit": "TFLOP/s", "frac": ach / PEAK_FP64_TFLOPS,
+                         "kernel": "bell_tree_kernel (batched, C candidates per launch)",
+                         "kernel_avg_ms": kern_ms, "launches": nl,
+                         "basis": f"executed work over all {C} candidates: {FLOPS_PER_TEST} flops "
+                                  f"per bound/candidate test, {FLOPS_PER_CANDIDATE} per exact "
+                                  f"evaluation (instrumented pass of the same {sweeps} sweeps): "
+                                  f"{executed:.3g} flops per launch",
+                         "tests_per_launch": {"exact": ex / sweeps, "superblock": sup / sweeps,
+                                              "block": blk / sweeps, "candidate": cand / sweeps},
+                         "effective_tflops_d3": FLOPS_PER_CANDIDATE * C * N * Na * Na
+                                                / (kern_ms * 1e-3) / 1e12},
+            "parity": "tests/test_pinned_gpu.py::test_batch_config4_share_sweep25_bitwise"}
+
+
+# ----------------------------------------------------------------------------------- A10 dist
+DIST_BYTES_PER_STATE = 20  # λ in (8), run offset (4), λ' out (8) per state and push
+
+
+def dist_leg(pkg, dev, Na=20000, pushes=320, cpu_pushes=600):
+    """A10 histogram pushes (csrc/dist_kernels.hip dist_push_kernel) on the config-2 policy
+    (Na = 20,000, Rouwenhorst, r = 0.04, the device VFI solve's argmax): `pushes` pushes from
+    the uniform distribution through aiy_dist_stationary_dev with tol = 0 (plan once, batches of
+    32 pushes per read), then the solve to max|Δλ| < 1e-13.  Unit: pushes/s over all N·Na
+    states; HBM roofline on the algorithmic 20 B per state and push.  CPU: the C restatement's
+    push (orc_dist_stationary, sequential), one core."""
+    import torch
+    from oracle import corc
+    cal = pkg.calibration.aiyagari(Na=Na, shocks="rouwenhorst")
+    N = cal["N"]
+    r = 0.04
+    w = pkg.calibration.wage(r, cal["alpha"], cal["delta"])
+    t = lambda x: torch.as_tensor(np.ascontiguousarray(x), device=dev)
+    a_t, s_t, P_t = t(cal["a_grid"]), t(cal["s"]), t(cal["P"])
+    vws = pkg.Workspace(N, Na)
+    va = torch.zeros((N, Na), dtype=torch.float64, device=dev)
+    vb = torch.zeros_like(va)
+    idx = torch.zeros((N, Na), dtype=torch.int32, device=dev)
+    iters, _ = vws.vfi_solve(va, vb, a_t, s_t, P_t, r, w, cal["beta"], cal["sigma"], 1e-5, 1000,
+                             idx)
+    vws.close()
+    lam0 = torch.full((N, Na), 1.0 / (N * Na), dtype=torch.float64, device=dev)
+    out = torch.empty_like(lam0)
+    K = torch.zeros(1, dtype=torch.float64, device=dev)
+    ws = pkg.Workspace(N, Na)
+    run = lambda n, tol=0.0: pkg.dist_stationary_dev(ws, lam0, a_t, P_t, out, policy_idx=idx,
+                                                     tol=tol, max_iter=n, k_supply=K)
+    run(64)
+    torch.cuda.synchronize()
+    ms = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        run(pushes)
+        torch.cuda.synchronize()
+        ms.append((time.perf_counter() - t0) * 1e3)
+    wall_ms = _median(ms)
+    ws.set_timing(True)
+    run(pushes)
+    torch.cuda.synchronize()
+    km, nl, _ = ws.timing()
+    ws.set_timing(False)
+    kern_ms = km / max(nl, 1)
+    t0 = time.perf_counter()
+    it_tol, d_tol = run(100000, 1e-13)
+    torch.cuda.synchronize()
+    tol_ms = (time.perf_counter() - t0) * 1e3
+    states = N * Na
+    gbs = DIST_BYTES_PER_STATE * states / (kern_ms * 1e-3) / 1e9
+    idx_np = idx.cpu().numpy()
+    lam_np = lam0.cpu().numpy()
+    dt = _time_cpu(lambda: corc.dist_stationary(lam_np, cal["a_grid"], cal["P"], idx=idx_np,
+                                                tol=0.0, max_iter=cpu_pushes), 1)
+    return {"workload": f"A10 histogram pushes, Na={Na} Nz={N} Rouwenhorst, policy = argmax of "
+                        f"the r=0.04 VFI solve ({iters} sweeps); {pushes} pushes from uniform "
+                        f"lambda, device tier (aiy_dist_stationary_dev, tol=0)",
+            "value": pushes / (wall_ms * 1e-3), "unit": "pushes/s",
+            "states_per_s": pushes * states / (wall_ms * 1e-3),
+            "us_per_push": wall_ms * 1e3 / pushes, "kernel_us": kern_ms * 1e3,
+            "to_tol": {"tol": 1e-13, "pushes": it_tol, "dist": d_tol, "wall_ms": tol_ms,
+                       "K": float(K[0])},
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gbs / HBM_PEAK_GBS, "kernel": "dist_push_kernel<false>",
+                         "kernel_avg_ms": kern_ms, "launches": nl,
+                         "basis": f"{DIST_BYTES_PER_STATE} B algorithmic per state and push "
+                                  f"(lambda in, run offset, lambda' out) x {states} states"},
+            "cpu_baseline": {"value": cpu_pushes / dt, "unit": "pushes/s", "cores": 1,
+                             "kind": "port", "states_per_s": cpu_pushes * states / dt,
+                             "sample": f"{cpu_pushes} pushes of orc_dist_stationary (sequential "
+                                       f"scatter, oracle/aiy_oracle.c) on the same policy: "
+                                       f"{dt:.2f} s"}}
 
 
 def ge_batch_leg(pkg, world, rank, dev, Na=400, levels=6, sequential=True):

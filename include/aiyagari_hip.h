@@ -309,6 +309,15 @@ int aiy_sim_capital_dev(aiy_ws* ws, const double* policy_rows, const double* a_g
 int aiy_dist_update_dev(aiy_ws* ws, const double* lambda, const int32_t* policy_idx,
                         const double* policy_k, const double* a_grid, const double* P,
                         double* lambda_out, double* diff, void* stream);
+/* A10 on device: the fixed-point loop of aiy_dist_stationary with everything in HBM.  The
+ * policy's plan (run offsets) is built once; pushes run in speculative batches of up to 32
+ * between reads of max|Δλ| (one synchronisation per batch).  lambda [N][Na] in (initial
+ * guess, not modified); lambda_out [N][Na] = the last push; k_supply (nullable, device
+ * double) = Σ λ·a; iters, dist host out. */
+int aiy_dist_stationary_dev(aiy_ws* ws, const double* lambda, const int32_t* policy_idx,
+                            const double* policy_k, const double* a_grid, const double* P,
+                            double tol, int64_t max_iter, double* lambda_out,
+                            double* k_supply, int64_t* iters, double* dist, void* stream);
 
 /* ---- A6/A7 device tier for one process per GPU.  A handle owns the shard
  * K in [K0, K1) of all four s; V / Vold / Vout / kopt are full k x K x S column-major device
@@ -333,6 +342,14 @@ int ks_dev_improve(ks_dev* h, const double* V, double* kopt, void* stream);
 int ks_dev_howard(ks_dev* h, const double* V, const double* kopt, double* Vout, void* stream);
 /* :195 max relative change over the shard, NaN ignored; out = device uint64[2]
  * {IEEE bits of the max, nonzero if any node was not NaN} */
+/* The fused schedule (one launch per Howard sweep): ks_dev_slopes writes the pchip slopes
+ * of every column h reads into dV (caller-owned k x K x S); ks_dev_howard_fused then sweeps h's
+ * nodes reading (V, dV) and writes the new values AND their slopes (Vout, dVout) on h's nodes,
+ * so consecutive sweeps over nested ghost rectangles need no slope launch in between.
+ * Bit-identical to ks_dev_howard. */
+int ks_dev_slopes(ks_dev* h, const double* V, double* dV, void* stream);
+int ks_dev_howard_fused(ks_dev* h, const double* V, const double* dV, const double* kopt,
+                        double* Vout, double* dVout, void* stream);
 int ks_dev_reldiff(ks_dev* h, const double* V, const double* Vold, void* out, void* stream);
 /* Ghost shards (ks_dist.py exchanges halos every m Howard sweeps and sweeps a widening
  * rectangle of other ranks' columns redundantly in between — same kernels, so still bit-exact):

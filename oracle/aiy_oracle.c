@@ -358,26 +358,59 @@ int orc_sim_capital(int64_t N, int64_t Na, const double* pol, int64_t zs, int64_
 }
 
 /* ------------------------------------------------------------------ A10 (new) */
-int orc_dist_update_ongrid(int64_t N, int64_t Na, const double* lam, const int32_t* idx,
-                           const double* P, double* out) {
-    double* mass = (double*)calloc((size_t)(N * Na), sizeof(double));
-    if (!mass) return 1;
-    for (int64_t i = 0; i < N; ++i)
-        for (int64_t j = 0; j < Na; ++j) mass[i * Na + idx[i * Na + j]] += lam[i * Na + j];
-    for (int64_t m = 0; m < N; ++m)
+/* A10 (new; no reference code).  The mass of destination (i,k) is the sum of the terms that
+ * land there, in ascending source j, summed sequentially in chunks of ORC_DIST_CHUNK terms with
+ * the chunk sums summed sequentially (the definition the HIP kernels follow,
+ * csrc/dist.hpp kDistChunk): runs of <= 32 terms are the plain sequential scatter. */
+#define ORC_DIST_CHUNK 32
+typedef struct { double *tot, *part; int* cnt; } orc_mass_acc;
+static int mass_acc_init(orc_mass_acc* m, int64_t n) {
+    m->tot = (double*)calloc((size_t)n, sizeof(double));
+    m->part = (double*)calloc((size_t)n, sizeof(double));
+    m->cnt = (int*)calloc((size_t)n, sizeof(int));
+    return !(m->tot && m->part && m->cnt);
+}
+static void mass_acc_add(orc_mass_acc* m, int64_t q, double x) {
+    m->part[q] = m->part[q] + x;
+    if (++m->cnt[q] == ORC_DIST_CHUNK) {
+        m->tot[q] = m->tot[q] + m->part[q];
+        m->part[q] = 0.0;
+        m->cnt[q] = 0;
+    }
+}
+/* finish the chunks and project: out(m,k) = sum_i P(i,m) mass(i,k), i ascending */
+static void mass_acc_project(orc_mass_acc* m, int64_t N, int64_t Na, const double* P,
+                             double* out) {
+    for (int64_t q = 0; q < N * Na; ++q)
+        if (m->cnt[q]) m->tot[q] = m->tot[q] + m->part[q];
+    for (int64_t c = 0; c < N; ++c)
         for (int64_t k = 0; k < Na; ++k) {
             double acc = 0.0;
-            for (int64_t i = 0; i < N; ++i) acc = acc + P[i * N + m] * mass[i * Na + k];
-            out[m * Na + k] = acc;
+            for (int64_t i = 0; i < N; ++i) acc = acc + P[i * N + c] * m->tot[i * Na + k];
+            out[c * Na + k] = acc;
         }
-    free(mass);
+}
+static void mass_acc_free(orc_mass_acc* m) {
+    free(m->tot);
+    free(m->part);
+    free(m->cnt);
+}
+
+int orc_dist_update_ongrid(int64_t N, int64_t Na, const double* lam, const int32_t* idx,
+                           const double* P, double* out) {
+    orc_mass_acc m;
+    if (mass_acc_init(&m, N * Na)) { mass_acc_free(&m); return 1; }
+    for (int64_t i = 0; i < N; ++i)
+        for (int64_t j = 0; j < Na; ++j) mass_acc_add(&m, i * Na + idx[i * Na + j], lam[i * Na + j]);
+    mass_acc_project(&m, N, Na, P, out);
+    mass_acc_free(&m);
     return 0;
 }
 
 int orc_dist_update_lottery(int64_t N, int64_t Na, const double* lam, const double* kp,
                             const double* a_grid, const double* P, double* out) {
-    double* mass = (double*)calloc((size_t)(N * Na), sizeof(double));
-    if (!mass) return 1;
+    orc_mass_acc m;
+    if (mass_acc_init(&m, N * Na)) { mass_acc_free(&m); return 1; }
     for (int64_t i = 0; i < N; ++i)
         for (int64_t j = 0; j < Na; ++j) {
             double x = kp[i * Na + j];
@@ -385,16 +418,11 @@ int orc_dist_update_lottery(int64_t N, int64_t Na, const double* lam, const doub
             if (x > a_grid[Na - 1]) x = a_grid[Na - 1];
             int64_t k = seg_of(Na, a_grid, x);
             double wr = (x - a_grid[k]) / (a_grid[k + 1] - a_grid[k]);
-            mass[i * Na + k] += lam[i * Na + j] * (1 - wr);
-            mass[i * Na + k + 1] += lam[i * Na + j] * wr;
+            mass_acc_add(&m, i * Na + k, lam[i * Na + j] * (1 - wr));
+            mass_acc_add(&m, i * Na + k + 1, lam[i * Na + j] * wr);
         }
-    for (int64_t m = 0; m < N; ++m)
-        for (int64_t k = 0; k < Na; ++k) {
-            double acc = 0.0;
-            for (int64_t i = 0; i < N; ++i) acc = acc + P[i * N + m] * mass[i * Na + k];
-            out[m * Na + k] = acc;
-        }
-    free(mass);
+    mass_acc_project(&m, N, Na, P, out);
+    mass_acc_free(&m);
     return 0;
 }
 

@@ -82,3 +82,60 @@ def test_bad_index_rejected(pkg, gpu):
     idx = np.ones((7, 50), np.int32); idx[2, 7] = 51
     with pytest.raises(pkg.AiyError):
         pkg.dist_stationary(cal["a_grid"], cal["P"], policy_idx=idx, tol=0.0, max_iter=1)
+
+
+def _long_run_policy(Na, rng):
+    """Monotone on-grid policy with runs far longer than one chunk (32) and than one wave's
+    64 chunks (2,048): a borrowing-constraint run of 4,500 sources, a top-of-grid run of 2,600,
+    short runs and gaps in between."""
+    idx = np.empty((3, Na), np.int32)
+    for i in range(3):
+        body = np.sort(rng.integers(1, Na - 1, Na - 4500 - 2600 * (i > 0)))
+        parts = [np.zeros(4500, np.int64), body]
+        if i > 0:
+            parts.append(np.full(2600, Na - 1))
+        idx[i] = np.concatenate(parts)[:Na]
+    return idx
+
+
+def test_long_runs_chunked_order_bitwise(pkg, gpu):
+    """Runs of 33 … 4,500 terms take the wave-cooperative chunk path (dist.hpp kDistChunk);
+    the C restatement sums the same chunks in the same order."""
+    rng = np.random.default_rng(7)
+    Na = 9000
+    a = np.linspace(0.0, 50.0, Na) ** 1.5
+    P = rng.random((3, 3)); P /= P.sum(1, keepdims=True)
+    idx = _long_run_policy(Na, rng)
+    lam0 = rng.random((3, Na)); lam0 /= lam0.sum()
+    lam, _, it, _ = pkg.dist_stationary(a, P, policy_idx=idx + 1, lam0=lam0, tol=0.0, max_iter=3)
+    lo, _, ito, _ = corc.dist_stationary(lam0, a, P, idx=idx, tol=0.0, max_iter=3)
+    assert it == ito == 3 and np.array_equal(lam, lo)
+    # lottery: a long run below the grid (key 0, weight 0) and one at its top (weight 1)
+    kp = np.concatenate([np.full((3, 3000), -1.0), np.sort(rng.uniform(0, a[-1], (3, Na - 5000)), 1),
+                         np.full((3, 2000), a[-1] + 1.0)], 1)
+    lam, _, _, _ = pkg.dist_stationary(a, P, policy_k=kp, lam0=lam0, tol=0.0, max_iter=2)
+    lo, _, _, _ = corc.dist_stationary(lam0, a, P, kp=kp, tol=0.0, max_iter=2)
+    assert np.array_equal(lam, lo)
+
+
+@pytest.mark.parametrize("tol,max_iter", [(1e-13, 5000), (1e-9, 5000), (0.0, 45), (1e-13, 70)])
+def test_stationary_dev_speculative_batches(pkg, gpu, tol, max_iter):
+    """aiy_dist_stationary_dev (plan once, up to 32 pushes per read) stops at the push the
+    one-read-per-push loop stops at — in the middle of a batch, at max_iter, on push counts that
+    are not multiples of the batch — with the same λ, dist and K."""
+    import torch
+    cal, R = _vfi_policy(1000)
+    dev = torch.device("cuda:0")
+    t = lambda x: torch.as_tensor(np.ascontiguousarray(x), device=dev)
+    lam0 = np.full((7, 1000), 1.0 / 7000)
+    ws = pkg.Workspace(7, 1000)
+    out = torch.empty((7, 1000), dtype=torch.float64, device=dev)
+    K = torch.zeros(1, dtype=torch.float64, device=dev)
+    it, dist = pkg.dist_stationary_dev(ws, t(lam0), t(cal["a_grid"]), t(cal["P"]), out,
+                                       policy_idx=t(R["idx"].astype(np.int32)), tol=tol,
+                                       max_iter=max_iter, k_supply=K)
+    lo, Ko, ito, disto = corc.dist_stationary(lam0, cal["a_grid"], cal["P"], idx=R["idx"],
+                                              tol=tol, max_iter=max_iter)
+    assert it == ito and dist == disto
+    assert np.array_equal(out.cpu().numpy(), lo)
+    assert abs(float(K[0]) - Ko) <= 1e-12 * abs(Ko)

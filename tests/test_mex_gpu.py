@@ -20,6 +20,16 @@ def test_vfi_solve_gateway(pkg, gpu, golden):
     v2, pk2, pc2, idx = mexstub.call("aiy_vfi_sweep_mex", 4, g["v20"], g["a_grid"], g["s"], g["P"],
                                      float(g["r"]), float(g["w"]), 0.96, 5.0)
     assert np.array_equal(v2, g["v21"]) and np.array_equal(idx - 1, g["idx21"])
+    # the optional 6th output: the last sweep's 1-based argmax (Aiyagari_VFI.m:79-80), so the
+    # host script needs no N x Na x Na min to rebuild it
+    out = mexstub.call("aiy_vfi_solve_mex", 6, np.zeros((7, 400)), g["a_grid"], g["s"], g["P"],
+                       float(g["r"]), float(g["w"]), 0.96, 5.0, 1e-5, 1000.0)
+    R = corc.vfi_solve(np.zeros((7, 400)), g["a_grid"], g["s"], g["P"], float(g["r"]),
+                       float(g["w"]), 0.96, 5.0)
+    idx6 = out[5]
+    assert idx6.shape == (7, 400) and np.array_equal(idx6 - 1, R["idx"])
+    assert np.array_equal(out[2], g["a_grid"][idx6.astype(int) - 1])  # policy_k = a_grid(idx)
+    assert np.array_equal(out[0], v_new)
 
 
 def test_egm_and_sim_gateways(pkg, gpu, golden):

@@ -11,6 +11,8 @@
 * F4 (Aiyagari_VFI.m:314-410) on HIP-produced outputs: Gini / quintiles of the A9 Monte-Carlo
   path and of the A10 histogram, against the same statistics of the oracle-composed pipeline.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -62,6 +64,46 @@ def test_bench_device_path_sweep25_bitwise(pkg, gpu, cal20k):
     assert np.array_equal(v[cur].cpu().numpy(), vo)
     assert np.array_equal(idx.cpu().numpy(), io)
     assert np.array_equal(pk.cpu().numpy(), pko) and np.array_equal(pc.cpu().numpy(), pco)
+
+
+def test_batch_config4_share_sweep25_bitwise(pkg, gpu, cal20k):
+    """bench_legs.batch_leg's exact path (BASELINE configs[3] per-GPU share, Aiyagari_VFI.m:
+    142-171): 8 rates linspace(-0.03, 0.035) solved as ONE batched solve at Na = 20,000
+    Rouwenhorst from v = 0 with tol = 0 (no early stop).  The batch is run for 24 sweeps, each
+    candidate's V copied back, then re-run from v = 0 for 25: every candidate's sweep 25
+    (v_new, argmax, policy_k, policy_c) must equal the C oracle's exhaustive sweep of its own
+    sweep-24 value bit for bit."""
+    import torch
+    cal = cal20k
+    N = cal["N"]
+    C = 8
+    a_t, s_t, P_t = _bench_tensors(pkg, cal, torch)
+    dev = a_t.device
+    rs = list(np.linspace(-0.03, 0.035, C))
+    w = [pkg.calibration.wage(r, cal["alpha"], cal["delta"]) for r in rs]
+    ws = pkg.Workspace(N, NA)
+
+    def run(sweeps):
+        va = torch.zeros((C, N, NA), dtype=torch.float64, device=dev)
+        vb = torch.zeros_like(va)
+        idx = torch.zeros((C, N, NA), dtype=torch.int32, device=dev)
+        pk, pc = torch.zeros_like(va), torch.zeros_like(va)
+        it, which = pkg.vfi.solve_batch_dev(ws, rs, w, va, vb, a_t, s_t, P_t, cal["beta"],
+                                            cal["sigma"], 0.0, sweeps, idx, pk, pc)
+        torch.cuda.synchronize()
+        assert it == [sweeps] * C
+        vn = [(vb if which[c] else va)[c].cpu().numpy() for c in range(C)]
+        return vn, idx.cpu().numpy(), pk.cpu().numpy(), pc.cpu().numpy()
+
+    v24, _, _, _ = run(24)
+    v25, idx, pk, pc = run(25)
+    corc.num_threads(min(16, os.cpu_count() or 1))  # 8 exhaustive sweeps of 2.8e9 candidates
+    for c in range(C):
+        vo, io, pko, pco = corc.vfi_sweep(v24[c], cal["a_grid"], cal["s"], cal["P"], rs[c], w[c],
+                                          cal["beta"], cal["sigma"])
+        assert np.array_equal(v25[c], vo), c
+        assert np.array_equal(idx[c], io), c
+        assert np.array_equal(pk[c], pko) and np.array_equal(pc[c], pco), c
 
 
 def test_solve_to_tol_full_size_fixed_point(pkg, gpu, cal20k):
