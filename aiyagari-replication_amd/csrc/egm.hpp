@@ -21,6 +21,10 @@ struct EgmArgs {
     unsigned* flags;           // bit 0: a_hat not increasing (small-grid fused step: bit 1 of
                                // the diff slots' second word instead, see egm_fused_kernel)
     bool fused;                // Na <= 1024: one launch per step (egm_fused_kernel)
+    bool onepass;              // Na > 1024: one launch per step (egm_scatter_kernel); the
+                               // caller zeroes `diff` before the launch, the flag rides in
+                               // bit 1 of the slots' second words
 };
+constexpr int kEgmFusedMaxNa = 1024;  // egm_fused_kernel: one state per thread
 int launch_egm_step(const EgmArgs& A, hipStream_t st);
 }  // namespace aiy

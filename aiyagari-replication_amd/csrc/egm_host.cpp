@@ -55,8 +55,10 @@ static EgmArgs egm_args(aiy_ws* ws, const double* c, const double* a, const doub
     A.ahat = ws->g0; A.cnext = ws->g1; A.cout = cout; A.pk = pk; A.pl = pl;
     A.diff = ws->diff;
     A.flags = (unsigned*)ws->gi;
-    // one launch per step on small grids unless the tuning variant sets bit 11 (A/B only)
+    // one launch per step: egm_fused_kernel on small grids, egm_scatter_kernel on large ones,
+    // unless the tuning variant sets bit 11 / bit 12 (the two-launch step, A/B only)
     A.fused = !(ws->variant >= 0 && (ws->variant & 2048));
+    A.onepass = A.Na > kEgmFusedMaxNa && !(ws->variant >= 0 && (ws->variant & 4096));
     return A;
 }
 
@@ -68,7 +70,10 @@ int egm_step_dev(aiy_ws* ws, const double* c, const double* a, const double* s, 
     if (labor && !(phi == phi && theta == theta)) return fail(AIY_NON_FINITE, "phi/theta");
     AIY_TRY(ensure_egm(ws));
     EgmArgs A = egm_args(ws, c, a, s, P, r, w, beta, sigma, amin, labor, phi, theta, cout, pk, pl);
-    // the RHS kernel clears the diff slots and the flag word itself (no memset launches)
+    // the two-launch and small-grid steps clear the diff slots and the flag word themselves;
+    // the one-pass scatter step accumulates from its first wave, so they are zeroed here
+    if (A.onepass)
+        AIY_HIP(hipMemsetAsync(ws->diff, 0, 2 * kDiffSlots * sizeof(unsigned long long), st));
     AIY_TRY(ws_timing_begin(ws, st));
     AIY_TRY(launch_egm_step(A, st));
     AIY_TRY(ws_timing_end(ws, st));
@@ -128,6 +133,8 @@ static int egm_solve_spec(aiy_ws* ws, const EgmArgs& A0, double* c0, double tol,
             if (need >= 1 && need < (double)m) m = (int64_t)need;
         }
         m = std::min<int64_t>(std::max<int64_t>(m, 1), max_iter - done);
+        if (A0.onepass)  // the scatter step does not clear its own slots
+            AIY_HIP(hipMemsetAsync(ws->egm_slots, 0, (size_t)m * SW * sizeof(unsigned long long), st));
         for (int64_t t = 0; t < m; ++t) AIY_TRY(step(done + 1 + t, (int)t));
         last_enq = done + m;
         AIY_HIP(hipMemcpyAsync(ws->egm_hslots, ws->egm_slots,
@@ -149,7 +156,11 @@ static int egm_solve_spec(aiy_ws* ws, const EgmArgs& A0, double* c0, double tol,
         if (!stop) done += m;
     }
     const int64_t g = stop ? stop : done;
-    if (g > 0 && g != last_enq) AIY_TRY(step(g, 0));  // policy_k/l of the stopping step
+    if (g > 0 && g != last_enq) {  // policy_k/l of the stopping step
+        if (A0.onepass)
+            AIY_HIP(hipMemsetAsync(ws->egm_slots, 0, SW * sizeof(unsigned long long), st));
+        AIY_TRY(step(g, 0));
+    }
     *cur_out = g > 0 ? slot(g) : slot(0);
     *dist = d_stop;
     *iters = g;

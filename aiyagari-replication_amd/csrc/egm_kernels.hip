@@ -178,8 +178,8 @@ __global__ __launch_bounds__(256) void egm_interp_kernel(EgmArgs A, int ntile) {
 // slot j outright — {max|Δc| bits, bit 0: some finite Δc | bit 1: â_j not increasing} — and
 // workgroup 0 clears the other slots and the flag word, so nothing is cleared and accumulated
 // by different workgroups of one launch.
-constexpr int kEgmFusedMaxNa = 1024;  // one state per thread: measured 8.8 vs 12.0 us per step
-                                       // at Na = 400, 27.6 vs 11.7 at 4,096 (4 per thread)
+// (kEgmFusedMaxNa = 1,024, egm.hpp: one state per thread — measured 8.8 vs 12.0 us per step
+// at Na = 400, 27.6 vs 11.7 at 4,096 with 4 per thread)
 __global__ __launch_bounds__(1024) void egm_fused_kernel(EgmArgs A) {
     __shared__ double s_x[kEgmFusedMaxNa];
     __shared__ double s_y[kEgmFusedMaxNa];
@@ -273,10 +273,179 @@ __global__ __launch_bounds__(1024) void egm_fused_kernel(EgmArgs A) {
     }
 }
 
+// Large grids: one launch per step by inverting the search.  interp1's segment of query a_i
+// in the monotone â_j is k iff â_k <= a_i < â_{k+1} (k = 0 takes every a_i < â_1, k = Na−2
+// every a_i >= â_{Na−2}: the clamps of seg_of_dev), so the queries of segment k are the index
+// range [B_k, B_{k+1}) with B_k = #{i : a_i < â_k} — a search of the FIXED a_grid, not of
+// â_j.  A workgroup owns 64 consecutive nodes k (stride 63: lane 63 only supplies â_{k+1}
+// of lane 62) for all N rows, exactly as egm_rhs_kernel computes â there (u'(c_m) once per
+// (m, k) in LDS, the Euler sum in m order, one pow per (j, k)); each wave then finds B_k of
+// its 64 increasing â (two 64-ary ballot searches of a_grid and an LDS window), and lane k
+// writes the outputs of its queries with its own (â_k, â_{k+1}, y_k, y_{k+1}) — the same
+// formulas, on the same segment, as egm_interp_kernel, so bit for bit the two-launch step.
+// A segment with more than 4 queries (the borrowing-constraint region, the clamps at both
+// ends) is finished by the whole wave, 64 queries at a time.  â_j not strictly increasing
+// (an adjacent pair checked per lane) sets bit 1 of the slot's second word: the host fails
+// the call, as the two-launch step does.  diff must be zero at launch (no in-launch clear).
+__global__ __launch_bounds__(1024) void egm_scatter_kernel(EgmArgs A) {
+    __shared__ double s_up[16][64];
+    __shared__ double s_a[16][256];
+    const int lane = threadIdx.x & 63, m = threadIdx.x >> 6;  // blockDim = 64·N
+    const int N = A.N, Na = A.Na;
+    const int k = blockIdx.x * 63 + lane;
+    const bool okk = k < Na;
+    const double* __restrict__ ag = A.a;
+    s_up[m][lane] = okk ? uprime_dev(A.c[(size_t)m * Na + k], A.sigma, A.ns) : 0.0;
+    __syncthreads();
+    const int j = m;
+    const double coef0 = A.beta * (1 + A.r);
+    const double ws = A.w * A.s[j];
+    double ah = 0.0, yk = 0.0;
+    if (okk) {
+        double acc = 0.0;
+        for (int q = 0; q < N; ++q) acc = acc + (coef0 * A.P[j * N + q]) * s_up[q][lane];
+        const double cn = aiy_pow(acc, -1.0 / A.sigma);  // :88
+        const double akv = ag[k];
+        if (A.labor) {
+            const double ls = labor_dev(cn, ws, A.sigma, A.ns, A.phi, A.theta);
+            ah = ((cn + akv) - ws * ls) / (1 + A.r);
+        } else {
+            ah = ((cn + akv) - ws) / (1 + A.r);
+        }
+        yk = A.labor ? cn : akv;
+    }
+    // neighbour k + 1 (lane 63 of the next tile is this tile's lane 63)
+    const double ah1 = __shfl_down(ah, 1), yk1 = __shfl_down(yk, 1);
+    const bool own = lane < 63 && okk && k <= Na - 2;  // segment k is this lane's
+    const bool bad = own && !(ah < ah1);               // interp1 needs increasing â
+    // B_k = #{i : a_i < â_k} for every valid lane (lane 63 supplies B_{k+1} of lane 62)
+    const int last = min(63, Na - 1 - blockIdx.x * 63);
+    const double q0 = readlane_d(ah, 0), q1 = readlane_d(ah, last);
+    int lo0 = 0, hi0 = Na, lo1 = 0, hi1 = Na;
+    while (lo0 < hi0 || lo1 < hi1) {  // wave-uniform 64-ary lower bounds of q0 and q1
+        const int st0 = max((hi0 - lo0 + 63) >> 6, 1), st1 = max((hi1 - lo1 + 63) >> 6, 1);
+        const int k0 = lo0 + (lane + 1) * st0 - 1, k1 = lo1 + (lane + 1) * st1 - 1;
+        const bool v0 = k0 < hi0, v1 = k1 < hi1;
+        const double x0 = v0 ? ag[k0] : 0.0, x1 = v1 ? ag[k1] : 0.0;
+        const int c0 = __popcll(__ballot(v0 && x0 < q0));
+        const int c1 = __popcll(__ballot(v1 && x1 < q1));
+        if (lo0 < hi0) {
+            const int nh = lo0 + (c0 + 1) * st0 - 1;
+            lo0 += c0 * st0;
+            hi0 = nh < hi0 ? nh : hi0;
+        }
+        if (lo1 < hi1) {
+            const int nh = lo1 + (c1 + 1) * st1 - 1;
+            lo1 += c1 * st1;
+            hi1 = nh < hi1 ? nh : hi1;
+        }
+    }
+    int Bk;
+    const int span = lo1 - lo0;
+    if (span >= 0 && span <= 256) {  // increasing â: every B_k in [lo0, lo1]
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (u * 64 + lane < span) s_a[m][u * 64 + lane] = ag[lo0 + u * 64 + lane];
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        int lo = 0, hi = span;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (s_a[m][mid] < ah) lo = mid + 1;
+            else hi = mid;
+        }
+        Bk = lo0 + lo;
+    } else {  // not increasing (flagged) or a wide spread: per-lane search of the range
+        int lo = min(lo0, lo1), hi = max(lo0, lo1);
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (ag[mid] < ah) lo = mid + 1;
+            else hi = mid;
+        }
+        Bk = lo;
+    }
+    if (k == 0) Bk = 0;  // segment 0 also takes every query below â_0
+    int Bk1 = __shfl_down(Bk, 1);
+    if (k == Na - 2) Bk1 = Na;  // segment Na−2 takes every query from â_{Na−2} up
+    int b = own ? Bk : 0, e = own ? Bk1 : 0;
+    b = min(max(b, 0), Na);
+    e = min(max(e, b), Na);
+    const double r1 = 1 + A.r;
+    unsigned long long key = 0ull;
+    bool any = false;
+    const double* __restrict__ crow = A.c + (size_t)j * Na;
+    auto query = [&](int i, double x0, double x1, double y0, double y1) {
+        const size_t t = (size_t)j * Na + i;
+        const double q = ag[i];
+        const double tt = (q - x0) / (x1 - x0);
+        double g = y0 + tt * (y1 - y0);
+        double cn;
+        if (A.labor) {
+            if (q < A.amin) g = A.amin;  // :91
+            cn = g;
+            const double l = labor_dev(g, ws, A.sigma, A.ns, A.phi, A.theta);  // :95
+            const double kk = (r1 * q + ws * l) - g;                            // :98
+            A.pk[t] = kk < 0 ? 0.0 : kk;                                         // :99
+            if (A.pl) A.pl[t] = l;
+        } else {
+            if (g < A.amin) g = A.amin;  // :98
+            A.pk[t] = g;
+            cn = (r1 * q + ws) - g;  // :102
+        }
+        A.cout[t] = cn;
+        const double d = fabs(cn - crow[i]);
+        if (d == d) {
+            const unsigned long long kb = (unsigned long long)aiy_dbits(d);
+            key = kb > key ? kb : key;
+            any = true;
+        }
+    };
+    constexpr int kShort = 4;
+    for (int u = 0; u < kShort; ++u)
+        if (b + u < e) query(b + u, ah, ah1, yk, yk1);
+    unsigned long long lm = __ballot(e - b > kShort);
+    while (lm) {  // long segments: the wave takes their remaining queries 64 at a time
+        const int ql = __builtin_ctzll(lm);
+        lm &= lm - 1;
+        const int qb = readlane_i(b, ql) + kShort, qe = readlane_i(e, ql);
+        const double x0 = readlane_d(ah, ql), x1 = readlane_d(ah1, ql);
+        const double y0 = readlane_d(yk, ql), y1 = readlane_d(yk1, ql);
+        for (int i = qb + lane; i < qe; i += 64) query(i, x0, x1, y0, y1);
+    }
+    // block max|Δc| into slot blockIdx % 64; the non-monotone flag in bit 1 of its second word
+    key = wave_max_u64_lane63(key);
+    const unsigned lo32 = __builtin_amdgcn_readlane((int)(unsigned)key, 63);
+    const unsigned hi32 = __builtin_amdgcn_readlane((int)(unsigned)(key >> 32), 63);
+    const int fl = (__ballot(any) != 0ull ? 1 : 0) | (__ballot(bad) != 0ull ? 2 : 0);
+    __shared__ unsigned long long s_key[16];
+    __shared__ int s_fl[16];
+    if (lane == 0) {
+        s_key[m] = ((unsigned long long)hi32 << 32) | lo32;
+        s_fl[m] = fl;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long kk = 0ull;
+        int f = 0;
+        for (int v = 0; v < N; ++v) {
+            kk = s_key[v] > kk ? s_key[v] : kk;
+            f |= s_fl[v];
+        }
+        unsigned long long* sl = A.diff + 2 * (blockIdx.x % kDiffSlots);
+        if (f & 1) atomicMax(sl, kk);
+        if (f) atomicOr(sl + 1, (unsigned long long)f);
+    }
+}
+
 int launch_egm_step(const EgmArgs& A, hipStream_t st) {
     if (A.N > 16) return fail(AIY_BAD_SHAPE, "EGM kernels support N <= 16 productivity states");
     if (A.fused && A.Na >= 2 && A.Na <= kEgmFusedMaxNa) {
         egm_fused_kernel<<<A.N, 1024, 0, st>>>(A);
+        AIY_HIP(hipGetLastError());
+        return AIY_OK;
+    }
+    if (A.onepass) {
+        egm_scatter_kernel<<<(A.Na - 1 + 62) / 63, 64 * A.N, 0, st>>>(A);
         AIY_HIP(hipGetLastError());
         return AIY_OK;
     }

@@ -50,16 +50,24 @@ def ks_howard(value, k_opt, k_grid, K_grid, B, P, params, steps=50):
 
 
 def ks_vfi_solve(value, k_opt, k_grid, K_grid, B, P, params, howard_steps=50, tol=1e-6,
-                 max_vfi=10000, n_devices=1):
-    """Replaces the VFI loop :143-204 for one ALM coefficient vector B."""
+                 max_vfi=10000, n_devices=1, depth=None):
+    """Replaces the VFI loop :143-204 for one ALM coefficient vector B.  n_devices > 1: the
+    in-process (K, Z)-sliced solve (ks_vfi_solve_sharded), `depth` Howard sweeps per exchange
+    (default 4)."""
     V = np.array(value, dtype=np.float64, order="F", copy=True)
     ko = np.array(k_opt, dtype=np.float64, order="F", copy=True)
     nk, nK, nS = V.shape
     kg, Kg, B, P, prm = _arrs(k_grid, K_grid, B, P, params)
     it, rel = C.c_int64(), C.c_double()
-    check(lib().ks_vfi_solve(ptr(V), ptr(ko), ptr(kg), ptr(Kg), ptr(B), ptr(P), ptr(prm),
-                             i64(nk), i64(nK), i64(howard_steps), d(tol), i64(max_vfi),
-                             ip(n_devices), C.byref(it), C.byref(rel)))
+    if depth is not None:
+        check(lib().ks_vfi_solve_sharded(ptr(V), ptr(ko), ptr(kg), ptr(Kg), ptr(B), ptr(P),
+                                         ptr(prm), i64(nk), i64(nK), i64(howard_steps), d(tol),
+                                         i64(max_vfi), ip(n_devices), ip(depth), C.byref(it),
+                                         C.byref(rel)))
+    else:
+        check(lib().ks_vfi_solve(ptr(V), ptr(ko), ptr(kg), ptr(Kg), ptr(B), ptr(P), ptr(prm),
+                                 i64(nk), i64(nK), i64(howard_steps), d(tol), i64(max_vfi),
+                                 ip(n_devices), C.byref(it), C.byref(rel)))
     return dict(value=V, k_opt=ko, iters=it.value, rel_diff=rel.value)
 
 

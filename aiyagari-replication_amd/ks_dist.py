@@ -220,6 +220,15 @@ class HipShard:
     def hints(self, kopt):
         check(lib().ks_dev_hints(self._h, ptr(kopt), stream_handle(None)))
 
+    def slopes(self, V, dV):
+        """pchip slopes of every column this shard's sweep reads, into dV (full array)."""
+        check(lib().ks_dev_slopes(self._h, ptr(V), ptr(dV), stream_handle(None)))
+
+    def howard_fused(self, V, dV, kopt, Vout, dVout):
+        """One Howard sweep on this shard's nodes writing the next sweep's slopes too."""
+        check(lib().ks_dev_howard_fused(self._h, ptr(V), ptr(dV), ptr(kopt), ptr(Vout),
+                                        ptr(dVout), stream_handle(None)))
+
     def reldiff(self, V, Vold):
         import torch
         out = torch.zeros(2, dtype=torch.int64, device=V.device)
@@ -284,6 +293,7 @@ class HowardSweeps:
         self.rects = [(shard.K0, shard.K1, shard.s0, shard.s1)]
         self.shards = [shard]
         self.kx = None
+        self.dV = None
         nk = V.shape[-1]
         self.nk = nk
         if world > 1:
@@ -327,9 +337,28 @@ class HowardSweeps:
             self.kx(kopt)
             self.shards[-1].hints(kopt)
 
+    def _slope_bufs(self, V):
+        if self.dV is None:
+            import torch
+            self.dV = [torch.empty_like(V), torch.empty_like(V)]
+        return self.dV
+
     def run(self, V, V2, kopt, n):
         """n sweeps from V (current on the rank's nodes and halo); returns (V, V2) with V the
-        newest buffer, current on the rank's nodes and halo."""
+        newest buffer, current on the rank's nodes and halo.  One launch per sweep (the fused
+        Howard + next-slopes kernel) whenever the columns a sweep reads were all written by
+        the previous sweep: on one rank, and inside a ghost block; with a halo exchange after
+        every sweep (depth 1 on several ranks) the received columns need their slopes rebuilt,
+        so the sweep is slopes + Howard there."""
+        if self.depth == 1 and self.world == 1:
+            if n:
+                dV, dV2 = self._slope_bufs(V)
+                self.shard.slopes(V, dV)
+                for _ in range(n):
+                    self.shard.howard_fused(V, dV, kopt, V2, dV2)
+                    V, V2 = V2, V
+                    dV, dV2 = dV2, dV
+            return V, V2
         if self.depth == 1:
             for _ in range(n):
                 self.shard.howard(V, kopt, V2)
@@ -344,12 +373,15 @@ class HowardSweeps:
                     _exchange(V, self.rank, self.world, self.nK)
             return V, V2
         done = 0
+        dV, dV2 = self._slope_bufs(V)
         while done < n:
             L = min(self.depth, n - done)
             self.blocks[L](V)                     # R_L current at this sweep
+            self.shards[L - 1].slopes(V, dV)      # what R_{L-1} reads (inside R_L)
             for i in range(1, L + 1):
-                self.shards[L - i].howard(V, kopt, V2)   # R_{L-i} at sweep + i
+                self.shards[L - i].howard_fused(V, dV, kopt, V2, dV2)   # R_{L-i} at sweep + i
                 V, V2 = V2, V
+                dV, dV2 = dV2, dV
             done += L
         if n:
             self.halo(V)

@@ -125,7 +125,8 @@ def _ks_pmc():
 def ghost_model(pkg, dev, world=8, nk=32768, nK=64, depths=(1, 2, 3, 4, 6, 8), sweeps=24):
     """Compute side of the communication-avoiding schedule on ONE GPU: for each emulated rank
     of `world` (K-range shards of the scaling grid), the time of `sweeps` Howard sweeps run as
-    blocks of `depth` (ghost rectangles R_{L-1} .. R_0, ks_dist.HowardSweeps) without the
+    blocks of `depth` (one slopes launch over what R_{L-1} reads, then one fused Howard+slopes
+    launch per sweep over the ghost rectangles R_{L-1} .. R_0, ks_dist.HowardSweeps) without the
     exchanges — what each rank's GPU does between exchanges at N = world.  Returns, per depth,
     the slowest emulated rank's ms per sweep."""
     import numpy as np
@@ -135,6 +136,7 @@ def ghost_model(pkg, dev, world=8, nk=32768, nK=64, depths=(1, 2, 3, 4, 6, 8), s
     B = np.array([0.1, 0.97, 0.08, 0.975])
     V = torch.as_tensor(np.ascontiguousarray(V0.transpose(2, 1, 0)), device=dev)
     V2 = V.clone()
+    dV, dV2 = torch.empty_like(V), torch.empty_like(V)
     ko = torch.ones_like(V)
     out = {}
     for rank in range(world):
@@ -146,14 +148,16 @@ def ghost_model(pkg, dev, world=8, nk=32768, nK=64, depths=(1, 2, 3, 4, 6, 8), s
             shards = [sh] + [sh.ghost(*r) for r in rects[1:d]]
             shards[-1].hints(ko)
 
-            def run(n):
-                nonlocal V, V2
+            def run(n):  # ks_dist.HowardSweeps' fused block schedule without the exchanges
+                nonlocal V, V2, dV, dV2
                 done = 0
                 while done < n:
                     L = min(d, n - done)
+                    shards[L - 1].slopes(V, dV)
                     for i in range(1, L + 1):
-                        shards[L - i].howard(V, ko, V2)
+                        shards[L - i].howard_fused(V, dV, ko, V2, dV2)
                         V, V2 = V2, V
+                        dV, dV2 = dV2, dV
                     done += L
             run(d)
             torch.cuda.synchronize()

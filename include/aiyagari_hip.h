@@ -148,15 +148,26 @@ int ks_howard(double* value, const double* k_opt, const double* k_grid, const do
               int64_t steps);
 /* A6+A7 — replaces the VFI loop Krusell_Smith_VFI.m:143-204 for one ALM coefficient B:
  * improvement every 5th iteration, `howard_steps` sweeps, relative-diff stop (:195-203).
- * n_devices > 1 shards the K range (all four s) over n_devices shards on devices
- * (shard % visible devices) in one process; after every Howard sweep each shard refreshes
- * only the value columns (K'_idx, s') its slices read, by peer copies over xGMI.  Results
- * equal the single-device solve bit for bit.  k_opt is in/out (used until the first
- * improvement).  iters = VFI iterations run, rel_diff = last max relative change. */
+ * n_devices > 1 = ks_vfi_solve_sharded(..., n_devices, depth = 4).  k_opt is in/out (used
+ * until the first improvement).  iters = VFI iterations run, rel_diff = last max relative
+ * change. */
 int ks_vfi_solve(double* value, double* k_opt, const double* k_grid, const double* K_grid,
                  const double* B, const double* P, const double* params, int64_t nk,
                  int64_t nK, int64_t howard_steps, double tol, int64_t max_vfi,
                  int n_devices, int64_t* iters, double* rel_diff);
+/* The same loop over n_shards (K, Z) slices in one process: up to K_size
+ * shards split the K range (all four s), up to 2·K_size split each K range by aggregate state
+ * too (the reference K = 4 runs on 8 devices); shard d on device d % visible, peer access
+ * enabled between the devices in use.  Howard sweeps run in blocks of `depth`: before a block
+ * each shard receives the value columns of its ghost rectangle (every column its next `depth`
+ * sweeps read, peer copies over xGMI) and sweeps the shrinking rectangles with the fused
+ * Howard+slopes kernel — one exchange per block, event-synchronised on the streams.  Results
+ * equal the single-device solve bit for bit for every n_shards and depth. */
+int ks_vfi_solve_sharded(double* value, double* k_opt, const double* k_grid,
+                         const double* K_grid, const double* B, const double* P,
+                         const double* params, int64_t nk, int64_t nK, int64_t howard_steps,
+                         double tol, int64_t max_vfi, int n_shards, int depth, int64_t* iters,
+                         double* rel_diff);
 
 /* A8: the EGM policy iteration of Krusell_Smith_EGM.m:129-209 for the current B (replaces the
  * `for egm_iter = 1:max_egm` loop, :130-209).  k_opt: k_size x K_size x 4, in/out (:96 start).

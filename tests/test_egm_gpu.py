@@ -98,15 +98,19 @@ def test_egm_solve_nonmonotone_grid_is_reported(pkg, gpu):
     assert e.value.status == "AIY_BAD_ARG"
 
 
-@pytest.mark.parametrize("Na", [2, 3, 65, 400, 1024, 1025])
+@pytest.mark.parametrize("Na,N", [(2, 7), (3, 7), (65, 7), (400, 7), (1024, 7), (1025, 7),
+                                  (1090, 7), (4099, 7), (20000, 7), (3000, 2),
+                                  (2000, 16)])
 @pytest.mark.parametrize("labor", [False, True])
-def test_egm_fused_small_grid_equals_two_launches(pkg, gpu, Na, labor):
-    """Na <= 1024 runs a step as ONE launch (egm_fused_kernel, a workgroup per productivity
-    state); variant bit 11 forces the two-launch path.  Both, and the C restatement, agree bit
-    for bit over several steps (policy_c, policy_k, policy_l and the step's dist)."""
+def test_egm_fused_small_grid_equals_two_launches(pkg, gpu, Na, N, labor):
+    """Every step is ONE launch by default — egm_fused_kernel (a workgroup per productivity
+    state) for Na <= 1024, egm_scatter_kernel (segments → query ranges of the fixed a_grid) above;
+    variant bits 11 | 12 force the two-launch path.  Both, and the C restatement, agree bit for
+    bit over several steps (policy_c, policy_k, policy_l and the step's dist), N = 1 … 16."""
     import torch
     dev = torch.device("cuda", 0)
-    cal = no.calib_aiyagari(Na=Na, shocks="rouwenhorst")
+    cal = no.calib_aiyagari(Na=Na, shocks="rouwenhorst", N=N) if N != 7 else \
+        no.calib_aiyagari(Na=Na, shocks="rouwenhorst")
     a, s, P = cal["a_grid"], cal["s"], cal["P"]
     N = P.shape[0]
     r = 0.03
@@ -115,7 +119,7 @@ def test_egm_fused_small_grid_equals_two_launches(pkg, gpu, Na, labor):
     a_t, s_t, P_t = t(a), t(s), t(P)
     pc = np.tile(((1 + r) * a + w * np.mean(s))[None, :], (N, 1))
     runs = []
-    for var in (-1, 2048):
+    for var in (-1, 2048 | 4096):
         ws = pkg.Workspace(N, Na)
         if var >= 0:
             ws.set_variant(var)
@@ -143,10 +147,41 @@ def test_egm_fused_small_grid_equals_two_launches(pkg, gpu, Na, labor):
         assert np.array_equal(o, co) and np.array_equal(k, ko)
 
 
-def test_egm_nonmonotone_grid_is_reported_two_launch_path(pkg, gpu):
-    """Na > 1024 takes the two-launch path (flag word) — reported like the fused path (slots)."""
+def test_egm_nonmonotone_grid_is_reported_large_grid(pkg, gpu):
+    """Na > 1024: the one-pass scatter step (flag in the slots) reports a folding â like the
+    small-grid step; so does the two-launch step (flag word), forced by variant bit 12."""
+    import torch
     a = np.linspace(0, 10, 5000)
     pc0 = np.tile(np.linspace(50, 0.01, 5000)[:, None], (1, 2))
     with pytest.raises(pkg.AiyError) as e:
         pkg.egm_step(pc0, a, np.array([1.0, 1.2]), np.full((2, 2), 0.5), 0.02, 1.0, 0.96, 5.0, 0.0)
     assert e.value.status == "AIY_BAD_ARG"
+    with pytest.raises(pkg.AiyError):
+        pkg.egm_solve(pc0, a, np.array([1.0, 1.2]), np.full((2, 2), 0.5), 0.02, 1.0, 0.96, 5.0,
+                      0.0, 1e-6, 50)
+    dev = torch.device("cuda", 0)
+    t = lambda x: torch.as_tensor(np.ascontiguousarray(x), device=dev)
+    for var in (-1, 4096):
+        ws = pkg.Workspace(2, 5000)
+        ws.set_variant(var)
+        c = t(pc0.T)
+        o, k = torch.empty_like(c), torch.empty_like(c)
+        dd = torch.zeros(2, dtype=torch.int64, device=dev)
+        pkg.egm_step_dev(ws, c, t(a), t(np.array([1.0, 1.2])), t(np.full((2, 2), 0.5)), 0.02, 1.0,
+                         0.96, 5.0, 0.0, o, k, diff=dd)
+        torch.cuda.synchronize()  # device tier: no error return, the step still completes
+
+
+@pytest.mark.parametrize("Na", [10000, 1500])
+def test_egm_n1_large_grid_solve(pkg, gpu, Na):
+    """N = 1 with more than 64 tiles (the slot clearing of the two-launch step) —
+    the speculative solve on both large-grid paths equals the C loop."""
+    a = no.calib_aiyagari(Na=Na)["a_grid"]
+    s, P = np.array([1.0]), np.array([[1.0]])
+    w = no.wage(0.03, 0.36, 0.08)
+    pc0 = ((1.03) * a + w)[:, None]
+    Ro = corc.egm_solve(pc0.T, a, s, P, 0.03, w, 0.96, 5.0, 0.0, 1e-6, 300)
+    R = pkg.egm_solve(pc0, a, s, P, 0.03, w, 0.96, 5.0, 0.0, 1e-6, 300)
+    assert R["iters"] == Ro["iters"] and R["dist"] == Ro["dist"]
+    assert np.array_equal(R["policy_c"], Ro["policy_c"].T)
+    assert np.array_equal(R["policy_k"], Ro["policy_k"].T)

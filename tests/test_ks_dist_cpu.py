@@ -47,6 +47,12 @@ class OracleShard:
         vt = torch.from_numpy(np.ascontiguousarray(Vn.transpose(2, 1, 0)))
         Vout[self.s0:self.s1, self.K0:self.K1, :] = vt[self.s0:self.s1, self.K0:self.K1, :]
 
+    def slopes(self, V, dV):
+        pass  # the restatement rebuilds the slopes inside every sweep
+
+    def howard_fused(self, V, dV, kopt, Vout, dVout):
+        self.howard(V, kopt, Vout)
+
     def ghost(self, K0, K1, s0, s1):
         g = OracleShard(self.p, self.kg, self.Kg, self.B, self.P, K0, K1, s0, s1)
         g.kp_idx = self.kp_idx

@@ -81,3 +81,73 @@ def test_scaling_size_sharded_equals_unsharded(pkg, gpu):
     assert np.array_equal(R1["k_opt"], R4["k_opt"])
     assert R1["rel_diff"] == R4["rel_diff"]
     assert np.isfinite(R1["value"]).all()
+
+
+@pytest.mark.parametrize("shards,depth", [(8, 1), (8, 2), (8, 4), (5, 3), (2, 7), (6, 4)])
+def test_kz_sliced_ghost_blocks_reference_size(pkg, gpu, golden, shards, depth):
+    """The MATLAB-facing multi-device path (ks_vfi_solve_sharded) at the
+    reference grid (k = 100, K = 4, Krusell_Smith_VFI.m:8): up to 8 (K, Z) slices on this card,
+    ghost-rectangle blocks of `depth` Howard sweeps (10 sweeps: blocks that do not divide it),
+    improvement every 5th iteration — bit for bit the single-device solve and the C oracle."""
+    g, prm = _setup(golden)
+    B = np.array([0.1, 0.97, 0.08, 0.975])
+    args = (g["V0"], g["V0"] * 0 + 1.0, g["k_grid"], g["K_grid"], B, g["P"], prm)
+    R1 = pkg.ks_vfi_solve(*args, howard_steps=10, tol=1e-6, max_vfi=12)
+    Rs = pkg.ks_vfi_solve(*args, howard_steps=10, tol=1e-6, max_vfi=12, n_devices=shards,
+                          depth=depth)
+    assert Rs["iters"] == R1["iters"] and Rs["rel_diff"] == R1["rel_diff"]
+    assert np.array_equal(Rs["value"], R1["value"])
+    assert np.array_equal(Rs["k_opt"], R1["k_opt"])
+
+
+def test_kz_sliced_ghost_blocks_k4096(pkg, gpu):
+    """ks_vfi_solve(n_devices = 8) (depth 4) at k = 4,096, K = 16 (the fused Howard+slopes
+    kernel with multi-block columns: 4 halo nodes per 256), 2 policy improvements and 7
+    Howard sweeps per iteration, vs the single-device tiled solve."""
+    kg, Kg, P, V0 = pkg.calibration.krusell_smith(k_size=4096, K_size=16)
+    prm = pkg.ks_params()
+    B = np.array([0.1, 0.97, 0.08, 0.975])
+    k0 = np.ones_like(V0)
+    R1 = pkg.ks_vfi_solve(V0, k0, kg, Kg, B, P, prm, howard_steps=7, tol=0.0, max_vfi=6)
+    R8 = pkg.ks_vfi_solve(V0, k0, kg, Kg, B, P, prm, howard_steps=7, tol=0.0, max_vfi=6,
+                          n_devices=8)
+    assert R1["iters"] == R8["iters"] == 6 and R1["rel_diff"] == R8["rel_diff"]
+    assert np.array_equal(R1["value"], R8["value"])
+    assert np.array_equal(R1["k_opt"], R8["k_opt"])
+    assert np.isfinite(R1["value"]).all()
+
+
+def test_fused_howard_equals_two_launch_sweep(pkg, gpu):
+    """ks_dev_howard_fused (value + the next sweep's slopes in one launch) vs ks_dev_howard
+    (slopes launch + sweep) over a sharded rectangle, nk = 300 (two blocks per column, halo
+    nodes evaluated twice) and nk = 4,099 (a short last block)."""
+    import torch
+    for nk, nK in ((300, 6), (4099, 5)):
+        kg, Kg, P, V0 = pkg.calibration.krusell_smith(k_size=nk, K_size=nK)
+        B = np.array([0.1, 0.97, 0.08, 0.975])
+        kd = pkg.ks_dist
+        dev = torch.device("cuda:0")
+        V = torch.as_tensor(np.ascontiguousarray(V0.transpose(2, 1, 0)), device=dev)
+        ko = torch.ones_like(V)
+        sh = kd.HipShard(kg, Kg, B, P, pkg.ks_params(), 1, nK - 1, 0, 4)
+        sh.improve(V, ko)
+        A = V.clone()
+        for _ in range(3):  # two-launch sweeps
+            An = A.clone()
+            sh.howard(A, ko, An)
+            A = An
+        dV, dV2 = torch.zeros_like(V), torch.zeros_like(V)
+        Bv, B2 = V.clone(), V.clone()
+        sh.slopes(Bv, dV)
+        for _ in range(3):
+            sh.howard_fused(Bv, dV, ko, B2, dV2)
+            Bv, B2 = B2, Bv
+            dV, dV2 = dV2, dV
+        torch.cuda.synchronize()
+        own = slice(1, nK - 1)
+        assert torch.equal(A[:, own], Bv[:, own]), nk
+        ref = torch.zeros_like(V)
+        sh.slopes(Bv, ref)  # slopes of the final values, by the separate kernel
+        torch.cuda.synchronize()
+        assert torch.equal(ref[:, own], dV[:, own]), nk
+        sh.close()

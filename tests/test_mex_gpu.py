@@ -73,6 +73,12 @@ def test_ks_gateway(pkg, gpu, golden):
                          howard_steps=5, tol=1e-6, max_vfi=3)
     assert int(it[0, 0]) == R["iters"]
     assert np.array_equal(V.reshape(R["value"].shape, order="F"), R["value"])
+    # n_devices = 8 at the reference K = 4: the (K, Z)-sliced path, depth 2 (12th argument)
+    V8, ko8, it8, _ = mexstub.call("ks_vfi_solve_mex", 4, g["V0"], g["V0"] * 0 + 1, g["k_grid"],
+                                   g["K_grid"], B, g["P"], prm, 5.0, 1e-6, 3.0, 8.0, 2.0)
+    assert int(it8[0, 0]) == R["iters"]
+    assert np.array_equal(V8.reshape(R["value"].shape, order="F"), R["value"])
+    assert np.array_equal(ko8.reshape(R["k_opt"].shape, order="F"), R["k_opt"])
 
 
 def test_ks_egm_gateway(pkg, gpu, golden):
