@@ -54,12 +54,24 @@ struct BellArgs {
     // C > 1: every per-state array above is C consecutive blocks of its single layout, diff is
     // [C][2][2*kDiffSlots] (parity = sweep & 1 selects the set this sweep writes).
     int C;
+    bool ev_mfma;      // EV = (βP)·V by fp64 MFMA (bell_ev_mfma_kernel) before the table kernel
     const double* rv;  // [C] device: r of each candidate
     const double* wv;  // [C] device: w of each candidate
     const int* stop;   // [C] device: nonzero = stopped at that sweep (skipped from then on)
     int parity;
 };
 
+// EV by fp64 MFMA from this productivity-grid size up (the variant bits 14 / 15 force VALU /
+// MFMA); below it the table kernel's sequential VALU sum, which the C oracle restates bit for
+// bit.  The MFMA's accumulation order is the hardware's: parity there is to rounding (MATLAB's
+// own BLAS order for beta*P*v_old is unpinned).
+constexpr int kEvMfmaMinN = 32;
+inline bool bell_ev_mfma(int N, int variant) {
+    if (variant >= 0 && (variant & 16384)) return false;
+    if (variant >= 0 && (variant & 32768)) return true;
+    return N >= kEvMfmaMinN;
+}
+int launch_bell_ev_mfma(const BellArgs& A, hipStream_t st);
 int launch_bell_table(const BellArgs& A, hipStream_t st);
 int launch_bell_kf(const BellArgs& A, hipStream_t st);
 int launch_bell_init(const BellArgs& A, hipStream_t st);

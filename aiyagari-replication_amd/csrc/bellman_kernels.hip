@@ -183,6 +183,42 @@ __device__ __forceinline__ BellArgs bell_cand(const BellArgs& A, int c) {
     return B;
 }
 
+// ------------------------------------------------------------------------------ 0. EV by MFMA
+// EV = (βP)·V on the fp64 matrix cores (v_mfma_f64_16x16x4_f64) when Nz is large enough for
+// the expectation to be a real contraction (north star).  A wave owns a 16 (i) x 16 (k) tile of
+// EV and walks m in steps of 4: A = βP[i][m] (lane l: row l & 15, m = l >> 4 — the product βP
+// formed first, as the reference's (beta * P) * v_old associates), B = V[m][k] (lane l: m =
+// l >> 4, column l & 15), C/D in the f64 layout (column l & 15, row (l >> 4) + 4·reg).  Four
+// waves per block cover 64 consecutive k; blockIdx.y = 16-row tile, blockIdx.z = candidate
+// (config 4 batches; stopped candidates are skipped).  Out-of-range rows/columns/m are zero.
+typedef double aiy_v4d __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void bell_ev_mfma_kernel(int N, int Na,
+                                                           const double* __restrict__ P,
+                                                           const double* __restrict__ V,
+                                                           double beta, double* __restrict__ EV,
+                                                           const int* __restrict__ stop) {
+    const int c = blockIdx.z;
+    if (stop && stop[c]) return;  // block-uniform
+    const size_t o = (size_t)c * N * Na;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int i0 = blockIdx.y * 16, k0 = blockIdx.x * 64 + wave * 16;
+    const int r = lane & 15, q = lane >> 4;
+    const int ia = i0 + r, kb = k0 + r;
+    aiy_v4d acc = {0.0, 0.0, 0.0, 0.0};
+    for (int m0 = 0; m0 < N; m0 += 4) {
+        const int m = m0 + q;
+        const double av = (ia < N && m < N) ? beta * P[ia * N + m] : 0.0;
+        const double bv = (m < N && kb < Na) ? V[o + (size_t)m * Na + kb] : 0.0;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+    }
+    const int kc = k0 + r;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int i = i0 + q + 4 * g;
+        if (i < N && kc < Na) EV[o + (size_t)i * Na + kc] = acc[g];
+    }
+}
+
 // ------------------------------------------------------------------------------ 1. table
 __device__ __forceinline__ double table_ev(int N, int Na, const double* __restrict__ P,
                                            const double* __restrict__ V, double beta, int i,
@@ -208,7 +244,7 @@ __global__ __launch_bounds__(kTableBlock) void bell_table_kernel(
     float* __restrict__ T32, int CK, double* __restrict__ Dm, double* __restrict__ Dm8,
     double* __restrict__ Dm512, int nb, int nb8, int nb512,
     unsigned long long* __restrict__ diff, double* __restrict__ Dt,
-    unsigned long long* __restrict__ fold) {
+    unsigned long long* __restrict__ fold, bool ev_in) {
     __shared__ double s_max[kTableBlock / 64];
     const int i = blockIdx.y;
     const int k = blockIdx.x * kTableBlock + threadIdx.x;
@@ -233,15 +269,21 @@ __global__ __launch_bounds__(kTableBlock) void bell_table_kernel(
     double D = -__builtin_inf();
     if (ok) {
         const size_t t = (size_t)i * Na + k;
-        double acc = table_ev(N, Na, P, V, beta, i, k);
-        EV[t] = acc;
+        double acc;
+        if (ev_in) {  // EV already written by bell_ev_mfma_kernel
+            acc = EV[t];
+        } else {
+            acc = table_ev(N, Na, P, V, beta, i, k);
+            EV[t] = acc;
+        }
         if (T || Dt) {
             D = table_D(acc, np);
             if (T) T[t] = make_double2(a[k], D);
             if (Dt) Dt[t] = D;
             if (T32) {  // relative to the chunk origin (a, D at k0): small magnitudes, fine ulps
                 int k0 = k - k % CK;
-                double D0 = table_D(table_ev(N, Na, P, V, beta, i, k0), np);
+                double D0 = table_D(ev_in ? EV[(size_t)i * Na + k0]
+                                          : table_ev(N, Na, P, V, beta, i, k0), np);
                 float* pr = T32 + 2 * (size_t)i * (Na + (Na & 1)) + 2 * (k & ~1) + (k & 1);
                 pr[0] = f32_dn(a[k] - a[k0]);  // pair layout {a_k, a_k+1, D_k, D_k+1}
                 pr[2] = f32_up(D - D0);
@@ -288,7 +330,8 @@ __global__ __launch_bounds__(kTableBlock) void bell_table_batch_kernel(
     int N, int Na, const double* __restrict__ P, const double* __restrict__ V, double beta,
     int np, const double* __restrict__ a, double* __restrict__ EV, double* __restrict__ Dt,
     double* __restrict__ Dm8, double* __restrict__ Dm512, int nb8, int nb512,
-    unsigned long long* __restrict__ slots, int* __restrict__ stop, int sweep, double tol) {
+    unsigned long long* __restrict__ slots, int* __restrict__ stop, int sweep, double tol,
+    bool ev_in) {
     __shared__ double s_max[kTableBlock / 64];
     __shared__ int s_stop;
     const int c = blockIdx.y / N, i = blockIdx.y - c * N;
@@ -319,8 +362,13 @@ __global__ __launch_bounds__(kTableBlock) void bell_table_batch_kernel(
     double D = -__builtin_inf();
     if (ok) {
         const size_t t = o + (size_t)i * Na + k;
-        const double acc = table_ev(N, Na, P, V + o, beta, i, k);
-        EV[t] = acc;
+        double acc;
+        if (ev_in) {
+            acc = EV[t];
+        } else {
+            acc = table_ev(N, Na, P, V + o, beta, i, k);
+            EV[t] = acc;
+        }
         D = table_D(acc, np);
         Dt[t] = D;
     }
@@ -352,7 +400,7 @@ int launch_bell_table_batch(const BellArgs& A, unsigned long long* slots, int sw
     dim3 grid((A.Na + kTableBlock - 1) / kTableBlock, A.C * A.N);
     bell_table_batch_kernel<<<grid, kTableBlock, 0, st>>>(
         A.N, A.Na, A.P, A.v_old, A.beta, A.np, A.a, A.EV, A.Dt, A.Dm8, A.Dm512, A.nb8, A.nb512,
-        slots, const_cast<int*>(A.stop), sweep, tol);
+        slots, const_cast<int*>(A.stop), sweep, tol, A.ev_mfma);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }
@@ -1996,14 +2044,24 @@ static void launch_dispatch_timed(K kernel, int grid, int block, hipStream_t st,
     }
 }
 
+int launch_bell_ev_mfma(const BellArgs& A, hipStream_t st) {
+    const dim3 grid(cdiv(A.Na, 64), cdiv(A.N, 16), std::max(A.C, 1));
+    bell_ev_mfma_kernel<<<grid, 256, 0, st>>>(A.N, A.Na, A.P, A.v_old, A.beta, A.EV,
+                                              A.C > 1 ? A.stop : nullptr);
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
+}
+
 int launch_bell_table(const BellArgs& A, hipStream_t st) {
     static_assert(2 * kDiffSlots <= kTableBlock, "table block clears the diff slots");
     dim3 grid(cdiv(A.Na, kTableBlock), A.N);
     const bool scr = A.np > 0;
+    if (A.ev_mfma) AIY_TRY(launch_bell_ev_mfma(A, st));
     bell_table_kernel<<<grid, kTableBlock, 0, st>>>(
         A.N, A.Na, A.P, A.v_old, A.beta, A.np, A.a, A.EV, (scr && !A.tree) ? A.T : nullptr,
         scr ? A.T32 : nullptr, A.CK, scr ? A.Dm : nullptr, scr ? A.Dm8 : nullptr,
-        scr ? A.Dm512 : nullptr, A.nb, A.nb8, A.nb512, A.diff, scr ? A.Dt : nullptr, A.fold);
+        scr ? A.Dm512 : nullptr, A.nb, A.nb8, A.nb512, A.diff, scr ? A.Dt : nullptr, A.fold,
+        A.ev_mfma);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }
@@ -2020,7 +2078,7 @@ int launch_bell_kf(const BellArgs& A, hipStream_t st) {
 #define AIY_BELL_R 2
 #endif
 bool bell_persist_eligible(const BellArgs& A) {
-    return A.np >= 1 && A.np <= 8 && !A.labor && A.C <= 1 && A.tree && A.Na <= 4096 &&
+    return A.np >= 1 && A.np <= 8 && !A.labor && A.C <= 1 && A.tree && A.Na <= 4096 && !A.ev_mfma &&
            A.Dt && A.Dm8 && A.Dm512 && !A.hitcount && !A.trace;
 }
 

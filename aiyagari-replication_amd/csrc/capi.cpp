@@ -141,6 +141,7 @@ static int bell_args(aiy_ws* ws, const BellCall& c, BellArgs& A, hipStream_t st)
     const int var = ws->variant >= 0 ? ws->variant
                                      : (ws->Na <= 4096 ? (c.labor ? 4 | 4096 : 2) : 16);
     A.variant = var;
+    A.ev_mfma = bell_ev_mfma(A.N, ws->variant);
     A.r = c.r;
     A.w = c.w;
     A.beta = c.beta;
@@ -525,6 +526,7 @@ int bell_solve_batch_dev(aiy_ws* ws, int64_t C, const double* r, const double* w
     A.coarse = ws->coarse; A.CK = ws->CK;
     A.variant = ws->variant >= 0 ? ws->variant : (ws->Na <= 4096 ? 0 : 16);
     A.variant &= ~(1 | 2 | 4 | 8);  // one state per lane, one wave per tile, tree screen
+    A.ev_mfma = bell_ev_mfma(A.N, ws->variant);
     A.beta = beta; A.sigma = sigma; A.a = a; A.s = s; A.P = P;
     A.EV = ws->bEV; A.Dt = ws->bDt; A.Dm8 = ws->bDm8; A.Dm512 = ws->bDm512;
     A.nb = (int)((ws->Na + 63) / 64); A.nb8 = nb8; A.nb512 = nb512;
@@ -545,6 +547,7 @@ int bell_solve_batch_dev(aiy_ws* ws, int64_t C, const double* r, const double* w
             A.v_new = buf[g & 1];
             A.parity = (int)(g & 1);
             A.hint = (g == 1 && !use_hint) ? nullptr : idx;
+            if (A.ev_mfma) AIY_TRY(launch_bell_ev_mfma(A, st));
             AIY_TRY(launch_bell_table_batch(A, ws->bslots, (int)g, tol, st));
             if (!A.hint) AIY_TRY(launch_bell_init(A, st));
             AIY_TRY(ws_timing_begin(ws, st));
@@ -698,7 +701,7 @@ int aiy_ws_invalidate(aiy_ws* ws) {
 
 int aiy_ws_set_variant(aiy_ws* ws, int variant) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
-    if (variant < -1 || variant > 16383) return fail(AIY_BAD_ARG, "variant in [-1, 16383]");
+    if (variant < -1 || variant > 65535) return fail(AIY_BAD_ARG, "variant in [-1, 65535]");
     ws->variant = variant;
     return AIY_OK;
 }

@@ -77,7 +77,10 @@ int orc_sim_capital(int64_t N, int64_t Na, const double* policy, int64_t z_strid
                     double k1, int64_t T, const double* uniforms, double* mean_k,
                     double* sim_k);
 
-/* A10 (new): one histogram push λ -> λ' for an on-grid (idx) or off-grid (kp) policy. */
+/* A10 (new): one histogram push λ -> λ' for an on-grid (idx) or off-grid (kp) policy.  The
+ * mass of a destination sums its terms in ascending source j in chunks of 32 (chunk sums summed
+ * in order) — the order the HIP gather kernel follows (csrc/dist.hpp kDistChunk); runs of up
+ * to 32 terms are the plain sequential scatter. */
 int orc_dist_update_ongrid(int64_t N, int64_t Na, const double* lam, const int32_t* idx,
                            const double* P, double* lam_out);
 int orc_dist_update_lottery(int64_t N, int64_t Na, const double* lam, const double* kp,
