@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "aiy_common.hpp"
+
 namespace aiy {
 struct EgmArgs {
     int N, Na;
@@ -21,10 +23,13 @@ struct EgmArgs {
     unsigned* flags;           // bit 0: a_hat not increasing (small-grid fused step: bit 1 of
                                // the diff slots' second word instead, see egm_fused_kernel)
     bool fused;                // Na <= 1024: one launch per step (egm_fused_kernel)
-    bool onepass;              // Na > 1024: one launch per step (egm_scatter_kernel); the
-                               // caller zeroes `diff` before the launch, the flag rides in
-                               // bit 1 of the slots' second words
+    bool onepass;              // Na > 1024: one launch per step (egm_scatter_kernel); `diff`
+                               // must be zero at launch (the previous step cleared it, see
+                               // diff_clear), the flag rides in bit 1 of the slots' second words
+    unsigned long long* diff_clear;  // onepass: the next step's slot set (kEgmSlotWords words),
+                                     // zeroed by this launch's first workgroup (nullable)
 };
+constexpr int kEgmSlotWords = 2 * kDiffSlots + 2;  // {max bits, any} x kDiffSlots + flag word
 constexpr int kEgmFusedMaxNa = 1024;  // egm_fused_kernel: one state per thread
 int launch_egm_step(const EgmArgs& A, hipStream_t st);
 }  // namespace aiy

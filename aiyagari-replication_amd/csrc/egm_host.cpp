@@ -37,6 +37,11 @@ static int ensure_egm(aiy_ws* ws) {
         AIY_HIP(hipMalloc((void**)&ws->diff, 2 * kDiffSlots * sizeof(unsigned long long)));
     if (!ws->hdiff)
         AIY_HIP(hipHostMalloc((void**)&ws->hdiff, (2 * kDiffSlots + 4) * sizeof(unsigned long long)));
+    if (!ws->egm_d2) {
+        AIY_HIP(hipMalloc((void**)&ws->egm_d2, 2 * kEgmSlotWords * sizeof(unsigned long long)));
+        AIY_HIP(hipMemset(ws->egm_d2, 0, 2 * kEgmSlotWords * sizeof(unsigned long long)));
+        ws->egm_par = 0;
+    }
     return AIY_OK;
 }
 
@@ -55,10 +60,13 @@ static EgmArgs egm_args(aiy_ws* ws, const double* c, const double* a, const doub
     A.ahat = ws->g0; A.cnext = ws->g1; A.cout = cout; A.pk = pk; A.pl = pl;
     A.diff = ws->diff;
     A.flags = (unsigned*)ws->gi;
-    // one launch per step: egm_fused_kernel on small grids, egm_scatter_kernel on large ones,
-    // unless the tuning variant sets bit 11 / bit 12 (the two-launch step, A/B only)
+    // small grids: one launch per step (egm_fused_kernel) unless the tuning variant sets bit 11;
+    // large grids: the two-launch step, or the one-pass egm_scatter_kernel with variant bit 12
+    // (opt-in: a segment owns its queries, and where â_j falls into the dense low end of the
+    // quadratic a_grid one wave owns thousands of them — 35.6 vs 12.1 us per step at
+    // Na = 20,000, profiles/r03_s3b_egm_ab.json)
     A.fused = !(ws->variant >= 0 && (ws->variant & 2048));
-    A.onepass = A.Na > kEgmFusedMaxNa && !(ws->variant >= 0 && (ws->variant & 4096));
+    A.onepass = A.Na > kEgmFusedMaxNa && ws->variant >= 0 && (ws->variant & 4096);
     return A;
 }
 
@@ -70,23 +78,34 @@ int egm_step_dev(aiy_ws* ws, const double* c, const double* a, const double* s, 
     if (labor && !(phi == phi && theta == theta)) return fail(AIY_NON_FINITE, "phi/theta");
     AIY_TRY(ensure_egm(ws));
     EgmArgs A = egm_args(ws, c, a, s, P, r, w, beta, sigma, amin, labor, phi, theta, cout, pk, pl);
-    // the two-launch and small-grid steps clear the diff slots and the flag word themselves;
-    // the one-pass scatter step accumulates from its first wave, so they are zeroed here
-    if (A.onepass)
-        AIY_HIP(hipMemsetAsync(ws->diff, 0, 2 * kDiffSlots * sizeof(unsigned long long), st));
+    // the two-launch and small-grid steps clear ws->diff and the flag word themselves; the
+    // one-pass scatter step accumulates from its first wave into a slot set the previous
+    // one-pass step (or the allocation) zeroed, and zeroes the other set for the next step
+    ws->egm_cur = ws->diff;
+    if (A.onepass) {
+        ws->egm_cur = ws->egm_d2 + (size_t)ws->egm_par * kEgmSlotWords;
+        A.diff = ws->egm_cur;
+        A.flags = (unsigned*)(ws->egm_cur + 2 * kDiffSlots);
+        A.diff_clear = ws->egm_d2 + (size_t)(ws->egm_par ^ 1) * kEgmSlotWords;
+        ws->egm_par ^= 1;
+    }
     AIY_TRY(ws_timing_begin(ws, st));
     AIY_TRY(launch_egm_step(A, st));
     AIY_TRY(ws_timing_end(ws, st));
-    if (diff_out) AIY_TRY(launch_reduce_slots(ws->diff, diff_out, st));
+    if (diff_out) AIY_TRY(launch_reduce_slots(ws->egm_cur, diff_out, st));
     return AIY_OK;
 }
 
 // dist of the last step + the non-monotone-grid flag (synchronises)
 static int read_egm(aiy_ws* ws, hipStream_t st, double* d) {
     unsigned long long* h = ws->hdiff;
-    AIY_HIP(hipMemcpyAsync(h, ws->diff, 2 * kDiffSlots * sizeof(unsigned long long),
+    const unsigned long long* src = ws->egm_cur ? ws->egm_cur : ws->diff;
+    AIY_HIP(hipMemcpyAsync(h, src, 2 * kDiffSlots * sizeof(unsigned long long),
                            hipMemcpyDeviceToHost, st));
-    AIY_HIP(hipMemcpyAsync(h + 2 * kDiffSlots, ws->gi, sizeof(int), hipMemcpyDeviceToHost, st));
+    if (src == ws->diff)  // the two-launch step's flag word (one-pass: in the slots)
+        AIY_HIP(hipMemcpyAsync(h + 2 * kDiffSlots, ws->gi, sizeof(int), hipMemcpyDeviceToHost, st));
+    else
+        h[2 * kDiffSlots] = 0;
     AIY_HIP(hipStreamSynchronize(st));
     *d = fold_slots_host(h);
     if (egm_nonmonotone(h, (unsigned)h[2 * kDiffSlots])) return fail_nonmonotone();
@@ -95,9 +114,10 @@ static int read_egm(aiy_ws* ws, hipStream_t st, double* d) {
 
 // The solve loop (Aiyagari_EGM.m:74-108, labour :67-105) with speculative batches, as the VFI
 // solve (capi.cpp, bell_solve_spec): steps are deterministic, so m steps are enqueued between
-// reads — step g reads ring slot (g−1) mod R and writes slot g mod R, its dist lands in its
-// own slot set and its flag word — and one D2H read per batch finds the first step whose dist
-// is not above tol.  The ring keeps that step's policy_c; its policy_k (and policy_l) were
+// reads — step g reads ring slot (g−1) mod R and writes slot g mod R, its dist lands in slot
+// set g mod R with its flag word (the one-pass step zeroes set (g+1) mod R for the next step;
+// the sets are zeroed once per solve) — and one D2H read per batch finds the first step whose
+// dist is not above tol.  The ring keeps that step's policy_c; its policy_k (and policy_l) were
 // overwritten by later speculative steps, so the stopping step is re-run from its input
 // (identical values).  Iteration count, dist and outputs equal the one-read-per-step loop's.
 static int egm_solve_spec(aiy_ws* ws, const EgmArgs& A0, double* c0, double tol,
@@ -105,23 +125,27 @@ static int egm_solve_spec(aiy_ws* ws, const EgmArgs& A0, double* c0, double tol,
                           hipStream_t st) {
     const int M = ws->spec_max, R = M + 1;
     const size_t n = (size_t)ws->N * ws->Na, nb = n * sizeof(double);
-    const int SW = 2 * kDiffSlots + 2;  // per step: {max bits, any} slots, then the flag word
+    const int SW = kEgmSlotWords;  // per step: {max bits, any} slots, then the flag word
+    const size_t SB = (size_t)R * SW * sizeof(unsigned long long);
     if (ws->egm_spec_n != n || ws->egm_spec_m != M) {
         ws->free_egm_spec();
         AIY_HIP(hipMalloc((void**)&ws->egm_ring, (size_t)R * nb));
-        AIY_HIP(hipMalloc((void**)&ws->egm_slots, (size_t)M * SW * sizeof(unsigned long long)));
-        AIY_HIP(hipHostMalloc((void**)&ws->egm_hslots, (size_t)M * SW * sizeof(unsigned long long)));
+        AIY_HIP(hipMalloc((void**)&ws->egm_slots, SB));
+        AIY_HIP(hipHostMalloc((void**)&ws->egm_hslots, SB));
         ws->egm_spec_n = n;
         ws->egm_spec_m = M;
     }
     auto slot = [&](int64_t g) { return ws->egm_ring + (size_t)(g % R) * n; };
+    auto sset = [&](int64_t g) { return ws->egm_slots + (size_t)(g % R) * SW; };
     AIY_HIP(hipMemcpyAsync(slot(0), c0, nb, hipMemcpyDeviceToDevice, st));
-    auto step = [&](int64_t g, int t) {
+    if (A0.onepass) AIY_HIP(hipMemsetAsync(ws->egm_slots, 0, SB, st));
+    auto step = [&](int64_t g) {
         EgmArgs A = A0;
         A.c = slot(g - 1);
         A.cout = slot(g);
-        A.diff = ws->egm_slots + (size_t)t * SW;
-        A.flags = (unsigned*)(ws->egm_slots + (size_t)t * SW + 2 * kDiffSlots);
+        A.diff = sset(g);
+        A.flags = (unsigned*)(sset(g) + 2 * kDiffSlots);
+        A.diff_clear = A0.onepass ? sset(g + 1) : nullptr;
         return launch_egm_step(A, st);
     };
     int64_t done = 0, stop = 0, last_enq = 0;
@@ -133,16 +157,12 @@ static int egm_solve_spec(aiy_ws* ws, const EgmArgs& A0, double* c0, double tol,
             if (need >= 1 && need < (double)m) m = (int64_t)need;
         }
         m = std::min<int64_t>(std::max<int64_t>(m, 1), max_iter - done);
-        if (A0.onepass)  // the scatter step does not clear its own slots
-            AIY_HIP(hipMemsetAsync(ws->egm_slots, 0, (size_t)m * SW * sizeof(unsigned long long), st));
-        for (int64_t t = 0; t < m; ++t) AIY_TRY(step(done + 1 + t, (int)t));
+        for (int64_t t = 0; t < m; ++t) AIY_TRY(step(done + 1 + t));
         last_enq = done + m;
-        AIY_HIP(hipMemcpyAsync(ws->egm_hslots, ws->egm_slots,
-                               (size_t)m * SW * sizeof(unsigned long long),
-                               hipMemcpyDeviceToHost, st));
+        AIY_HIP(hipMemcpyAsync(ws->egm_hslots, ws->egm_slots, SB, hipMemcpyDeviceToHost, st));
         AIY_HIP(hipStreamSynchronize(st));
         for (int64_t t = 0; t < m; ++t) {
-            const unsigned long long* h = ws->egm_hslots + (size_t)t * SW;
+            const unsigned long long* h = ws->egm_hslots + (size_t)((done + 1 + t) % R) * SW;
             if (egm_nonmonotone(h, (unsigned)h[2 * kDiffSlots])) return fail_nonmonotone();
             const double d = fold_slots_host(h);
             d_prev = d_last;
@@ -156,11 +176,8 @@ static int egm_solve_spec(aiy_ws* ws, const EgmArgs& A0, double* c0, double tol,
         if (!stop) done += m;
     }
     const int64_t g = stop ? stop : done;
-    if (g > 0 && g != last_enq) {  // policy_k/l of the stopping step
-        if (A0.onepass)
-            AIY_HIP(hipMemsetAsync(ws->egm_slots, 0, SW * sizeof(unsigned long long), st));
-        AIY_TRY(step(g, 0));
-    }
+    if (g > 0 && g != last_enq) AIY_TRY(step(g));  // policy_k/l of the stopping step (its
+                                                   // slots are not read again)
     *cur_out = g > 0 ? slot(g) : slot(0);
     *dist = d_stop;
     *iters = g;

@@ -283,10 +283,18 @@ __global__ __launch_bounds__(1024) void egm_fused_kernel(EgmArgs A) {
 // its 64 increasing â (two 64-ary ballot searches of a_grid and an LDS window), and lane k
 // writes the outputs of its queries with its own (â_k, â_{k+1}, y_k, y_{k+1}) — the same
 // formulas, on the same segment, as egm_interp_kernel, so bit for bit the two-launch step.
-// A segment with more than 4 queries (the borrowing-constraint region, the clamps at both
-// ends) is finished by the whole wave, 64 queries at a time.  â_j not strictly increasing
-// (an adjacent pair checked per lane) sets bit 1 of the slot's second word: the host fails
-// the call, as the two-launch step does.  diff must be zero at launch (no in-launch clear).
+// The two end segments hold the long runs: segment 0 takes every query below â_1 (the
+// borrowing-constraint region, thousands of nodes for low productivity at Na = 20,000) and
+// segment Na−2 every query from â_{Na−2} up.  Their owners would walk those runs serially, so
+// instead every workgroup recomputes the four end nodes â_j(0, 1, Na−2, Na−1) of every row
+// (4N u′ evaluations in parallel lanes, the Euler sums in m order, four pows per wave) and
+// answers the end-segment queries among its own query indices i ∈ [63b, 63b + 63) — query i
+// is in segment 0 iff a_i < â_1 and in segment Na−2 iff a_i >= â_{Na−2}, the same tests that
+// define B_1 and B_{Na−2}.  Another segment with more than 4 queries is finished by the whole
+// wave, 64 queries at a time.  â_j not strictly increasing (an adjacent pair checked per
+// lane) sets bit 1 of the slot's second word: the host fails the call, as the two-launch step
+// does.  diff must be zero at launch; the first workgroup zeroes the next step's slot set
+// (diff_clear), so a step is one launch.
 __global__ __launch_bounds__(1024) void egm_scatter_kernel(EgmArgs A) {
     __shared__ double s_up[16][64];
     __shared__ double s_a[16][256];
@@ -295,11 +303,40 @@ __global__ __launch_bounds__(1024) void egm_scatter_kernel(EgmArgs A) {
     const int k = blockIdx.x * 63 + lane;
     const bool okk = k < Na;
     const double* __restrict__ ag = A.a;
+    if (blockIdx.x == 0 && A.diff_clear)  // the next step's slots (a different set)
+        for (int q = threadIdx.x; q < kEgmSlotWords; q += blockDim.x) A.diff_clear[q] = 0ull;
+    // u'(c_q) at the end nodes {0, 1, Na−2, Na−1}: lane 4q + e of every wave (N <= 16)
+    const int e_end = lane & 3, q_end = lane >> 2;
+    const int k_end = e_end < 2 ? e_end : Na - 4 + e_end;
+    const double up_end =
+        q_end < N ? uprime_dev(A.c[(size_t)q_end * Na + k_end], A.sigma, A.ns) : 0.0;
     s_up[m][lane] = okk ? uprime_dev(A.c[(size_t)m * Na + k], A.sigma, A.ns) : 0.0;
     __syncthreads();
     const int j = m;
     const double coef0 = A.beta * (1 + A.r);
     const double ws = A.w * A.s[j];
+    // â_j and y_j at the end nodes (lanes 0-3), the same operations as the owners' below
+    double ahe = 0.0, ye = 0.0;
+    {
+        double acc = 0.0;
+        for (int q = 0; q < N; ++q)
+            acc = acc + (coef0 * A.P[j * N + q]) * __shfl(up_end, 4 * q + e_end);
+        if (lane < 4) {
+            const double cn = aiy_pow(acc, -1.0 / A.sigma);  // :88
+            const double akv = ag[k_end];
+            if (A.labor) {
+                const double ls = labor_dev(cn, ws, A.sigma, A.ns, A.phi, A.theta);
+                ahe = ((cn + akv) - ws * ls) / (1 + A.r);
+            } else {
+                ahe = ((cn + akv) - ws) / (1 + A.r);
+            }
+            ye = A.labor ? cn : akv;
+        }
+    }
+    const double xe0 = readlane_d(ahe, 0), xe1 = readlane_d(ahe, 1);
+    const double ye0 = readlane_d(ye, 0), ye1 = readlane_d(ye, 1);
+    const double xt0 = readlane_d(ahe, 2), xt1 = readlane_d(ahe, 3);
+    const double yt0 = readlane_d(ye, 2), yt1 = readlane_d(ye, 3);
     double ah = 0.0, yk = 0.0;
     if (okk) {
         double acc = 0.0;
@@ -364,10 +401,10 @@ __global__ __launch_bounds__(1024) void egm_scatter_kernel(EgmArgs A) {
         }
         Bk = lo;
     }
-    if (k == 0) Bk = 0;  // segment 0 also takes every query below â_0
-    int Bk1 = __shfl_down(Bk, 1);
-    if (k == Na - 2) Bk1 = Na;  // segment Na−2 takes every query from â_{Na−2} up
-    int b = own ? Bk : 0, e = own ? Bk1 : 0;
+    const int Bk1 = __shfl_down(Bk, 1);
+    // segments 0 and Na−2 are answered per query index below, not by their owners
+    const bool mid = own && k != 0 && k != Na - 2;
+    int b = mid ? Bk : 0, e = mid ? Bk1 : 0;
     b = min(max(b, 0), Na);
     e = min(max(e, b), Na);
     const double r1 = 1 + A.r;
@@ -400,6 +437,14 @@ __global__ __launch_bounds__(1024) void egm_scatter_kernel(EgmArgs A) {
             any = true;
         }
     };
+    {  // end segments among this workgroup's query indices (lane 63 only in the last one)
+        const int i = blockIdx.x * 63 + lane;
+        if (i < Na && (lane < 63 || blockIdx.x == gridDim.x - 1)) {
+            const double qa = ag[i];
+            if (qa < xe1) query(i, xe0, xe1, ye0, ye1);           // i < B_1: segment 0
+            else if (qa >= xt0) query(i, xt0, xt1, yt0, yt1);     // i >= B_{Na−2}
+        }
+    }
     constexpr int kShort = 4;
     for (int u = 0; u < kShort; ++u)
         if (b + u < e) query(b + u, ah, ah1, yk, yk1);

@@ -85,8 +85,13 @@ struct aiy_ws {
     size_t egm_spec_n = 0;
     int egm_spec_m = 0;
     double* egm_ring = nullptr;
-    unsigned long long* egm_slots = nullptr;    // device [spec_max][2*kDiffSlots + 2]
+    unsigned long long* egm_slots = nullptr;    // device [spec_max + 1][2*kDiffSlots + 2]
     unsigned long long* egm_hslots = nullptr;   // pinned host, same shape
+    // single EGM steps on the one-pass path: two slot sets (step t writes set t & 1 and clears
+    // the other), zeroed at allocation; egm_cur = the set of the last step
+    unsigned long long* egm_d2 = nullptr;
+    unsigned long long* egm_cur = nullptr;
+    int egm_par = 0;
     void free_egm_spec() {
         if (egm_ring) (void)hipFree(egm_ring);
         if (egm_slots) (void)hipFree(egm_slots);
@@ -140,7 +145,7 @@ struct aiy_ws {
     }
     void free_all() {
         void* ps[] = {EV, T, T32, Dm, Dm8, Dt, Dm512, touched, best0, idx0, mom, dis, kf, partial, diff, hitcount, trace, g0, g1, g2, gi,
-                      d_key, d_off, d_wr, d_mass, d_part, pers};
+                      d_key, d_off, d_wr, d_mass, d_part, pers, egm_d2};
         for (void* p : ps)
             if (p) (void)hipFree(p);
         free_spec();
@@ -152,6 +157,7 @@ struct aiy_ws {
         kf_ok = false;
         idx0 = nullptr; mom = nullptr; partial = nullptr; diff = nullptr; hitcount = nullptr; trace = nullptr; trace_cap = 0; hdiff = nullptr;
         g0 = g1 = g2 = nullptr; gi = nullptr; pers = nullptr;
+        egm_d2 = egm_cur = nullptr; egm_par = 0;
         d_key = d_off = nullptr; d_wr = d_mass = d_part = nullptr;
         partial_cap = 0;
     }

@@ -225,10 +225,13 @@ def egm_leg(pkg, dev, Na, labor=False, steps=50, reps=5, cpu_threads=1, variant=
         walls.append(time.perf_counter() - t0)
         iters = R["iters"]
     solve_s = _median(walls)
-    fused = Na <= 1024 and not (variant >= 0 and variant & 2048)
-    return {"workload": f"{name} steps, Na={Na} Nz={N} Rouwenhorst, device tier (" +
-                        ("1 launch per step: egm_fused_kernel, a workgroup per z-state)" if fused
-                         else "2 launches per step: Euler RHS, interp1 inversion)"),
+    if Na <= 1024 and not (variant >= 0 and variant & 2048):
+        path = "1 launch per step: egm_fused_kernel, a workgroup per z-state)"
+    elif Na > 1024 and variant >= 0 and variant & 4096:
+        path = "1 launch per step: egm_scatter_kernel, segments -> query ranges of a_grid)"
+    else:
+        path = "2 launches per step: Euler RHS, interp1 inversion)"
+    return {"workload": f"{name} steps, Na={Na} Nz={N} Rouwenhorst, device tier (" + path,
             "solve": {"iters": iters, "wall_ms": solve_s * 1e3,
                       "us_per_iteration": solve_s / max(iters, 1) * 1e6,
                       "path": "host tier (aiy_egm_solve / aiy_labor_egm_solve): speculative "

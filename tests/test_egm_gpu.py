@@ -103,10 +103,11 @@ def test_egm_solve_nonmonotone_grid_is_reported(pkg, gpu):
                                   (2000, 16)])
 @pytest.mark.parametrize("labor", [False, True])
 def test_egm_fused_small_grid_equals_two_launches(pkg, gpu, Na, N, labor):
-    """Every step is ONE launch by default — egm_fused_kernel (a workgroup per productivity
-    state) for Na <= 1024, egm_scatter_kernel (segments → query ranges of the fixed a_grid) above;
-    variant bits 11 | 12 force the two-launch path.  Both, and the C restatement, agree bit for
-    bit over several steps (policy_c, policy_k, policy_l and the step's dist), N = 1 … 16."""
+    """The default step — egm_fused_kernel (one launch, a workgroup per productivity state) for
+    Na <= 1024, the two-launch step above — against variant bits 11 | 12 (the two-launch step
+    on small grids, the one-pass egm_scatter_kernel on large ones: segments → query ranges of
+    the fixed a_grid).  Both, and the C restatement, agree bit for bit over several steps
+    (policy_c, policy_k, policy_l and the step's dist), N = 1 … 16."""
     import torch
     dev = torch.device("cuda", 0)
     cal = no.calib_aiyagari(Na=Na, shocks="rouwenhorst", N=N) if N != 7 else \
@@ -148,8 +149,8 @@ def test_egm_fused_small_grid_equals_two_launches(pkg, gpu, Na, N, labor):
 
 
 def test_egm_nonmonotone_grid_is_reported_large_grid(pkg, gpu):
-    """Na > 1024: the one-pass scatter step (flag in the slots) reports a folding â like the
-    small-grid step; so does the two-launch step (flag word), forced by variant bit 12."""
+    """Na > 1024: the two-launch step (flag word) reports a folding â like the small-grid
+    step; so does the one-pass scatter step (flag in the slots), variant bit 12."""
     import torch
     a = np.linspace(0, 10, 5000)
     pc0 = np.tile(np.linspace(50, 0.01, 5000)[:, None], (1, 2))

@@ -149,5 +149,7 @@ def test_fused_howard_equals_two_launch_sweep(pkg, gpu):
         ref = torch.zeros_like(V)
         sh.slopes(Bv, ref)  # slopes of the final values, by the separate kernel
         torch.cuda.synchronize()
-        assert torch.equal(ref[:, own], dV[:, own]), nk
+        x, y = ref[:, own], dV[:, own]  # (NaN slopes at a degenerate first node: same places)
+        assert torch.equal(torch.isnan(x), torch.isnan(y)), nk
+        assert torch.equal(torch.nan_to_num(x, nan=0.0), torch.nan_to_num(y, nan=0.0)), nk
         sh.close()
