@@ -220,11 +220,21 @@ __global__ __launch_bounds__(256) void bell_ev_mfma_kernel(int N, int Na,
 }
 
 // ------------------------------------------------------------------------------ 1. table
+// EV(i,k) = Σ_m (β·P(i,m))·V(m,k) in m order (Aiyagari_VFI.m:79).  The V column is loaded 16
+// rows at a time, every load in flight before the ordered sum (a plain loop waits one L2 round
+// trip per row: N of them per thread); i is uniform, so P comes by scalar loads.
 __device__ __forceinline__ double table_ev(int N, int Na, const double* __restrict__ P,
                                            const double* __restrict__ V, double beta, int i,
                                            int k) {
     double acc = 0.0;
-    for (int m = 0; m < N; ++m) acc = acc + (beta * P[i * N + m]) * V[m * Na + k];
+    for (int m0 = 0; m0 < N; m0 += 16) {
+        double vv[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) vv[u] = m0 + u < N ? V[(size_t)(m0 + u) * Na + k] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+            if (m0 + u < N) acc = acc + (beta * P[i * N + m0 + u]) * vv[u];
+    }
     return acc;
 }
 __device__ __forceinline__ double table_D(double ev, int np) {
@@ -872,7 +882,7 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
     const int jbase = tile * (64 * R);
     __shared__ double2 s_cand[W][512];  // each wave's current superblock: (a_k, D_k)
     __shared__ unsigned long long s_pass[W];  // (first superblock, bit 12) per-wave pass masks
-    // W >= 2 (cooperating waves): registers are budgeted for 5 waves per SIMD, so the staging
+    // W >= 2 (cooperating waves): registers were budgeted for 5 waves per SIMD, so the staging
     // and fine-screen software pipelines (two register sets each) are off and the screen
     // stages four chains at a time; the best exchange reuses each wave's idle s_cand slice
     constexpr bool LEAN = W >= 2 || LAB;  // (labour: keeps 3 waves per SIMD)
@@ -1253,13 +1263,36 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
                     pass = all & (pat << bsel);
                 }
             }
+            if constexpr (LEAN) {
+                // no register set for all eight: the passing 64-blocks two at a time, both
+                // loads issued before either LDS write (a load and its write in one guarded
+                // block would cost one L2 round trip per block)
+                unsigned bm = 0;
 #pragma unroll
-            for (int b = 0; b < 8; ++b)  // all loads issued before any is used
-                if ((pass >> (8 * b)) & 0xffull) {
-                    const int k = min(sbase + (b << 6) + lane, Na - 1);
-                    if constexpr (LEAN) s_cand[wave][(b << 6) + lane] = make_double2(a[k], Drow[k]);
-                    else st[b] = make_double2(a[k], Drow[k]);
+                for (int b = 0; b < 8; ++b) bm |= ((pass >> (8 * b)) & 0xffull) ? 1u << b : 0u;
+                while (bm) {
+                    const int b0 = __builtin_ctz(bm);
+                    bm &= bm - 1;
+                    const int b1 = bm ? __builtin_ctz(bm) : -1;
+                    if (bm) bm &= bm - 1;
+                    const int k0 = min(sbase + (b0 << 6) + lane, Na - 1);
+                    const double2 v0 = make_double2(a[k0], Drow[k0]);
+                    double2 v1 = make_double2(0.0, 0.0);
+                    if (b1 >= 0) {
+                        const int k1 = min(sbase + (b1 << 6) + lane, Na - 1);
+                        v1 = make_double2(a[k1], Drow[k1]);
+                    }
+                    s_cand[wave][(b0 << 6) + lane] = v0;
+                    if (b1 >= 0) s_cand[wave][(b1 << 6) + lane] = v1;
                 }
+            } else {
+#pragma unroll
+                for (int b = 0; b < 8; ++b)  // all loads issued before any is used
+                    if ((pass >> (8 * b)) & 0xffull) {
+                        const int k = min(sbase + (b << 6) + lane, Na - 1);
+                        st[b] = make_double2(a[k], Drow[k]);
+                    }
+            }
             stamp(1);
             return pass;
         };
@@ -1470,7 +1503,10 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
 }
 
 template <int NP, bool LAB, int R, int LB, int W, bool INS>
-__global__ __launch_bounds__(64 * W, W >= 2 ? 5 : 3) void bell_tree_kernel(BellArgs A0, int ntile) {
+// min waves per SIMD 3 (168 VGPRs): every item of Na = 20,000 is resident at W = 1; the
+// cooperative tiles (W >= 2) serve small grids and labour, where a few hundred waves run and
+// latency, not occupancy, bounds them — a budget of 5 (and of 4) made those builds spill
+__global__ __launch_bounds__(64 * W, 3) void bell_tree_kernel(BellArgs A0, int ntile) {
     bell_tree_item<NP, LAB, R, LB, W, INS>(A0, ntile, (int)blockIdx.x, (int)gridDim.x);
 }
 

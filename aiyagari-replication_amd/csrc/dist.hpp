@@ -9,6 +9,9 @@ namespace aiy {
 // at most kDistChunk terms is the plain sequential sum; a long run (the borrowing constraint,
 // the top of the grid) has a dependent chain of ≈ L/G + G additions instead of L.
 constexpr int kDistChunk = 32;
+// a push wave stages its source range in LDS when it holds at most this many sources
+// (8 KB per wave on the on-grid path, 16 KB with lottery weights)
+constexpr int kDistStage = 1024;
 
 struct DistArgs {
     int N, Na;
@@ -25,6 +28,8 @@ struct DistArgs {
     double* mass;        // scratch [N][Na] (non-monotone fallback only)
     unsigned long long* diff;  // [2*kDiffSlots]
     unsigned* flags;     // bit 0 non-monotone policy, bit 1 index out of range
+    int stage;           // push: sources a wave stages in LDS (set by launch_dist_push)
+    long long* trace;    // (instrumentation, aiy_ws_set_timing bit 2) per-wave phase records
 };
 // the policy's plan (keys, lottery weights, run offsets, flags) — once per policy
 int launch_dist_prepare(const DistArgs& A, hipStream_t st);

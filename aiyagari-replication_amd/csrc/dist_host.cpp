@@ -54,6 +54,19 @@ static int dist_plan(aiy_ws* ws, const int* idx, const double* kp, const double*
     A->idx = idx; A->kp = kp; A->a = a; A->P = P;
     A->key = ws->d_key; A->off = ws->d_off; A->wr = ws->d_wr; A->mass = ws->d_mass;
     A->diff = ws->diff; A->flags = (unsigned*)ws->gi;
+    A->trace = nullptr;
+    if (ws->tracing) {  // (instrumentation) one record per push wave: ceil(Na/64)·N <= cap
+        const int64_t cap = (int64_t)ws->N * ((ws->Na + 15) / 16);
+        if (ws->trace_cap < cap) {
+            if (ws->trace) (void)hipFree(ws->trace);
+            ws->trace = nullptr;
+            ws->trace_cap = 0;
+            AIY_HIP(hipMalloc((void**)&ws->trace, 16 * (size_t)cap * sizeof(long long)));
+            ws->trace_cap = cap;
+        }
+        AIY_HIP(hipMemsetAsync(ws->trace, 0, 16 * (size_t)cap * sizeof(long long), st));
+        A->trace = ws->trace;
+    }
     AIY_HIP(hipMemsetAsync(ws->gi, 0, sizeof(int), st));
     AIY_TRY(launch_dist_prepare(*A, st));
     AIY_HIP(hipMemcpyAsync(&ws->hdiff[2 * kDiffSlots], ws->gi, sizeof(int), hipMemcpyDeviceToHost, st));

@@ -35,7 +35,8 @@ __device__ __forceinline__ double labor_dev(double c, double ws, double sigma, i
 // slots and flags (the interp kernel of the same step accumulates into them).
 __global__ __launch_bounds__(1024) void egm_rhs_kernel(EgmArgs A) {
     __shared__ double s_up[16][64];
-    const int lane = threadIdx.x & 63, m = threadIdx.x >> 6;  // blockDim = 64·N
+    const int lane = threadIdx.x & 63;
+    const int m = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // blockDim = 64·N
     const int N = A.N, Na = A.Na;
     const int a_i = blockIdx.x * 64 + lane;
     const bool ok = a_i < Na;
@@ -43,13 +44,18 @@ __global__ __launch_bounds__(1024) void egm_rhs_kernel(EgmArgs A) {
         for (int q = threadIdx.x; q < 2 * kDiffSlots; q += blockDim.x) A.diff[q] = 0ull;
         if (threadIdx.x == 0) *A.flags = 0u;
     }
+    const int j = m;
+    const double coef0 = A.beta * (1 + A.r);
+    double pj[16];  // row j of βP-ready weights, scalar loads issued before the barrier
+#pragma unroll
+    for (int q = 0; q < 16; ++q) pj[q] = q < N ? coef0 * A.P[j * N + q] : 0.0;
     s_up[m][lane] = ok ? uprime_dev(A.c[(size_t)m * Na + a_i], A.sigma, A.ns) : 0.0;
     __syncthreads();
     if (!ok) return;
-    const int j = m;
-    const double coef0 = A.beta * (1 + A.r);
     double acc = 0.0;
-    for (int q = 0; q < N; ++q) acc = acc + (coef0 * A.P[j * N + q]) * s_up[q][lane];
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+        if (q < N) acc = acc + pj[q] * s_up[q][lane];
     const double cn = aiy_pow(acc, -1.0 / A.sigma);  // :88
     const double ws = A.w * A.s[j];
     const double ag = A.a[a_i];
@@ -85,7 +91,7 @@ __device__ __forceinline__ int count_le(const double* __restrict__ x, int lo, in
 // the count — and everything after it — is the plain binary search's.
 __global__ __launch_bounds__(256) void egm_interp_kernel(EgmArgs A, int ntile) {
     __shared__ double s_x[4][256];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int Na = A.Na;
     const int wv = blockIdx.x * 4 + wave;
     bool ok = false;
@@ -197,9 +203,13 @@ __global__ __launch_bounds__(1024) void egm_fused_kernel(EgmArgs A) {
     const double coef0 = A.beta * (1 + A.r);
     const double ws = A.w * A.s[j];
     for (int a_i = threadIdx.x; a_i < Na; a_i += blockDim.x) {  // :80-92 (labour :80-87)
+        double cq[16];  // every c_q(a) load in flight before the ordered Euler sum
+#pragma unroll
+        for (int q = 0; q < 16; ++q) cq[q] = q < N ? A.c[(size_t)q * Na + a_i] : 1.0;
         double acc = 0.0;
-        for (int q = 0; q < N; ++q)
-            acc = acc + (coef0 * A.P[j * N + q]) * uprime_dev(A.c[(size_t)q * Na + a_i], A.sigma, A.ns);
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            if (q < N) acc = acc + (coef0 * A.P[j * N + q]) * uprime_dev(cq[q], A.sigma, A.ns);
         const double cn = aiy_pow(acc, -1.0 / A.sigma);
         const double ag = A.a[a_i];
         double ah;
@@ -298,7 +308,8 @@ __global__ __launch_bounds__(1024) void egm_fused_kernel(EgmArgs A) {
 __global__ __launch_bounds__(1024) void egm_scatter_kernel(EgmArgs A) {
     __shared__ double s_up[16][64];
     __shared__ double s_a[16][256];
-    const int lane = threadIdx.x & 63, m = threadIdx.x >> 6;  // blockDim = 64·N
+    const int lane = threadIdx.x & 63;
+    const int m = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // blockDim = 64·N
     const int N = A.N, Na = A.Na;
     const int k = blockIdx.x * 63 + lane;
     const bool okk = k < Na;

@@ -139,3 +139,24 @@ def test_stationary_dev_speculative_batches(pkg, gpu, tol, max_iter):
     assert it == ito and dist == disto
     assert np.array_equal(out.cpu().numpy(), lo)
     assert abs(float(K[0]) - Ko) <= 1e-12 * abs(Ko)
+
+
+@pytest.mark.parametrize("N,Na", [(16, 3000), (1, 70), (5, 1025)])
+def test_staged_push_shapes_bitwise(pkg, gpu, N, Na):
+    """The push stages each wave's source range in LDS (kDistStage within a 64 KB budget: 512
+    sources per wave on the on-grid path at N = 16, 256 with lottery weights); random monotone
+    policies with runs from 0 to a few hundred sources, N = 1 … 16, ragged last tiles — on-grid
+    and lottery pushes bit-exact against the C restatement."""
+    rng = np.random.default_rng(N * 1000 + Na)
+    a = np.linspace(0.0, 30.0, Na) ** 2 / 30.0
+    P = rng.random((N, N)); P /= P.sum(1, keepdims=True)
+    steps = rng.choice([0, 1, 1, 1, 2, 0, 0], size=(N, Na))
+    idx = np.minimum(np.cumsum(steps, 1), Na - 1).astype(np.int64)
+    lam0 = rng.random((N, Na)); lam0 /= lam0.sum()
+    lam, _, _, _ = pkg.dist_stationary(a, P, policy_idx=idx + 1, lam0=lam0, tol=0.0, max_iter=3)
+    lo, _, _, _ = corc.dist_stationary(lam0, a, P, idx=idx, tol=0.0, max_iter=3)
+    assert np.array_equal(lam, lo)
+    kp = np.sort(rng.uniform(-1.0, a[-1] * 0.8, (N, Na)), 1)
+    lam, _, _, _ = pkg.dist_stationary(a, P, policy_k=kp, lam0=lam0, tol=0.0, max_iter=2)
+    lo, _, _, _ = corc.dist_stationary(lam0, a, P, kp=kp, tol=0.0, max_iter=2)
+    assert np.array_equal(lam, lo)
