@@ -5,11 +5,12 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/pmc}
 ARGS=${BENCH_ARGS:---no-cpu-baseline --no-ge --steps 3 --warmup 2}
+CMD=${PMC_CMD:-$PWD/bench.py}  # the program each pass profiles (bench.py $ARGS by default)
 mkdir -p "$OUT"
 pass() {  # name, counters...
   local name=$1; shift
   echo "=== pmc $name: $*"
-  timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv -d "$PWD/$OUT/$name" -o run -- python3 "$PWD/bench.py" $ARGS > "$OUT/$name.log" 2>&1
+  timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv -d "$PWD/$OUT/$name" -o run -- python3 $CMD $ARGS > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "=== pmc $name rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 "$OUT/$name.log"; exit $rc; fi
