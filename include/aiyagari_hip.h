@@ -262,7 +262,8 @@ int aiy_ws_set_persistent(aiy_ws* ws, int persistent);
  * 1, 2, 4 or 8, bit 9 = no extrapolated (hint + last shift) start, bit 6 = 4 lanes per state,
  * bit 10 = the plain exhaustive scan, bit 12 = cooperating waves deal the first superblock's
  * passing 8-blocks round-robin (else by 64-block).  EGM steps on this workspace: bit 11 = two
- * launches per step even when Na <= 1024 (default there: one fused launch).  Bit 13 = tiles in
+ * launches per step even when Na <= 1024 (default there: one fused launch); bit 12 = the one-pass
+ * scatter step when Na > 1024 (default there: two launches).  Bit 13 = tiles in
  * descending asset order (one wave per tile).  Results are identical for every value in
  * [-1, 16383].
  * -1 (default): chosen by size — Na <= 4096: 2 cooperating waves per tile (A1), 4 with bit 12
