@@ -254,10 +254,19 @@ __global__ __launch_bounds__(kTableBlock) void bell_table_kernel(
     float* __restrict__ T32, int CK, double* __restrict__ Dm, double* __restrict__ Dm8,
     double* __restrict__ Dm512, int nb, int nb8, int nb512,
     unsigned long long* __restrict__ diff, double* __restrict__ Dt,
-    unsigned long long* __restrict__ fold, bool ev_in) {
+    unsigned long long* __restrict__ fold, bool ev_in, bool xcd) {
     __shared__ double s_max[kTableBlock / 64];
-    const int i = blockIdx.y;
-    const int k = blockIdx.x * kTableBlock + threadIdx.x;
+    // xcd: the (chunk, row) of this block is dealt like the tree kernel's items (xcd_remap over
+    // the row-major order), so the XCD that writes a row's table chunk is the one whose tree
+    // tiles read it first (the hint window, the climb, the 8-block bounds near the optimum):
+    // those first touches hit that XCD's L2 instead of the MALL.  Work order only.
+    int i = blockIdx.y, cx = blockIdx.x;
+    if (xcd) {
+        const int p = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+        i = p / gridDim.x;
+        cx = p - i * gridDim.x;
+    }
+    const int k = cx * kTableBlock + threadIdx.x;
     if (diff && blockIdx.x == 0 && blockIdx.y == 0) {  // block-uniform branch
         if (fold && threadIdx.x < 64) {  // same fold as reduce_slots_kernel
             const int l = threadIdx.x;
@@ -324,7 +333,7 @@ __global__ __launch_bounds__(kTableBlock) void bell_table_kernel(
         if (threadIdx.x == 0) {
             double m = s_max[0];
             for (int q = 1; q < kTableBlock / 64; ++q) m = fmax(m, s_max[q]);
-            Dm512[(size_t)i * nb512 + blockIdx.x] = m;
+            Dm512[(size_t)i * nb512 + cx] = m;
         }
     }
 }
@@ -341,10 +350,16 @@ __global__ __launch_bounds__(kTableBlock) void bell_table_batch_kernel(
     int np, const double* __restrict__ a, double* __restrict__ EV, double* __restrict__ Dt,
     double* __restrict__ Dm8, double* __restrict__ Dm512, int nb8, int nb512,
     unsigned long long* __restrict__ slots, int* __restrict__ stop, int sweep, double tol,
-    bool ev_in) {
+    bool ev_in, bool xcd) {
     __shared__ double s_max[kTableBlock / 64];
     __shared__ int s_stop;
-    const int c = blockIdx.y / N, i = blockIdx.y - c * N;
+    int cy = blockIdx.y, cx = blockIdx.x;  // (xcd: dealt as the tree's items, bell_table_kernel)
+    if (xcd) {
+        const int p = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+        cy = p / gridDim.x;
+        cx = p - cy * gridDim.x;
+    }
+    const int c = cy / N, i = cy - c * N;
     if (stop[c]) return;  // block-uniform
     if (sweep > 1) {
         if (threadIdx.x < 64) {
@@ -360,14 +375,14 @@ __global__ __launch_bounds__(kTableBlock) void bell_table_batch_kernel(
         }
         __syncthreads();
         if (s_stop) {
-            if (blockIdx.x == 0 && i == 0 && threadIdx.x == 0) stop[c] = sweep - 1;
+            if (cx == 0 && i == 0 && threadIdx.x == 0) stop[c] = sweep - 1;
             return;
         }
     }
-    if (blockIdx.x == 0 && i == 0 && threadIdx.x < 2 * kDiffSlots)
+    if (cx == 0 && i == 0 && threadIdx.x < 2 * kDiffSlots)
         slots[((size_t)c * 2 + (sweep & 1)) * 2 * kDiffSlots + threadIdx.x] = 0ull;
     const size_t o = (size_t)c * N * Na;
-    const int k = blockIdx.x * kTableBlock + threadIdx.x;
+    const int k = cx * kTableBlock + threadIdx.x;
     const bool ok = k < Na;
     double D = -__builtin_inf();
     if (ok) {
@@ -401,7 +416,7 @@ __global__ __launch_bounds__(kTableBlock) void bell_table_batch_kernel(
     if (threadIdx.x == 0) {
         double m = s_max[0];
         for (int q = 1; q < kTableBlock / 64; ++q) m = fmax(m, s_max[q]);
-        Dm512[rb512 + blockIdx.x] = m;
+        Dm512[rb512 + cx] = m;
     }
 }
 
@@ -410,7 +425,7 @@ int launch_bell_table_batch(const BellArgs& A, unsigned long long* slots, int sw
     dim3 grid((A.Na + kTableBlock - 1) / kTableBlock, A.C * A.N);
     bell_table_batch_kernel<<<grid, kTableBlock, 0, st>>>(
         A.N, A.Na, A.P, A.v_old, A.beta, A.np, A.a, A.EV, A.Dt, A.Dm8, A.Dm512, A.nb8, A.nb512,
-        slots, const_cast<int*>(A.stop), sweep, tol, A.ev_mfma);
+        slots, const_cast<int*>(A.stop), sweep, tol, A.ev_mfma, (A.variant & 16) != 0);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }
@@ -2097,7 +2112,7 @@ int launch_bell_table(const BellArgs& A, hipStream_t st) {
         A.N, A.Na, A.P, A.v_old, A.beta, A.np, A.a, A.EV, (scr && !A.tree) ? A.T : nullptr,
         scr ? A.T32 : nullptr, A.CK, scr ? A.Dm : nullptr, scr ? A.Dm8 : nullptr,
         scr ? A.Dm512 : nullptr, A.nb, A.nb8, A.nb512, A.diff, scr ? A.Dt : nullptr, A.fold,
-        A.ev_mfma);
+        A.ev_mfma, (A.variant & 16) != 0);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }
