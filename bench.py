@@ -5,12 +5,14 @@ Aiyagari VFI, Na = 20,000, Nz = 7 Rouwenhorst, one exhaustive Bellman sweep per 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
-Multi-GPU: the general-equilibrium loop's candidate interest rates are independent units
-(SURVEY §8(e) E2), so each rank solves its own r (weak scaling, no collective on the data
-path); the timing is max over ranks.  Rank 0 prints one JSON line.  The line also carries
-`ks_sharded` (BASELINE configs[4]): one VFI iteration of the Krusell-Smith solve at k = 32,768,
-K = 64 sharded over the same N ranks (strong scaling, halo exchange per Howard sweep), so the
-driver's N = 1, 2, 4, 8 runs give its speed-up directly.
+Multi-GPU: the Aiyagari sweep does not shard (replicas only), so every rank
+runs the same sweeps (weak scaling, no collective on the data path; --distinct-r gives each
+rank its own GE candidate r instead); the timing is max over ranks.  Rank 0 prints one JSON
+line.  The line also carries `ks_sharded` (BASELINE configs[4]): one VFI iteration of the
+Krusell-Smith solve at k = 32,768, K = 64 sharded over the same N ranks ((K, Z) slices, one
+ghost-rectangle exchange per block of 4 Howard sweeps on > 1 rank; strong scaling), and
+`ge_batch` (configs[3]: multisection GE, candidates round-robin over the ranks, one all-gather
+per round), so the driver's N = 1, 2, 4, 8 runs give their speed-ups directly.
 """
 from __future__ import annotations
 
@@ -299,11 +301,13 @@ def main():
         # result is bit-identical to -- the rate an exhaustive kernel would need to match it
         effective = FLOPS_PER_CANDIDATE * evals_per_sweep / (kern_avg_ms * 1e-3) / 1e12
         traffic = None
-        tf = _json_profile("r02b_traffic_vfi_tree.json") or _json_profile("traffic_vfi_tree.json")
+        # PMC / HBM-traffic passes over the same sweeps 6..25 on the current kernels
+        # (tools/exp/exp_r03_s3s.sh: tools/pmc.sh + pmc_summary / pmc_traffic, skip 5 take 20)
+        tf_name, pmc_name = "r03_traffic_vfi_tree.json", "r03_pmc_tree.json"
+        tf = _json_profile(tf_name)
         if tf:
             traffic = tf.get("bytes_per_launch")
-        pmc = (_json_profile("r02b_pmc_tree_final.json") or _json_profile("r02_pmc_tree_final.json")
-               or _json_profile("r02_pmc_tree_climb.json"))
+        pmc = _json_profile(pmc_name)
         step_ms = sorted(blocks)
         out = {
             "metric": "Bellman evals/sec (Na·Na'·Nz, fp64)",
@@ -354,8 +358,9 @@ def main():
                                             f"{evals_per_sweep} candidates per launch, the exhaustive "
                                             f"scan this kernel reproduces bit for bit",
                          "pmc": (pmc or {}).get("derived"),
-                         "pmc_source": "profiles/r02b_pmc_tree_final.json (rocprofv3 --pmc, "
-                                       "tools/pmc.sh + tools/pmc_summary.py, same sweeps)"},
+                         "pmc_source": f"profiles/{pmc_name}, profiles/{tf_name} (rocprofv3 "
+                                       f"--pmc, tools/pmc.sh + tools/pmc_summary.py / "
+                                       f"pmc_traffic.py, same sweeps 6..25)"},
         }
         out.update(legs)
         if exh is not None:  # the plain exhaustive scan's own roofline (mode 2)
@@ -375,6 +380,15 @@ def main():
         if world == 1 and not args.no_extra:
             out["batch_config4_share"] = BL.batch_leg(pkg, dev)
             out["dist"] = BL.dist_leg(pkg, dev)
+            # counter passes of these kernels (tools/pmc_workloads.py under tools/pmc.sh)
+            pm = lambda n: ((_json_profile(f"r03_pmc_{n}.json") or {}).get("derived"))
+            tr = lambda n: ((_json_profile(f"r03_traffic_{n}.json") or {}).get("bytes_per_launch"))
+            out["batch_config4_share"]["roofline"].update(
+                pmc=pm("batch"), traffic=tr("batch"),
+                pmc_source="profiles/r03_pmc_batch.json, r03_traffic_batch.json")
+            out["dist"]["roofline"].update(
+                pmc=pm("dist_push"), traffic=tr("dist_push"),
+                pmc_source="profiles/r03_pmc_dist_push.json, r03_traffic_dist_push.json")
             out["labor_vfi"] = {"Na400": BL.labor_leg(pkg, dev, 400, cpu_threads=threads,
                                                       cpu=not args.no_cpu_baseline),
                                 "Na20000": BL.labor_leg(pkg, dev, 20000, steps=5, reps=3, cpu=False)}
@@ -382,6 +396,12 @@ def main():
                           "Na400": BL.egm_leg(pkg, dev, 400, cpu_threads=threads)}
             out["labor_egm"] = {"Na20000": BL.egm_leg(pkg, dev, 20000, labor=True,
                                                       cpu_threads=threads)}
+            out["labor_vfi"]["Na400"]["roofline"]["pmc"] = pm("labor_na400")
+            out["labor_vfi"]["Na20000"]["roofline"]["pmc"] = pm("labor_na20000")
+            out["egm"]["Na20000"]["roofline"].update(
+                pmc={"egm_rhs_kernel": pm("egm_rhs"), "egm_interp_kernel": pm("egm_interp")},
+                traffic=(tr("egm_rhs") or 0) + (tr("egm_interp") or 0) or None,
+                pmc_source="profiles/r03_pmc_egm_{rhs,interp}.json, r03_traffic_egm_*.json")
         if not args.no_panel and world == 1:   # F3/F2: KS shock panel + agent simulation
             import bench_panel
             out["ks_panel"] = bench_panel.panel_leg(pkg, dev)
