@@ -8,7 +8,8 @@ library or a device raises.
 """
 from . import calibration
 from .dist import dist_stationary, dist_stationary_dev, dist_update_dev
-from .egm import egm_solve, egm_step, egm_step_dev, labor_egm_solve, labor_egm_step
+from .egm import (egm_solve, egm_solve_dev, egm_step, egm_step_dev, labor_egm_solve,
+                  labor_egm_step)
 from ._capi import AiyError, LIB_PATH, declared_symbols, lib
 from . import ge
 from . import ge_batch
@@ -20,6 +21,6 @@ from .sim import sim_capital, sim_capital_dev
 from . import vfi
 from .vfi import Workspace, labor_vfi_solve, labor_vfi_sweep, solve_batch_dev, vfi_solve, vfi_sweep
 
-__all__ = ["ge", "ge_batch", "ks_dist", "ks_panel", "stats", "ks_egm_solve", "ks_howard", "ks_params", "ks_policy_improve", "ks_vfi_solve", "dist_stationary", "dist_stationary_dev", "dist_update_dev", "egm_solve", "egm_step", "egm_step_dev", "labor_egm_solve", "labor_egm_step",
+__all__ = ["ge", "ge_batch", "ks_dist", "ks_panel", "stats", "ks_egm_solve", "ks_howard", "ks_params", "ks_policy_improve", "ks_vfi_solve", "dist_stationary", "dist_stationary_dev", "dist_update_dev", "egm_solve", "egm_solve_dev", "egm_step", "egm_step_dev", "labor_egm_solve", "labor_egm_step",
            "AiyError", "LIB_PATH", "Workspace", "calibration", "declared_symbols", "lib",
            "labor_vfi_solve", "sim_capital", "sim_capital_dev", "labor_vfi_sweep", "vfi_solve", "vfi_sweep"]

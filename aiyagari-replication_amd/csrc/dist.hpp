@@ -29,6 +29,8 @@ struct DistArgs {
     unsigned long long* diff;  // [2*kDiffSlots]
     unsigned* flags;     // bit 0 non-monotone policy, bit 1 index out of range
     int stage;           // push: sources a wave stages in LDS (set by launch_dist_push)
+    unsigned long long* diff_clear;  // push (monotone plan): the next push's slot set, zeroed
+                                     // by the first workgroup (nullable)
     long long* trace;    // (instrumentation, aiy_ws_set_timing bit 2) per-wave phase records
 };
 // the policy's plan (keys, lottery weights, run offsets, flags) — once per policy

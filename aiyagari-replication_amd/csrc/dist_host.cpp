@@ -5,9 +5,9 @@
 // The policy is fixed across the fixed-point iteration, so its plan (keys, lottery weights,
 // run offsets, the monotonicity flag) is built ONCE per call and read back once; every push is
 // then one launch (dist_push_kernel).  The iteration runs in speculative batches as the VFI
-// and EGM solves do: m pushes are enqueued between reads — push g reads ring slot (g−1) mod R
-// and writes slot g mod R, its max|Δλ| lands in its own slot set — and one D2H read per batch
-// finds the first push with max|Δλ| < tol.  Pushes are deterministic, so the iteration count,
+// and EGM solves do: m pushes are enqueued per batch — push g reads ring slot (g−1) mod R
+// and writes slot g mod R, its max|Δλ| lands in its own slot set — and the host reads one
+// batch's slot sets while the next batch runs, to find the first push with max|Δλ| < tol.  Pushes are deterministic, so the iteration count,
 // the returned λ and dist are exactly the one-read-per-push loop's.
 #include <hip/hip_runtime.h>
 
@@ -24,7 +24,7 @@
 
 namespace aiy {
 
-constexpr int kDistSpecMax = 32;  // pushes per convergence read
+constexpr int kDistSpecMax = 32;  // pushes per batch (two batches in flight)
 
 static int ensure_dist(aiy_ws* ws) {
     const size_t n = (size_t)ws->N * ws->Na;
@@ -102,7 +102,10 @@ int dist_update_dev(aiy_ws* ws, const double* lam, const int* idx, const double*
 }
 
 // the fixed-point loop of aiy_dist_stationary on device:  for it = 1..max_iter: push; stop
-// when max|Δλ| < tol.  lam_out receives the last push; k_dev (nullable) = Σ λ·a.
+// when max|Δλ| < tol.  lam_out receives the last push; k_dev (nullable) = Σ λ·a.  Batches of
+// pushes with one D2H copy of their diff slots and an event each; two batches in flight (the
+// host reads batch k while batch k+1 runs), a ring of 2M + 1 λ buffers so that the stopping
+// push's λ survives the next batch.
 int dist_stationary_dev(aiy_ws* ws, const double* lam0, const int* idx, const double* kp,
                         const double* a, const double* P, double tol, int64_t max_iter,
                         double* lam_out, double* k_dev, int64_t* iters, double* dist,
@@ -112,58 +115,88 @@ int dist_stationary_dev(aiy_ws* ws, const double* lam0, const int* idx, const do
     DistArgs A0;
     bool fb = false;
     AIY_TRY(dist_plan(ws, idx, kp, a, P, &A0, &fb, st));
-    const int M = kDistSpecMax, R = M + 1;
+    const int M = kDistSpecMax, R = 2 * M + 1;
     const size_t n = (size_t)ws->N * ws->Na, nb = n * sizeof(double);
     const int SW = 2 * kDiffSlots;
+    const size_t SB = (size_t)R * SW * sizeof(unsigned long long);
     if (ws->dist_n != n || ws->dist_m != M) {
         ws->free_dist_spec();
         AIY_HIP(hipMalloc((void**)&ws->dist_ring, (size_t)R * nb));
-        AIY_HIP(hipMalloc((void**)&ws->dist_slots, (size_t)M * SW * sizeof(unsigned long long)));
-        AIY_HIP(hipHostMalloc((void**)&ws->dist_hslots, (size_t)M * SW * sizeof(unsigned long long)));
+        AIY_HIP(hipMalloc((void**)&ws->dist_slots, SB));
+        AIY_HIP(hipHostMalloc((void**)&ws->dist_hslots, 2 * SB));
+        for (int b = 0; b < 2; ++b)
+            AIY_HIP(hipEventCreateWithFlags(&ws->dist_ev[b], hipEventDisableTiming));
         ws->dist_n = n;
         ws->dist_m = M;
     }
     auto slot = [&](int64_t g) { return ws->dist_ring + (size_t)(g % R) * n; };
+    auto sset = [&](int64_t g) { return ws->dist_slots + (size_t)(g % R) * SW; };
     AIY_HIP(hipMemcpyAsync(slot(0), lam0, nb, hipMemcpyDeviceToDevice, st));
-    int64_t done = 0, stop = 0;
+    AIY_HIP(hipMemsetAsync(sset(1), 0, SW * sizeof(unsigned long long), st));
+    struct Batch {
+        int64_t s0, m;  // pushes s0 + 1 .. s0 + m
+        int hb;
+    };
+    Batch q[2];
+    int nq = 0, hb_next = 0;
+    int64_t enq = 0, stop = 0;
     double d_prev = NAN, d_last = NAN, d_stop = NAN;
-    while (!stop && done < max_iter) {
+    auto enqueue = [&]() -> int {
         int64_t m = M;
         if (d_last == d_last && d_prev == d_prev && d_last < d_prev && d_last > 0 && tol > 0) {
             const double need = std::ceil(std::log(tol / d_last) / std::log(d_last / d_prev));
-            if (need >= 1 && need < (double)m) m = (int64_t)need;
+            int64_t ahead = 0;  // pushes in flight, not yet read
+            for (int b = 0; b < nq; ++b) ahead += q[b].m;
+            if (need >= 1 && need - (double)ahead < (double)m)
+                m = (int64_t)std::max(1.0, need - (double)ahead);
         }
-        m = std::min<int64_t>(std::max<int64_t>(m, 1), max_iter - done);
-        AIY_HIP(hipMemsetAsync(ws->dist_slots, 0, (size_t)m * SW * sizeof(unsigned long long), st));
+        m = std::min<int64_t>(std::max<int64_t>(m, 1), max_iter - enq);
         for (int64_t t = 0; t < m; ++t) {
+            const int64_t g = enq + 1 + t;
             DistArgs A = A0;
-            A.lam = slot(done + t);
-            A.out = slot(done + t + 1);
-            A.diff = ws->dist_slots + (size_t)t * SW;
+            A.lam = slot(g - 1);
+            A.out = slot(g);
+            A.diff = sset(g);
+            // push g's set was zeroed by push g−1 (monotone plan) or is zeroed here
+            if (fb) AIY_HIP(hipMemsetAsync(sset(g), 0, SW * sizeof(unsigned long long), st));
+            else A.diff_clear = sset(g + 1);
             AIY_TRY(ws_timing_begin(ws, st));
             AIY_TRY(launch_dist_push(A, fb, st));
             AIY_TRY(ws_timing_end(ws, st));
         }
-        AIY_HIP(hipMemcpyAsync(ws->dist_hslots, ws->dist_slots,
-                               (size_t)m * SW * sizeof(unsigned long long),
-                               hipMemcpyDeviceToHost, st));
-        AIY_HIP(hipStreamSynchronize(st));
-        for (int64_t t = 0; t < m; ++t) {
-            const double d = fold_slots_host(ws->dist_hslots + (size_t)t * SW);
+        unsigned long long* h = ws->dist_hslots + (size_t)hb_next * R * SW;
+        AIY_HIP(hipMemcpyAsync(h, ws->dist_slots, SB, hipMemcpyDeviceToHost, st));
+        AIY_HIP(hipEventRecord(ws->dist_ev[hb_next], st));
+        q[nq++] = Batch{enq, m, hb_next};
+        hb_next ^= 1;
+        enq += m;
+        return AIY_OK;
+    };
+    AIY_TRY(enqueue());
+    while (nq > 0) {
+        if (nq < 2 && enq < max_iter) AIY_TRY(enqueue());  // keep the device busy while reading
+        const Batch b = q[0];
+        AIY_HIP(hipEventSynchronize(ws->dist_ev[b.hb]));
+        const unsigned long long* hs = ws->dist_hslots + (size_t)b.hb * R * SW;
+        for (int64_t t = 0; t < b.m; ++t) {
+            const double d = fold_slots_host(hs + (size_t)((b.s0 + 1 + t) % R) * SW);
             d_prev = d_last;
             d_last = d;
             d_stop = d;
             if (d < tol) {
-                stop = done + 1 + t;
+                stop = b.s0 + 1 + t;
                 break;
             }
         }
-        if (!stop) done += m;
+        q[0] = q[1];
+        --nq;
+        if (stop) break;
     }
-    const int64_t g = stop ? stop : done;
+    const int64_t g = stop ? stop : enq;
     AIY_HIP(hipMemcpyAsync(lam_out, slot(g), nb, hipMemcpyDeviceToDevice, st));
     if (k_dev)
         AIY_TRY(launch_dist_capital(lam_out, a, (int)ws->N, (int)ws->Na, ws->d_part, k_dev, st));
+    AIY_HIP(hipStreamSynchronize(st));  // (a speculative batch may still be running)
     *iters = g;
     *dist = d_stop;
     return AIY_OK;

@@ -194,6 +194,8 @@ __global__ __launch_bounds__(1024) void dist_push_kernel(DistArgs A) {
     long long cy[6] = {0, 0, 0, 0, 0, 0};
     const long long t_in = A.trace ? (long long)wall_clock64() : 0;
     if (A.trace) cy[0] = (long long)__builtin_amdgcn_s_memtime();
+    if (blockIdx.x == 0 && A.diff_clear)  // the next push's slots (a different set)
+        for (int q = threadIdx.x; q < 2 * kDiffSlots; q += blockDim.x) A.diff_clear[q] = 0ull;
     const int* __restrict__ off = A.off + (size_t)i * (Na + 1);
     const double* __restrict__ lam = A.lam + (size_t)i * Na;
     const double* __restrict__ wr = LOT ? A.wr + (size_t)i * Na : nullptr;

@@ -26,10 +26,20 @@ struct EgmArgs {
     bool onepass;              // Na > 1024: one launch per step (egm_scatter_kernel); `diff`
                                // must be zero at launch (the previous step cleared it, see
                                // diff_clear), the flag rides in bit 1 of the slots' second words
-    unsigned long long* diff_clear;  // onepass: the next step's slot set (kEgmSlotWords words),
-                                     // zeroed by this launch's first workgroup (nullable)
+    unsigned long long* diff_clear;  // onepass / chain: the next step's slot set (kEgmSlotWords
+                                     // words), zeroed by this launch's first workgroup (nullable)
+    double* ahat_next;               // chain: step t+1's â and c̃ (the other scratch pair)
+    double* cnext_next;
+    int* seg;                        // [N][Na] interp1 segment of each query at the last step
+                                     // (a verified hint for the next; -1 = none)
+    long long* trace;                // (instrumentation, aiy_ws_set_timing bit 2) per-wave
+                                     // phase records of the interp / chain kernels
 };
 constexpr int kEgmSlotWords = 2 * kDiffSlots + 2;  // {max bits, any} x kDiffSlots + flag word
 constexpr int kEgmFusedMaxNa = 1024;  // egm_fused_kernel: one state per thread
 int launch_egm_step(const EgmArgs& A, hipStream_t st);
+// the chained solve (Na > 1,024): the Euler RHS of the first step, then one launch per step
+// (interp1 of step t + the RHS of step t+1 on the same tiles)
+int launch_egm_rhs(const EgmArgs& A, hipStream_t st);
+int launch_egm_chain(const EgmArgs& A, hipStream_t st);
 }  // namespace aiy

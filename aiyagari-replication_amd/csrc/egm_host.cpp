@@ -37,6 +37,21 @@ static int ensure_egm(aiy_ws* ws) {
         AIY_HIP(hipMalloc((void**)&ws->diff, 2 * kDiffSlots * sizeof(unsigned long long)));
     if (!ws->hdiff)
         AIY_HIP(hipHostMalloc((void**)&ws->hdiff, (2 * kDiffSlots + 4) * sizeof(unsigned long long)));
+    if (ws->tracing) {  // (instrumentation) one record per interp / chain wave: N·ntile
+        const int64_t cap = (int64_t)ws->N * ((ws->Na + 15) / 16);
+        if (ws->trace_cap < cap) {
+            if (ws->trace) (void)hipFree(ws->trace);
+            ws->trace = nullptr;
+            ws->trace_cap = 0;
+            AIY_HIP(hipMalloc((void**)&ws->trace, 16 * (size_t)cap * sizeof(long long)));
+            AIY_HIP(hipMemset(ws->trace, 0, 16 * (size_t)cap * sizeof(long long)));
+            ws->trace_cap = cap;
+        }
+    }
+    if (!ws->egm_seg) {
+        AIY_HIP(hipMalloc((void**)&ws->egm_seg, n * sizeof(int)));
+        AIY_HIP(hipMemset(ws->egm_seg, 0xff, n * sizeof(int)));  // -1: no hint yet
+    }
     if (!ws->egm_d2) {
         AIY_HIP(hipMalloc((void**)&ws->egm_d2, 2 * kEgmSlotWords * sizeof(unsigned long long)));
         AIY_HIP(hipMemset(ws->egm_d2, 0, 2 * kEgmSlotWords * sizeof(unsigned long long)));
@@ -60,6 +75,9 @@ static EgmArgs egm_args(aiy_ws* ws, const double* c, const double* a, const doub
     A.ahat = ws->g0; A.cnext = ws->g1; A.cout = cout; A.pk = pk; A.pl = pl;
     A.diff = ws->diff;
     A.flags = (unsigned*)ws->gi;
+    A.trace = ws->tracing ? ws->trace : nullptr;  // (instrumentation; see ensure_egm)
+    // interp1 segment hints (verified in the kernel; variant bit 14 turns them off, A/B only)
+    A.seg = (ws->variant >= 0 && (ws->variant & 16384)) ? nullptr : ws->egm_seg;
     // small grids: one launch per step (egm_fused_kernel) unless the tuning variant sets bit 11;
     // large grids: the two-launch step, or the one-pass egm_scatter_kernel with variant bit 12
     // (opt-in: a segment owns its queries, and where â_j falls into the dense low end of the
@@ -113,17 +131,19 @@ static int read_egm(aiy_ws* ws, hipStream_t st, double* d) {
 }
 
 // The solve loop (Aiyagari_EGM.m:74-108, labour :67-105) with speculative batches, as the VFI
-// solve (capi.cpp, bell_solve_spec): steps are deterministic, so m steps are enqueued between
-// reads — step g reads ring slot (g−1) mod R and writes slot g mod R, its dist lands in slot
-// set g mod R with its flag word (the one-pass step zeroes set (g+1) mod R for the next step;
-// the sets are zeroed once per solve) — and one D2H read per batch finds the first step whose
-// dist is not above tol.  The ring keeps that step's policy_c; its policy_k (and policy_l) were
-// overwritten by later speculative steps, so the stopping step is re-run from its input
+// solve (capi.cpp, bell_solve_spec): steps are deterministic, so batches of m steps are
+// enqueued between reads — step g reads ring slot (g−1) mod R and writes slot g mod R, its
+// dist lands in slot set g mod R with its flag word (a one-pass or chained step zeroes set
+// (g+1) mod R for the next step; the sets are zeroed once per solve) — and each batch ends with
+// one D2H copy of the slot sets and an event.  Two batches are in flight: the host reads batch
+// k's dists while batch k+1 runs, so the device never idles at a read; with R = 2M + 1 slots
+// the stopping step's policy_c survives the next batch's writes.  Its policy_k (and policy_l)
+// were overwritten by later speculative steps, so the stopping step is re-run from its input
 // (identical values).  Iteration count, dist and outputs equal the one-read-per-step loop's.
 static int egm_solve_spec(aiy_ws* ws, const EgmArgs& A0, double* c0, double tol,
                           int64_t max_iter, double** cur_out, double* dist, int64_t* iters,
                           hipStream_t st) {
-    const int M = ws->spec_max, R = M + 1;
+    const int M = ws->spec_max, R = 2 * M + 1;
     const size_t n = (size_t)ws->N * ws->Na, nb = n * sizeof(double);
     const int SW = kEgmSlotWords;  // per step: {max bits, any} slots, then the flag word
     const size_t SB = (size_t)R * SW * sizeof(unsigned long long);
@@ -131,7 +151,9 @@ static int egm_solve_spec(aiy_ws* ws, const EgmArgs& A0, double* c0, double tol,
         ws->free_egm_spec();
         AIY_HIP(hipMalloc((void**)&ws->egm_ring, (size_t)R * nb));
         AIY_HIP(hipMalloc((void**)&ws->egm_slots, SB));
-        AIY_HIP(hipHostMalloc((void**)&ws->egm_hslots, SB));
+        AIY_HIP(hipHostMalloc((void**)&ws->egm_hslots, 2 * SB));
+        for (int b = 0; b < 2; ++b)
+            AIY_HIP(hipEventCreateWithFlags(&ws->egm_ev[b], hipEventDisableTiming));
         ws->egm_spec_n = n;
         ws->egm_spec_m = M;
     }
@@ -139,6 +161,16 @@ static int egm_solve_spec(aiy_ws* ws, const EgmArgs& A0, double* c0, double tol,
     auto sset = [&](int64_t g) { return ws->egm_slots + (size_t)(g % R) * SW; };
     AIY_HIP(hipMemcpyAsync(slot(0), c0, nb, hipMemcpyDeviceToDevice, st));
     if (A0.onepass) AIY_HIP(hipMemsetAsync(ws->egm_slots, 0, SB, st));
+    // chained steps (the default for Na > 1,024): the RHS of step 1 here, then one launch per
+    // step — interp1 of step g on â/c̃ pair (g−1) & 1, the RHS of step g+1 into pair g & 1
+    const bool chain = !A0.onepass && !(A0.fused && A0.Na <= kEgmFusedMaxNa) &&
+                       !(ws->variant >= 0 && (ws->variant & 8192));
+    if (chain) {
+        if (!ws->egm_x2) AIY_HIP(hipMalloc((void**)&ws->egm_x2, nb));
+        if (!ws->egm_y2) AIY_HIP(hipMalloc((void**)&ws->egm_y2, nb));
+    }
+    double* xs[2] = {ws->g0, ws->egm_x2};
+    double* ys[2] = {ws->g1, ws->egm_y2};
     auto step = [&](int64_t g) {
         EgmArgs A = A0;
         A.c = slot(g - 1);
@@ -146,38 +178,88 @@ static int egm_solve_spec(aiy_ws* ws, const EgmArgs& A0, double* c0, double tol,
         A.diff = sset(g);
         A.flags = (unsigned*)(sset(g) + 2 * kDiffSlots);
         A.diff_clear = A0.onepass ? sset(g + 1) : nullptr;
-        return launch_egm_step(A, st);
+        if (!chain) return launch_egm_step(A, st);
+        A.ahat = xs[(g - 1) & 1];
+        A.cnext = ys[(g - 1) & 1];
+        A.ahat_next = xs[g & 1];
+        A.cnext_next = ys[g & 1];
+        A.diff_clear = sset(g + 1);
+        return launch_egm_chain(A, st);
     };
-    int64_t done = 0, stop = 0, last_enq = 0;
+    if (chain) {  // step 1's RHS from slot 0; it clears step 1's slot set and flag word
+        EgmArgs A = A0;
+        A.c = slot(0);
+        A.ahat = xs[0];
+        A.cnext = ys[0];
+        A.diff = sset(1);
+        A.flags = (unsigned*)(sset(1) + 2 * kDiffSlots);
+        AIY_TRY(launch_egm_rhs(A, st));
+    }
+    struct Batch {
+        int64_t s0, m;  // steps s0 + 1 .. s0 + m
+        int hb;         // host half holding its slot sets
+    };
+    Batch q[2];
+    int nq = 0, hb_next = 0;
+    int64_t enq = 0, stop = 0;
     double d_prev = NAN, d_last = NAN, d_stop = 1.0;
-    while (!stop && done < max_iter) {
+    auto enqueue = [&]() -> int {
         int64_t m = M;
         if (d_last == d_last && d_prev == d_prev && d_last < d_prev && d_last > 0) {
+            // steps the observed geometric decay still needs, counted from the last read
             const double need = std::ceil(std::log(tol / d_last) / std::log(d_last / d_prev));
-            if (need >= 1 && need < (double)m) m = (int64_t)need;
+            int64_t ahead = 0;  // steps in flight, not yet read
+            for (int b = 0; b < nq; ++b) ahead += q[b].m;
+            if (need >= 1 && need - (double)ahead < (double)m)
+                m = (int64_t)std::max(1.0, need - (double)ahead);
         }
-        m = std::min<int64_t>(std::max<int64_t>(m, 1), max_iter - done);
-        for (int64_t t = 0; t < m; ++t) AIY_TRY(step(done + 1 + t));
-        last_enq = done + m;
-        AIY_HIP(hipMemcpyAsync(ws->egm_hslots, ws->egm_slots, SB, hipMemcpyDeviceToHost, st));
-        AIY_HIP(hipStreamSynchronize(st));
-        for (int64_t t = 0; t < m; ++t) {
-            const unsigned long long* h = ws->egm_hslots + (size_t)((done + 1 + t) % R) * SW;
-            if (egm_nonmonotone(h, (unsigned)h[2 * kDiffSlots])) return fail_nonmonotone();
+        m = std::min<int64_t>(std::max<int64_t>(m, 1), max_iter - enq);
+        for (int64_t t = 0; t < m; ++t) AIY_TRY(step(enq + 1 + t));
+        unsigned long long* h = ws->egm_hslots + (size_t)hb_next * R * SW;
+        AIY_HIP(hipMemcpyAsync(h, ws->egm_slots, SB, hipMemcpyDeviceToHost, st));
+        AIY_HIP(hipEventRecord(ws->egm_ev[hb_next], st));
+        q[nq++] = Batch{enq, m, hb_next};
+        hb_next ^= 1;
+        enq += m;
+        return AIY_OK;
+    };
+    if (max_iter > 0) AIY_TRY(enqueue());
+    while (nq > 0) {
+        if (nq < 2 && enq < max_iter) AIY_TRY(enqueue());  // keep the device busy while reading
+        const Batch b = q[0];
+        AIY_HIP(hipEventSynchronize(ws->egm_ev[b.hb]));
+        const unsigned long long* hs = ws->egm_hslots + (size_t)b.hb * R * SW;
+        for (int64_t t = 0; t < b.m; ++t) {
+            const unsigned long long* h = hs + (size_t)((b.s0 + 1 + t) % R) * SW;
+            if (egm_nonmonotone(h, (unsigned)h[2 * kDiffSlots])) {
+                AIY_HIP(hipStreamSynchronize(st));
+                return fail_nonmonotone();
+            }
             const double d = fold_slots_host(h);
             d_prev = d_last;
             d_last = d;
             d_stop = d;
             if (!(d > tol)) {  // Aiyagari_EGM.m:74 `while dist > tol`
-                stop = done + 1 + t;
+                stop = b.s0 + 1 + t;
                 break;
             }
         }
-        if (!stop) done += m;
+        q[0] = q[1];
+        --nq;
+        if (stop) break;
     }
-    const int64_t g = stop ? stop : done;
-    if (g > 0 && g != last_enq) AIY_TRY(step(g));  // policy_k/l of the stopping step (its
-                                                   // slots are not read again)
+    AIY_HIP(hipStreamSynchronize(st));  // (a speculative batch may still be running)
+    const int64_t g = stop ? stop : enq;
+    if (g > 0 && g != enq) {  // policy_k/l of the stopping step (its slots are not read
+                              // again): the two-launch step from its input
+        EgmArgs A = A0;
+        A.c = slot(g - 1);
+        A.cout = slot(g);
+        A.diff = sset(g);
+        A.flags = (unsigned*)(sset(g) + 2 * kDiffSlots);
+        A.diff_clear = A0.onepass ? sset(g + 1) : nullptr;
+        AIY_TRY(launch_egm_step(A, st));
+    }
     *cur_out = g > 0 ? slot(g) : slot(0);
     *dist = d_stop;
     *iters = g;
@@ -279,6 +361,50 @@ int aiy_labor_egm_solve(double* policy_c, const double* a_grid, const double* s,
     if (!policy_l) return fail(AIY_BAD_ARG, "NULL policy_l");
     return egm_host(policy_c, a_grid, s, P, N, Na, r, w, beta, sigma, amin, true, phi, theta,
                     true, tol, max_iter, nullptr, policy_k, policy_l, dist, iters);
+}
+
+int aiy_egm_solve_dev(aiy_ws* ws, double* policy_c, const double* a_grid, const double* s,
+                      const double* P, double r, double w, double beta, double sigma,
+                      double amin, int labor, double phi, double theta, double tol,
+                      int64_t max_iter, double* policy_k, double* policy_l, int64_t* iters,
+                      double* dist, void* stream) {
+    if (!ws || !policy_c || !a_grid || !s || !P || !policy_k || !iters || !dist)
+        return fail(AIY_BAD_ARG, "NULL argument");
+    if (labor && !(phi == phi && theta == theta)) return fail(AIY_NON_FINITE, "phi/theta");
+    if (max_iter < 0) return fail(AIY_BAD_ARG, "max_iter must be >= 0");
+    hipStream_t st = (hipStream_t)stream;
+    AIY_TRY(ensure_egm(ws));
+    const size_t nb = sizeof(double) * ws->N * ws->Na;
+    double d = 1.0;
+    int64_t it = 0;
+    if (max_iter > 0 && d > tol) {  // Aiyagari_EGM.m:74 tests dist = 1 first
+        if (ws->spec_max > 1) {
+            const EgmArgs A = egm_args(ws, policy_c, a_grid, s, P, r, w, beta, sigma, amin,
+                                       labor != 0, phi, theta, nullptr, policy_k,
+                                       labor ? policy_l : nullptr);
+            double* cur = nullptr;
+            AIY_TRY(egm_solve_spec(ws, A, policy_c, tol, max_iter, &cur, &d, &it, st));
+            AIY_HIP(hipMemcpyAsync(policy_c, cur, nb, hipMemcpyDeviceToDevice, st));
+        } else {
+            double* nxt = ws->g2;
+            if (!nxt) {
+                AIY_HIP(hipMalloc((void**)&ws->g2, nb));
+                nxt = ws->g2;
+            }
+            while (d > tol && it < max_iter) {  // :74 (one read per step)
+                ++it;
+                AIY_TRY(egm_step_dev(ws, policy_c, a_grid, s, P, r, w, beta, sigma, amin,
+                                     labor != 0, phi, theta, nxt, policy_k,
+                                     labor ? policy_l : nullptr, nullptr, st));
+                AIY_TRY(read_egm(ws, st, &d));
+                AIY_HIP(hipMemcpyAsync(policy_c, nxt, nb, hipMemcpyDeviceToDevice, st));
+            }
+        }
+    }
+    AIY_HIP(hipStreamSynchronize(st));
+    *iters = it;
+    *dist = d;
+    return AIY_OK;
 }
 
 int aiy_egm_step_dev(aiy_ws* ws, const double* policy_c, const double* a_grid,

@@ -89,90 +89,223 @@ __device__ __forceinline__ int count_le(const double* __restrict__ x, int lo, in
 // trip and each lane finishes its count there.  A wider spread (or a non-increasing â, which
 // the flag turns into an error) falls back to a per-lane search over the narrowed range, so
 // the count — and everything after it — is the plain binary search's.
-__global__ __launch_bounds__(256) void egm_interp_kernel(EgmArgs A, int ntile) {
-    __shared__ double s_x[4][256];
-    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+// interp1 of row j's 64 queries a_grid(a0 .. a0+63), a0 = 64·tile (one wave): writes
+// policy_c_next (cout), policy_k (and policy_l), flags a non-increasing â; returns whether the
+// lane holds a query and sets its |Δc| (d) and policy_c_next (cn).  s_xw: the wave's 256-double
+// LDS window.
+__device__ __forceinline__ bool egm_interp_wave(const EgmArgs& A, int j, int tile,
+                                                double* s_xw, double& d, double& cn,
+                                                long long* cy = nullptr) {
+    const int lane = threadIdx.x & 63;
     const int Na = A.Na;
-    const int wv = blockIdx.x * 4 + wave;
-    bool ok = false;
-    double d = 0.0;
-    if (wv < A.N * ntile) {  // wave-uniform
-        const int j = wv / ntile, tile = wv - j * ntile;
-        const int a0 = tile * 64, a_i = a0 + lane;
-        const int last = min(63, Na - 1 - a0);
-        const bool okl = lane <= last;
-        const size_t t = (size_t)j * Na + (okl ? a_i : a0);
-        const double* __restrict__ x = A.ahat + (size_t)j * Na;
-        const double* __restrict__ y = A.labor ? A.cnext + (size_t)j * Na : A.a;
-        const double q = A.a[okl ? a_i : a0 + last];
-        const double q0 = readlane_d(q, 0), q1 = readlane_d(q, last);
-        int lo0 = 0, hi0 = Na, lo1 = 0, hi1 = Na;
-        while (lo0 < hi0 || lo1 < hi1) {  // wave-uniform bounds
-            const int st0 = max((hi0 - lo0 + 63) >> 6, 1), st1 = max((hi1 - lo1 + 63) >> 6, 1);
-            const int k0 = lo0 + (lane + 1) * st0 - 1, k1 = lo1 + (lane + 1) * st1 - 1;
-            const bool v0 = k0 < hi0, v1 = k1 < hi1;
-            const double x0 = v0 ? x[k0] : 0.0, x1 = v1 ? x[k1] : 0.0;
-            const int c0 = __popcll(__ballot(v0 && x0 <= q0));
-            const int c1 = __popcll(__ballot(v1 && x1 <= q1));
-            if (lo0 < hi0) {
-                const int nh = lo0 + (c0 + 1) * st0 - 1;
-                lo0 += c0 * st0;
-                hi0 = nh < hi0 ? nh : hi0;
-            }
-            if (lo1 < hi1) {
-                const int nh = lo1 + (c1 + 1) * st1 - 1;
-                lo1 += c1 * st1;
-                hi1 = nh < hi1 ? nh : hi1;
-            }
-        }
-        // every lane's count is in [lo0, lo1] (increasing â and queries)
-        int cnt;
-        const int span = lo1 - lo0;
-        if (span >= 0 && span <= 256) {
+    if (cy) cy[0] = (long long)__builtin_amdgcn_s_memtime();
+    const int a0 = tile * 64, a_i = a0 + lane;
+    const int last = min(63, Na - 1 - a0);
+    const bool okl = lane <= last;
+    const size_t t = (size_t)j * Na + (okl ? a_i : a0);
+    const double* __restrict__ x = A.ahat + (size_t)j * Na;
+    const double* __restrict__ y = A.labor ? A.cnext + (size_t)j * Na : A.a;
+    const double q = A.a[okl ? a_i : a0 + last];
+    // the previous step's segments as hints: the wave stages x over [h_first − 16, h_last + 18)
+    // (h = the first and the last lane's segment) in LDS in one round trip and every lane checks
+    // that its count #{k : x_k <= q} lies inside — x_{lo−1} <= q < x_{hi} — before finishing it
+    // there; if any lane's does not (segments moved further, or no hints yet), the wave runs
+    // the full 64-ary search below.  The count, hence everything after it, is the search's.
+    int sgi = -1;
+    if (A.seg) {
+        const int h0 = A.seg[(size_t)j * Na + a0], h1 = A.seg[(size_t)j * Na + a0 + last];
+        const int wlo = max(min(h0, h1) - 16, 0), whi = min(max(h0, h1) + 18, Na);
+        if (h0 >= 0 && h1 >= 0 && h0 <= Na - 2 && h1 <= Na - 2 && whi - wlo + 2 <= 256) {
+            // s_xw[0] = x_{wlo−1} (−inf at 0), s_xw[1 + u] = x_{wlo+u}, s_xw[n−1] = x_{whi} (+inf
+            // at Na): all loads in flight, then the LDS writes
+            const int n = whi - wlo + 2;
+            double v[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const int k = lo0 + u * 64 + lane;
-                if (u * 64 + lane < span) s_x[wave][u * 64 + lane] = x[k];
+                const int k = wlo - 1 + u * 64 + lane;
+                v[u] = (u * 64 + lane < n && k >= 0 && k < Na) ? x[k] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int e = u * 64 + lane, k = wlo - 1 + e;
+                if (e < n) s_xw[e] = k < 0 ? -__builtin_inf() : (k >= Na ? __builtin_inf() : v[u]);
             }
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            int lo = 0, hi = span;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (s_x[wave][mid] <= q) lo = mid + 1;
-                else hi = mid;
+            const bool inl = s_xw[0] <= q;     // count >= wlo
+            const bool inr = q < s_xw[n - 1];  // count <= whi
+            if (__ballot(okl && !(inl && inr)) == 0ull) {
+                int lo = 1, hi = n - 1;  // 1 + #{k in [wlo, whi) : x_k <= q} over s_xw[1 .. n−1)
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (s_xw[mid] <= q) lo = mid + 1;
+                    else hi = mid;
+                }
+                int c = wlo + lo - 1 - 1;  // count − 1
+                c = c < 0 ? 0 : c;
+                sgi = c > Na - 2 ? Na - 2 : c;
             }
-            cnt = lo0 + lo;
-        } else {
-            cnt = count_le(x, min(lo0, lo1), max(lo0, lo1), q);
-        }
-        int sgi = cnt - 1;
-        sgi = sgi < 0 ? 0 : sgi;
-        sgi = sgi > Na - 2 ? Na - 2 : sgi;
-        if (okl) {
-            const double tt = (q - x[sgi]) / (x[sgi + 1] - x[sgi]);
-            double g = y[sgi] + tt * (y[sgi + 1] - y[sgi]);
-            if (a_i > 0 && !(x[a_i - 1] < x[a_i])) atomicOr(A.flags, 1u);
-            const double ws = A.w * A.s[j];
-            double cn;
-            if (A.labor) {
-                if (q < A.amin) g = A.amin;  // :91 (a no-op for a_grid >= amin)
-                cn = g;
-                const double l = labor_dev(g, ws, A.sigma, A.ns, A.phi, A.theta);  // :95
-                const double k = ((1 + A.r) * q + ws * l) - g;                       // :98
-                A.pk[t] = k < 0 ? 0.0 : k;                                           // :99
-                if (A.pl) A.pl[t] = l;
-            } else {
-                if (g < A.amin) g = A.amin;  // :98
-                A.pk[t] = g;
-                cn = ((1 + A.r) * q + ws) - g;  // :102
-            }
-            A.cout[t] = cn;
-            d = fabs(cn - A.c[t]);
-            ok = (d == d);
+            __builtin_amdgcn_wave_barrier();  // window reads done before any reuse of s_xw
         }
     }
+    if (cy) cy[1] = (long long)__builtin_amdgcn_s_memtime();
+    if (sgi < 0) {
+    const double q0 = readlane_d(q, 0), q1 = readlane_d(q, last);
+    int lo0 = 0, hi0 = Na, lo1 = 0, hi1 = Na;
+    while (lo0 < hi0 || lo1 < hi1) {  // wave-uniform bounds
+        const int st0 = max((hi0 - lo0 + 63) >> 6, 1), st1 = max((hi1 - lo1 + 63) >> 6, 1);
+        const int k0 = lo0 + (lane + 1) * st0 - 1, k1 = lo1 + (lane + 1) * st1 - 1;
+        const bool v0 = k0 < hi0, v1 = k1 < hi1;
+        const double x0 = v0 ? x[k0] : 0.0, x1 = v1 ? x[k1] : 0.0;
+        const int c0 = __popcll(__ballot(v0 && x0 <= q0));
+        const int c1 = __popcll(__ballot(v1 && x1 <= q1));
+        if (lo0 < hi0) {
+            const int nh = lo0 + (c0 + 1) * st0 - 1;
+            lo0 += c0 * st0;
+            hi0 = nh < hi0 ? nh : hi0;
+        }
+        if (lo1 < hi1) {
+            const int nh = lo1 + (c1 + 1) * st1 - 1;
+            lo1 += c1 * st1;
+            hi1 = nh < hi1 ? nh : hi1;
+        }
+    }
+    // every lane's count is in [lo0, lo1] (increasing â and queries)
+    int cnt;
+    const int span = lo1 - lo0;
+    if (span >= 0 && span <= 256) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = lo0 + u * 64 + lane;
+            if (u * 64 + lane < span) s_xw[u * 64 + lane] = x[k];
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        int lo = 0, hi = span;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (s_xw[mid] <= q) lo = mid + 1;
+            else hi = mid;
+        }
+        cnt = lo0 + lo;
+    } else {
+        cnt = count_le(x, min(lo0, lo1), max(lo0, lo1), q);
+    }
+    sgi = cnt - 1;
+    sgi = sgi < 0 ? 0 : sgi;
+    sgi = sgi > Na - 2 ? Na - 2 : sgi;
+    }
+    if (A.seg && okl) A.seg[t] = sgi;
+    if (cy) cy[2] = (long long)__builtin_amdgcn_s_memtime();
+    d = 0.0;
+    cn = 0.0;
+    if (!okl) return false;
+    const double tt = (q - x[sgi]) / (x[sgi + 1] - x[sgi]);
+    double g = y[sgi] + tt * (y[sgi + 1] - y[sgi]);
+    if (a_i > 0 && !(x[a_i - 1] < x[a_i])) atomicOr(A.flags, 1u);
+    const double ws = A.w * A.s[j];
+    if (A.labor) {
+        if (q < A.amin) g = A.amin;  // :91 (a no-op for a_grid >= amin)
+        cn = g;
+        const double l = labor_dev(g, ws, A.sigma, A.ns, A.phi, A.theta);  // :95
+        const double k = ((1 + A.r) * q + ws * l) - g;                       // :98
+        A.pk[t] = k < 0 ? 0.0 : k;                                           // :99
+        if (A.pl) A.pl[t] = l;
+    } else {
+        if (g < A.amin) g = A.amin;  // :98
+        A.pk[t] = g;
+        cn = ((1 + A.r) * q + ws) - g;  // :102
+    }
+    A.cout[t] = cn;
+    d = fabs(cn - A.c[t]);
+    if (cy) {
+        __builtin_amdgcn_s_waitcnt(0);  // (instrumentation) the loads above have landed
+        cy[3] = (long long)__builtin_amdgcn_s_memtime();
+    }
+    return true;
+}
+
+// (instrumentation) one record per wave: entry/exit wall clock, XCC, then shader cycles of
+// the phases: search, window count, interpolation loads, the rest (RHS of t+1 / reduction)
+__device__ __forceinline__ void egm_trace(const EgmArgs& A, int rec, long long t_in,
+                                          const long long* cy, int ncy) {
+    if ((threadIdx.x & 63) != 0) return;
+    const long long now = (long long)__builtin_amdgcn_s_memtime();
+    long long* tr = A.trace + 16 * (size_t)rec;
+    tr[0] = t_in;
+    tr[1] = (long long)wall_clock64();
+    tr[2] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));  // HW_REG_XCC_ID
+    for (int p = 1; p < ncy; ++p) tr[2 + p] = cy[p] - cy[p - 1];
+    tr[2 + ncy] = now - cy[ncy - 1];
+}
+
+__global__ __launch_bounds__(256) void egm_interp_kernel(EgmArgs A, int ntile) {
+    __shared__ double s_x[4][256];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wv = blockIdx.x * 4 + wave;
+    bool ok = false;
+    double d = 0.0;
+    long long cy[4] = {0, 0, 0, 0};
+    const long long t_in = A.trace ? (long long)wall_clock64() : 0;
+    if (wv < A.N * ntile) {  // wave-uniform
+        const int j = wv / ntile, tile = wv - j * ntile;
+        double cn;
+        ok = egm_interp_wave(A, j, tile, s_x[wave], d, cn, A.trace ? cy : nullptr) && d == d;
+    }
     block_max_to_slots(ok, d, A.diff);
+    if (A.trace && wv < A.N * ntile) egm_trace(A, wv, t_in, cy, 4);
+}
+
+// Chained steps for large grids (the speculative solve, Na > 1,024): ONE launch per step in
+// the steady state.  The Euler RHS of a node needs policy_c at that node for every m only, so
+// the workgroup that produces step t's policy_c_next on a tile of 64 nodes (wave j: interp1 of
+// row j, as egm_interp_kernel) holds step t+1's inputs there and forms step t+1's RHS and â on
+// the same tile (as egm_rhs_kernel, u'(c_m) through LDS) into the other â/c̃ buffer.  The
+// interp1 of step t+1 then runs in the next launch, after every â of step t+1 exists.  Same
+// operations on the same values as rhs + interp, so bit for bit the two-launch step.  The first
+// workgroup clears step t+1's slot set and flag word (diff_clear) for the next launch.
+__global__ __launch_bounds__(1024) void egm_chain_kernel(EgmArgs A) {
+    __shared__ double s_x[16][256];
+    __shared__ double s_up[16][64];
+    const int lane = threadIdx.x & 63;
+    const int m = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // blockDim = 64·N
+    const int N = A.N, Na = A.Na;
+    if (blockIdx.x == 0 && A.diff_clear)
+        for (int q = threadIdx.x; q < kEgmSlotWords; q += blockDim.x) A.diff_clear[q] = 0ull;
+    const int j = m;
+    const double coef0 = A.beta * (1 + A.r);
+    double pj[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) pj[q] = q < N ? coef0 * A.P[j * N + q] : 0.0;
+    double d, cn;
+    long long cy[4] = {0, 0, 0, 0};
+    const long long t_in = A.trace ? (long long)wall_clock64() : 0;
+    const bool okl = egm_interp_wave(A, j, blockIdx.x, s_x[m], d, cn, A.trace ? cy : nullptr);
+    const bool ok = okl && d == d;
+    // step t+1's Euler RHS on this tile: u'(policy_c_next) of every row through LDS
+    const int a_i = blockIdx.x * 64 + lane;
+    s_up[m][lane] = okl ? uprime_dev(cn, A.sigma, A.ns) : 0.0;
+    __syncthreads();
+    if (okl) {
+        double acc = 0.0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            if (q < N) acc = acc + pj[q] * s_up[q][lane];
+        const double c2 = aiy_pow(acc, -1.0 / A.sigma);  // :88
+        const double ws = A.w * A.s[j];
+        const double ag = A.a[a_i];
+        double ah;
+        if (A.labor) {
+            const double ls = labor_dev(c2, ws, A.sigma, A.ns, A.phi, A.theta);
+            ah = ((c2 + ag) - ws * ls) / (1 + A.r);
+        } else {
+            ah = ((c2 + ag) - ws) / (1 + A.r);
+        }
+        A.ahat_next[(size_t)j * Na + a_i] = ah;
+        A.cnext_next[(size_t)j * Na + a_i] = c2;
+    }
+    block_max_to_slots(ok, d, A.diff);
+    if (A.trace) egm_trace(A, blockIdx.x * N + j, t_in, cy, 4);
 }
 
 // Small grids (the scripts' Na = 400, up to 1,024): one launch per step, one workgroup per productivity
@@ -491,6 +624,20 @@ __global__ __launch_bounds__(1024) void egm_scatter_kernel(EgmArgs A) {
         if (f & 1) atomicMax(sl, kk);
         if (f) atomicOr(sl + 1, (unsigned long long)f);
     }
+}
+
+int launch_egm_rhs(const EgmArgs& A, hipStream_t st) {
+    if (A.N > 16) return fail(AIY_BAD_SHAPE, "EGM kernels support N <= 16 productivity states");
+    egm_rhs_kernel<<<(A.Na + 63) / 64, 64 * A.N, 0, st>>>(A);
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
+}
+
+int launch_egm_chain(const EgmArgs& A, hipStream_t st) {
+    if (A.N > 16) return fail(AIY_BAD_SHAPE, "EGM kernels support N <= 16 productivity states");
+    egm_chain_kernel<<<(A.Na + 63) / 64, 64 * A.N, 0, st>>>(A);
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
 }
 
 int launch_egm_step(const EgmArgs& A, hipStream_t st) {

@@ -55,12 +55,17 @@ struct aiy_ws {
     size_t dist_n = 0;
     int dist_m = 0;
     double* dist_ring = nullptr;
-    unsigned long long* dist_slots = nullptr;   // device [dist_m][2*kDiffSlots]
-    unsigned long long* dist_hslots = nullptr;  // pinned host, same shape
+    unsigned long long* dist_slots = nullptr;   // device [2 dist_m + 1][2*kDiffSlots]
+    unsigned long long* dist_hslots = nullptr;  // pinned host, two copies (batches in flight)
+    hipEvent_t dist_ev[2] = {nullptr, nullptr};
     void free_dist_spec() {
         if (dist_ring) (void)hipFree(dist_ring);
         if (dist_slots) (void)hipFree(dist_slots);
         if (dist_hslots) (void)hipHostFree(dist_hslots);
+        for (auto& e : dist_ev) {
+            if (e) (void)hipEventDestroy(e);
+            e = nullptr;
+        }
         dist_ring = nullptr; dist_slots = nullptr; dist_hslots = nullptr;
         dist_n = 0; dist_m = 0;
     }
@@ -85,17 +90,26 @@ struct aiy_ws {
     size_t egm_spec_n = 0;
     int egm_spec_m = 0;
     double* egm_ring = nullptr;
-    unsigned long long* egm_slots = nullptr;    // device [spec_max + 1][2*kDiffSlots + 2]
-    unsigned long long* egm_hslots = nullptr;   // pinned host, same shape
+    unsigned long long* egm_slots = nullptr;    // device [2 spec_max + 1][2*kDiffSlots + 2]
+    unsigned long long* egm_hslots = nullptr;   // pinned host, two copies (batches in flight)
+    hipEvent_t egm_ev[2] = {nullptr, nullptr};  // end of each in-flight batch's slot copy
     // single EGM steps on the one-pass path: two slot sets (step t writes set t & 1 and clears
     // the other), zeroed at allocation; egm_cur = the set of the last step
     unsigned long long* egm_d2 = nullptr;
     unsigned long long* egm_cur = nullptr;
     int egm_par = 0;
+    // chained EGM solve (Na > 1,024): the second â / c̃ pair (step parity)
+    double* egm_x2 = nullptr;
+    double* egm_y2 = nullptr;
+    int* egm_seg = nullptr;  // [N][Na] interp1 segments of the last step (hints), -1 = none
     void free_egm_spec() {
         if (egm_ring) (void)hipFree(egm_ring);
         if (egm_slots) (void)hipFree(egm_slots);
         if (egm_hslots) (void)hipHostFree(egm_hslots);
+        for (auto& e : egm_ev) {
+            if (e) (void)hipEventDestroy(e);
+            e = nullptr;
+        }
         egm_ring = nullptr; egm_slots = nullptr; egm_hslots = nullptr;
         egm_spec_n = 0; egm_spec_m = 0;
     }
@@ -145,7 +159,7 @@ struct aiy_ws {
     }
     void free_all() {
         void* ps[] = {EV, T, T32, Dm, Dm8, Dt, Dm512, touched, best0, idx0, mom, dis, kf, partial, diff, hitcount, trace, g0, g1, g2, gi,
-                      d_key, d_off, d_wr, d_mass, d_part, pers, egm_d2};
+                      d_key, d_off, d_wr, d_mass, d_part, pers, egm_d2, egm_x2, egm_y2, egm_seg};
         for (void* p : ps)
             if (p) (void)hipFree(p);
         free_spec();
@@ -158,6 +172,8 @@ struct aiy_ws {
         idx0 = nullptr; mom = nullptr; partial = nullptr; diff = nullptr; hitcount = nullptr; trace = nullptr; trace_cap = 0; hdiff = nullptr;
         g0 = g1 = g2 = nullptr; gi = nullptr; pers = nullptr;
         egm_d2 = egm_cur = nullptr; egm_par = 0;
+        egm_x2 = egm_y2 = nullptr;
+        egm_seg = nullptr;
         d_key = d_off = nullptr; d_wr = d_mass = d_part = nullptr;
         partial_cap = 0;
     }

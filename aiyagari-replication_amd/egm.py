@@ -72,3 +72,16 @@ def egm_step_dev(ws, policy_c, a_grid, s, P, r, w, beta, sigma, amin, out, polic
                                  d(w), d(beta), d(sigma), d(amin), ip(1 if labor else 0), d(phi),
                                  d(theta), ptr(out), ptr(policy_k), ptr(policy_l), ptr(diff),
                                  stream_handle(stream)))
+
+
+def egm_solve_dev(ws, policy_c, a_grid, s, P, r, w, beta, sigma, amin, tol, max_iter, policy_k,
+                  labor=False, phi=1.0, theta=1.0, policy_l=None, stream=None):
+    """aiy_egm_solve_dev: the solve loop on device (torch tensors [N][Na]); policy_c is
+    updated in place.  Returns (iters, dist)."""
+    it, dist = C.c_int64(), C.c_double()
+    check(lib().aiy_egm_solve_dev(ws.handle, ptr(policy_c), ptr(a_grid), ptr(s), ptr(P), d(r),
+                                  d(w), d(beta), d(sigma), d(amin), ip(1 if labor else 0),
+                                  d(phi), d(theta), d(tol), i64(max_iter), ptr(policy_k),
+                                  ptr(policy_l), C.byref(it), C.byref(dist),
+                                  stream_handle(stream)))
+    return it.value, dist.value

@@ -196,7 +196,29 @@ def egm_leg(pkg, dev, Na, labor=False, steps=50, reps=5, cpu_threads=1, variant=
         e1.record()
         torch.cuda.synchronize()
         ms.append(e0.elapsed_time(e1) / steps)
-    step_ms = _median(ms)
+    single_ms = _median(ms)
+    # the device-tier solve loop (aiy_egm_solve_dev: speculative batches of steps; for
+    # Na > 1,024 each step is ONE chained launch, interp1 of t + the RHS of t+1): `steps`
+    # steps at tol = 0 from the same start, wall per step (host reads of the batches included)
+    ws2 = pkg.Workspace(N, Na)
+    if variant >= 0:
+        ws2.set_variant(variant)
+    c2 = t(pc0)
+    pk2 = torch.zeros_like(c2)
+    pl2 = torch.zeros_like(c2) if labor else None
+    solve_dev = lambda n: pkg.egm_solve_dev(ws2, c2, a_t, s_t, P_t, r, w, cal["beta"], cal["sigma"],
+                                            cal["amin"], 0.0, n, pk2, labor=labor, phi=1.0,
+                                            theta=1.0, policy_l=pl2)
+    solve_dev(20)
+    sms = []
+    for _ in range(reps):
+        c2.copy_(t(pc0))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        solve_dev(200)
+        torch.cuda.synchronize()
+        sms.append((time.perf_counter() - t0) * 1e3 / 200)
+    step_ms = _median(sms)
     bps = 32 if labor else 24
     states = N * Na
     gbs = states * bps / (step_ms * 1e-3) / 1e9
@@ -229,9 +251,16 @@ def egm_leg(pkg, dev, Na, labor=False, steps=50, reps=5, cpu_threads=1, variant=
         path = "1 launch per step: egm_fused_kernel, a workgroup per z-state)"
     elif Na > 1024 and variant >= 0 and variant & 4096:
         path = "1 launch per step: egm_scatter_kernel, segments -> query ranges of a_grid)"
+    elif Na > 1024 and not (variant >= 0 and variant & 8192):
+        path = ("1 launch per step in the solve loop: egm_chain_kernel, interp1 of step t + "
+                "the Euler RHS of step t+1 on the same tiles)")
     else:
         path = "2 launches per step: Euler RHS, interp1 inversion)"
-    return {"workload": f"{name} steps, Na={Na} Nz={N} Rouwenhorst, device tier (" + path,
+    return {"workload": f"{name} steps, Na={Na} Nz={N} Rouwenhorst, device-tier solve loop "
+                        f"(aiy_egm_solve_dev, 200 steps at tol = 0; " + path,
+            "single_step_dev": {"us_per_step": single_ms * 1e3,
+                                "path": "aiy_egm_step_dev one step at a time (the two-launch step "
+                                        "for Na > 1,024, the fused launch below), Python-issued"},
             "solve": {"iters": iters, "wall_ms": solve_s * 1e3,
                       "us_per_iteration": solve_s / max(iters, 1) * 1e6,
                       "path": "host tier (aiy_egm_solve / aiy_labor_egm_solve): speculative "

@@ -263,7 +263,8 @@ int aiy_ws_set_persistent(aiy_ws* ws, int persistent);
  * bit 10 = the plain exhaustive scan, bit 12 = cooperating waves deal the first superblock's
  * passing 8-blocks round-robin (else by 64-block).  EGM steps on this workspace: bit 11 = two
  * launches per step even when Na <= 1024 (default there: one fused launch); bit 12 = the one-pass
- * scatter step when Na > 1024 (default there: two launches).  Bit 13 = tiles in
+ * scatter step when Na > 1024 (default there: two launches, one chained launch per step in the
+ * solve loops); bit 13 = no chaining in the solve loops; bit 14 = no interp1 segment hints.  Bit 13 = tiles in
  * descending asset order (one wave per tile).  Results are identical for every value in
  * [-1, 16383].
  * -1 (default): chosen by size — Na <= 4096: 2 cooperating waves per tile (A1), 4 with bit 12
@@ -309,6 +310,16 @@ int aiy_egm_step_dev(aiy_ws* ws, const double* policy_c, const double* a_grid,
                      double sigma, double amin, int labor, double phi, double theta,
                      double* policy_c_next, double* policy_k, double* policy_l, double* diff,
                      void* stream);
+/* A4/A5 solve loop on device (Aiyagari_EGM.m:71-110, labour :64-107): policy_c (in: the guess,
+ * out: the last policy_c_next) [N][Na]; policy_k, policy_l (labour, nullable otherwise)
+ * [N][Na].  Speculative batches of steps between dist reads, as aiy_egm_solve; for Na > 1024
+ * each step is ONE launch (interp1 of step t with the Euler RHS of step t+1 on the same tiles;
+ * variant bit 13: two launches).  iters, dist: host. */
+int aiy_egm_solve_dev(aiy_ws* ws, double* policy_c, const double* a_grid, const double* s,
+                      const double* P, double r, double w, double beta, double sigma,
+                      double amin, int labor, double phi, double theta, double tol,
+                      int64_t max_iter, double* policy_k, double* policy_l, int64_t* iters,
+                      double* dist, void* stream);
 /* A9 on device: policy_rows [N][Na]; z1 0-based; k_supply (device double), sim_k/sim_z
  * nullable (device), status (device int32: 0 ok, 1 = find() empty). */
 int aiy_sim_capital_dev(aiy_ws* ws, const double* policy_rows, const double* a_grid,

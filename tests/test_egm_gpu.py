@@ -186,3 +186,46 @@ def test_egm_n1_large_grid_solve(pkg, gpu, Na):
     assert R["iters"] == Ro["iters"] and R["dist"] == Ro["dist"]
     assert np.array_equal(R["policy_c"], Ro["policy_c"].T)
     assert np.array_equal(R["policy_k"], Ro["policy_k"].T)
+
+
+@pytest.mark.parametrize("Na,N,labor", [(1025, 7, False), (4099, 7, True), (20000, 7, False),
+                                        (20000, 7, True), (3000, 1, False), (2000, 16, True)])
+def test_egm_chained_solve_dev(pkg, gpu, Na, N, labor):
+    """aiy_egm_solve_dev: for Na > 1,024 each step of the speculative solve is ONE launch
+    (egm_chain_kernel: interp1 of step t + the Euler RHS of step t+1 on the same tiles) — equal
+    bit for bit to the two-launch steps (variant bit 13) and to the C loop: iteration count,
+    dist, policy_c, policy_k (and policy_l)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    cal = no.calib_aiyagari(Na=Na, shocks="rouwenhorst", N=N) if N not in (7, 1) else \
+        no.calib_aiyagari(Na=Na, shocks="rouwenhorst")
+    a, s, P = cal["a_grid"], cal["s"], cal["P"]
+    if N == 1:
+        s, P = np.array([1.0]), np.array([[1.0]])
+    N = P.shape[0]
+    r = 0.03
+    w = no.wage(r, 0.36, 0.08)
+    t = lambda x: torch.as_tensor(np.ascontiguousarray(x), device=dev)
+    pc0 = np.tile(((1 + r) * a + w * np.mean(s))[None, :], (N, 1))
+    outs = []
+    for var in (-1, 8192):
+        ws = pkg.Workspace(N, Na)
+        if var >= 0:
+            ws.set_variant(var)
+        c = t(pc0)
+        pk = torch.zeros_like(c)
+        pl = torch.zeros_like(c) if labor else None
+        it, dist = pkg.egm_solve_dev(ws, c, t(a), t(s), t(P), r, w, 0.96, 5.0, cal["amin"], 1e-6,
+                                     400, pk, labor=labor, phi=1.0, theta=1.0, policy_l=pl)
+        outs.append((it, dist, c.cpu().numpy(), pk.cpu().numpy(),
+                     pl.cpu().numpy() if labor else None))
+    (i0, d0, c0_, k0, l0), (i1, d1, c1, k1, l1) = outs
+    assert i0 == i1 and d0 == d1
+    assert np.array_equal(c0_, c1) and np.array_equal(k0, k1)
+    if labor:
+        assert np.array_equal(l0, l1)
+        Ro = corc.labor_egm_solve(pc0, a, s, P, r, w, 0.96, 5.0, 1.0, 1.0, cal["amin"], 1e-6, 400)
+    else:
+        Ro = corc.egm_solve(pc0, a, s, P, r, w, 0.96, 5.0, cal["amin"], 1e-6, 400)
+    assert i0 == Ro["iters"] and d0 == Ro["dist"]
+    assert np.array_equal(c0_, Ro["policy_c"]) and np.array_equal(k0, Ro["policy_k"])

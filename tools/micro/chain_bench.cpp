@@ -76,6 +76,19 @@ int main() {
         span(step, 20);
         printf("{\"egm_step_variant\": %d, \"us_per_step\": %.3f}\n", variant, span(step, 200));
     }
+    for (int variant : {-1, 8192}) {  // the device-tier EGM solve: chained steps (default), two
+        CK(aiy_ws_set_variant(ws, variant));  // launches per step (bit 13); 200 steps at tol = 0
+        int64_t itn;
+        double dd;
+        auto solve = [&](int) {
+            hipMemcpyAsync(dc[0], c0.data(), n * 8, hipMemcpyHostToDevice, st);
+            return aiy_egm_solve_dev(ws, dc[0], da, ds, dP, r, w, beta, sigma, 0.0, 0, 1.0, 1.0,
+                                     0.0, 200, dpk, nullptr, &itn, &dd, st);
+        };
+        solve(0);
+        printf("{\"egm_solve_dev_variant\": %d, \"us_per_step\": %.3f}\n", variant,
+               span(solve, 3) / 200);
+    }
     CK(aiy_ws_set_variant(ws, -1));
     int cur = 0;
     auto sweep = [&](int q) {  // headline sweeps from v = 0, hint = the previous argmax
