@@ -271,20 +271,26 @@ int ws_read_diff(aiy_ws* ws, hipStream_t st, double* d) {
 // of the diff (sweeps still needed to reach tol), capped at spec_max.
 static int bell_solve_spec(aiy_ws* ws, BellCall c, double* v_a, double* v_b, double tol,
                            int64_t max_iter, int64_t* iters, int* out_new, hipStream_t st) {
-    const int R = ws->spec_max + 1, Rp = ws->spec_max;
+    // rings sized for two batches in flight: v 2M + 1 (the stopping sweep's v_new and v_old
+    // survive the next batch), idx / policies 2M, diff pairs 2M (indexed by sweep)
+    const int M = ws->spec_max, R = 2 * M + 1, Rp = 2 * M, D = 2 * M;
     const size_t n = (size_t)ws->N * ws->Na;
-    if (ws->spec_n != n) {
+    if (ws->spec_n != n || ws->spec_m != M) {
         ws->free_spec();
         AIY_TRY(dalloc(&ws->spec_v, (size_t)R * n));
         AIY_TRY(dalloc(&ws->spec_idx, (size_t)Rp * n));
         AIY_TRY(dalloc(&ws->spec_pol, (size_t)Rp * 3 * n));
-        AIY_TRY(dalloc(&ws->spec_diff, 2 * (size_t)Rp));
-        AIY_HIP(hipHostMalloc((void**)&ws->spec_hdiff, 2 * (size_t)Rp * sizeof(unsigned long long)));
+        AIY_TRY(dalloc(&ws->spec_diff, 2 * (size_t)D));
+        AIY_HIP(hipHostMalloc((void**)&ws->spec_hdiff, 2 * 2 * (size_t)D * sizeof(unsigned long long)));
+        for (int b = 0; b < 2; ++b)
+            AIY_HIP(hipEventCreateWithFlags(&ws->spec_ev[b], hipEventDisableTiming));
         ws->spec_n = n;
+        ws->spec_m = M;
     }
     auto vslot = [&](int64_t g) { return ws->spec_v + (size_t)(g % R) * n; };
     auto islot = [&](int64_t g) { return ws->spec_idx + (size_t)(g % Rp) * n; };
     auto pslot = [&](int64_t g, int q) { return ws->spec_pol + ((size_t)(g % Rp) * 3 + q) * n; };
+    auto dslot = [&](int64_t g) { return ws->spec_diff + 2 * (size_t)(g % D); };
     const size_t vb = n * sizeof(double);
     // slot 0 = v_old of sweep 1; slot 1 = the incoming v_new buffer (the labour sweep's
     // keep-incoming rule reads it on sweep 1)
@@ -310,17 +316,28 @@ static int bell_solve_spec(aiy_ws* ws, BellCall c, double* v_a, double* v_b, dou
                                            hipMemcpyDeviceToDevice, st));
         }
     }
-    int64_t done = 0, stop = 0;
+    // Batches of m sweeps, each ending with a D2H copy of the diff pairs and an event; two in
+    // flight: the host reads batch k while batch k+1 runs, so the device never waits for a read
+    struct Batch {
+        int64_t s0, m;  // sweeps s0 + 1 .. s0 + m
+        int hb;         // host half holding its diff pairs
+    };
+    Batch q[2];
+    int nq = 0, hb_next = 0;
+    int64_t enq = 0, stop = 0;
     double d_prev = NAN, d_last = NAN;
-    while (!stop && done < max_iter) {
-        int64_t m = ws->spec_max;
+    auto enqueue = [&]() -> int {
+        int64_t m = M;
         if (d_last == d_last && d_prev == d_prev && d_last < d_prev && d_last > 0) {
-            double need = std::ceil(std::log(tol / d_last) / std::log(d_last / d_prev));
-            if (need >= 1 && need < (double)m) m = (int64_t)need;
+            const double need = std::ceil(std::log(tol / d_last) / std::log(d_last / d_prev));
+            int64_t ahead = 0;  // sweeps in flight, not yet read
+            for (int b = 0; b < nq; ++b) ahead += q[b].m;
+            if (need >= 1 && need - (double)ahead < (double)m)
+                m = (int64_t)std::max(1.0, need - (double)ahead);
         }
-        m = std::min<int64_t>(std::max<int64_t>(m, 1), max_iter - done);
+        m = std::min<int64_t>(std::max<int64_t>(m, 1), max_iter - enq);
         for (int64_t t = 0; t < m; ++t) {
-            const int64_t g = done + 1 + t;
+            const int64_t g = enq + 1 + t;
             c.hint = (g == 1) ? first_hint : islot(g - 1);
             c.keep_incoming = (g == 1);
             c.v_old = vslot(g - 1);
@@ -329,30 +346,43 @@ static int bell_solve_spec(aiy_ws* ws, BellCall c, double* v_a, double* v_b, dou
             c.pk = upk ? pslot(g, 0) : nullptr;
             c.pc = upc ? pslot(g, 1) : nullptr;
             c.pl = upl ? pslot(g, 2) : nullptr;
-            // sweep t's {max bits, any} lands in slot t: folded by sweep t+1's table kernel,
+            // sweep g's {max bits, any} lands in pair g: folded by sweep g+1's table kernel,
             // or by a reduce launch after the batch's last sweep
-            c.prev_diff_out = t ? ws->spec_diff + 2 * (t - 1) : nullptr;
-            c.diff_out = (t == m - 1) ? reinterpret_cast<double*>(ws->spec_diff + 2 * t) : nullptr;
+            c.prev_diff_out = t ? dslot(g - 1) : nullptr;
+            c.diff_out = (t == m - 1) ? reinterpret_cast<double*>(dslot(g)) : nullptr;
             AIY_TRY(bell_sweep_dev(ws, c, st));
         }
-        AIY_HIP(hipMemcpyAsync(ws->spec_hdiff, ws->spec_diff,
-                               2 * (size_t)m * sizeof(unsigned long long),
+        unsigned long long* h = ws->spec_hdiff + (size_t)hb_next * 2 * D;
+        AIY_HIP(hipMemcpyAsync(h, ws->spec_diff, 2 * (size_t)D * sizeof(unsigned long long),
                                hipMemcpyDeviceToHost, st));
-        AIY_HIP(hipStreamSynchronize(st));
-        for (int64_t t = 0; t < m; ++t) {
-            const unsigned long long* h = ws->spec_hdiff + 2 * t;
+        AIY_HIP(hipEventRecord(ws->spec_ev[hb_next], st));
+        q[nq++] = Batch{enq, m, hb_next};
+        hb_next ^= 1;
+        enq += m;
+        return AIY_OK;
+    };
+    if (max_iter > 0) AIY_TRY(enqueue());
+    while (nq > 0) {
+        if (nq < 2 && enq < max_iter) AIY_TRY(enqueue());
+        const Batch b = q[0];
+        AIY_HIP(hipEventSynchronize(ws->spec_ev[b.hb]));
+        const unsigned long long* hs = ws->spec_hdiff + (size_t)b.hb * 2 * D;
+        for (int64_t t = 0; t < b.m; ++t) {
+            const unsigned long long* h = hs + 2 * ((b.s0 + 1 + t) % D);
             double d = NAN;  // {max|Δ| bits, any non-NaN} (reduce_slots_kernel)
             if (h[1]) std::memcpy(&d, &h[0], sizeof d);
             d_prev = d_last;
             d_last = d;
             if (d < tol) {  // Aiyagari_VFI.m:85-86
-                stop = done + 1 + t;
+                stop = b.s0 + 1 + t;
                 break;
             }
         }
-        if (!stop) done += m;
+        q[0] = q[1];
+        --nq;
+        if (stop) break;
     }
-    const int64_t g = stop ? stop : max_iter;
+    const int64_t g = stop ? stop : enq;
     // the plain loop leaves v_new in v_b after odd sweep counts (ping-pong from v_a)
     const int nw = (g & 1) ? 1 : 0;
     double* vnew = nw ? v_b : v_a;

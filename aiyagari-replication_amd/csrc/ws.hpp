@@ -81,8 +81,10 @@ struct aiy_ws {
     double* spec_v = nullptr;
     int* spec_idx = nullptr;
     double* spec_pol = nullptr;                 // [spec_max][3][N*Na] (k, c, l)
-    unsigned long long* spec_diff = nullptr;    // device [2*spec_max]
-    unsigned long long* spec_hdiff = nullptr;   // pinned host [2*spec_max]
+    int spec_m = 0;                             // spec_max the rings were sized for
+    unsigned long long* spec_diff = nullptr;    // device [2 * 2*spec_max]: a pair per sweep
+    unsigned long long* spec_hdiff = nullptr;   // pinned host, two copies (batches in flight)
+    hipEvent_t spec_ev[2] = {nullptr, nullptr};
     // persistent small-grid solve: diff slots [2][2*kDiffSlots], barrier words, result
     unsigned long long* pers = nullptr;
     bool persist = false;  // aiy_ws_set_persistent (measured slower: off by default)
@@ -154,8 +156,12 @@ struct aiy_ws {
         for (void* p : ps)
             if (p) (void)hipFree(p);
         if (spec_hdiff) (void)hipHostFree(spec_hdiff);
+        for (auto& e : spec_ev) {
+            if (e) (void)hipEventDestroy(e);
+            e = nullptr;
+        }
         spec_v = nullptr; spec_idx = nullptr; spec_pol = nullptr; spec_diff = nullptr;
-        spec_hdiff = nullptr; spec_n = 0;
+        spec_hdiff = nullptr; spec_n = 0; spec_m = 0;
     }
     void free_all() {
         void* ps[] = {EV, T, T32, Dm, Dm8, Dt, Dm512, touched, best0, idx0, mom, dis, kf, partial, diff, hitcount, trace, g0, g1, g2, gi,
