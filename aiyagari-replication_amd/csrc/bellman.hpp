@@ -59,7 +59,22 @@ struct BellArgs {
     const double* wv;  // [C] device: w of each candidate
     const int* stop;   // [C] device: nonzero = stopped at that sweep (skipped from then on)
     int parity;
+    // Chained sweeps (A1 tree screen, one wave per tile): the tree kernel also builds the NEXT
+    // sweep's table from the v_new it writes, so a chain of sweeps is one launch per sweep.
+    // Each wave stores its v_new write-through and adds to its tile's arrival counter; the wave
+    // whose add completes the tile's N rows computes EV, D, the 8-block and 64-block maxima of
+    // that tile's 64 candidates for every row (bell_table_kernel's values, bit for bit).
+    const double* Dm64;  // nullable: level-0 superblock bounds = max of 8 64-block maxima (Dm512 unused)
+    double* nEV;         // nullable (chain off): the next sweep's EV / Dt / Dm8 / Dm64
+    double* nDt;
+    double* nDm8;
+    double* nDm64;
+    unsigned* tcnt;                  // [ntile] arrival counters, zero between launches
+    const unsigned long long* fsrc;  // nullable: the previous sweep's slot set, folded into fold[]
+    unsigned long long* clr;         // nullable: slot set cleared for the sweep after next
 };
+// rows per chained table tile (the last arriver holds one V column of the tile in registers)
+constexpr int kChainMaxN = 16;
 
 // EV by fp64 MFMA from this productivity-grid size up (the variant bits 14 / 15 force VALU /
 // MFMA); below it the table kernel's sequential VALU sum, which the C oracle restates bit for

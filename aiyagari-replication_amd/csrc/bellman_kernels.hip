@@ -835,6 +835,97 @@ __global__ __launch_bounds__(256, MINW) void bell_screen_kernel(BellArgs A, int 
     }
 }
 
+// ------------------------------------------------------------------------------ chained tables
+// Level-0 bound of superblock sb of row i: the table kernel's 512-block maximum, or — chained
+// sweeps — the maximum of its eight 64-block maxima (the same blocks; any upper bound of the
+// superblock's keys is a valid bound, so the screen's result cannot depend on which)
+__device__ __forceinline__ double sb_bound(const BellArgs& A, int i, int sb) {
+    if (!A.Dm64) return A.Dm512[(size_t)i * A.nb512 + sb];
+    const double* __restrict__ p = A.Dm64 + (size_t)i * A.nb + 8 * sb;
+    const int n = A.nb - 8 * sb;
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = u < n ? p[u] : -__builtin_inf();  // all loads in flight
+    return fmax(fmax(fmax(v[0], v[1]), fmax(v[2], v[3])), fmax(fmax(v[4], v[5]), fmax(v[6], v[7])));
+}
+
+// Chained sweeps, the slot ring: sweep g writes slot set g mod 3; one wave of sweep g folds set
+// g − 1 (complete: its launch has ended) into fold[0..1] and clears set g + 1 (folded or
+// reduced by an earlier launch), so no sweep of a chain needs a memset or a reduce launch.
+__device__ __forceinline__ void chain_slots(const BellArgs& A) {
+    const int l = threadIdx.x & 63;
+    static_assert(kDiffSlots == 64, "one wave folds the slots");
+    if (A.fsrc && A.fold) {  // reduce_slots_kernel's fold
+        unsigned long long m = A.fsrc[2 * l];
+        const int any = __ballot((A.fsrc[2 * l + 1] & 1ull) != 0ull) != 0ull;
+        for (int off = 32; off > 0; off >>= 1) {
+            const unsigned long long o = __shfl_xor(m, off);
+            m = o > m ? o : m;
+        }
+        if (l == 0) {
+            A.fold[0] = m;
+            A.fold[1] = any ? 1ull : 0ull;
+        }
+    }
+    if (A.clr) {
+        A.clr[l] = 0ull;
+        A.clr[l + 64] = 0ull;
+    }
+}
+
+// The next sweep's table on tile `tile` (candidates k = 64·tile + lane), built by the wave whose
+// arrival completes the tile: every wave of the launch has stored its v_new write-through (sc1)
+// and waited for the stores (vmcnt 0) before its lane 0 adds to the tile's agent-scope counter,
+// so the wave that draws N − 1 reads the tile's N rows of v_new with sc1 loads after its add
+// has returned (MI355X_MICROARCH.md, inter-workgroup visibility: the counter hand-off row).
+// EV(i,k) = Σ_m (β·P(i,m))·V(m,k) in m order, D, and the 8- and 64-block maxima: the operations
+// of table_ev / table_D / bell_table_kernel on the same values, so the table is bit-identical.
+__device__ __forceinline__ void chain_table_tile(const BellArgs& A, int tile) {
+    const int lane = threadIdx.x & 63;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's v_new stores are complete
+    unsigned old = 0;
+    if (lane == 0)
+        old = __hip_atomic_fetch_add(A.tcnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old != (unsigned)(A.N - 1)) return;  // wave-uniform
+    if (lane == 0)  // re-armed for the next launch (every other wave of the tile has arrived)
+        __hip_atomic_store(A.tcnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int N = A.N, Na = A.Na;
+    const int k = tile * 64 + lane;
+    const bool ok = k < Na;
+    double vv[kChainMaxN];
+#pragma unroll
+    for (int m = 0; m < kChainMaxN; ++m)
+        vv[m] = (m < N && ok) ? __hip_atomic_load(A.v_new + (size_t)m * Na + k, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT)
+                              : 0.0;
+    for (int i = 0; i < N; ++i) {
+        double D = -__builtin_inf();
+        if (ok) {
+            const size_t t = (size_t)i * Na + k;
+            double acc = 0.0;
+#pragma unroll
+            for (int m = 0; m < kChainMaxN; ++m)
+                if (m < N) acc = acc + (A.beta * A.P[i * N + m]) * vv[m];
+            A.nEV[t] = acc;
+            D = table_D(acc, A.np);
+            A.nDt[t] = D;
+        }
+        double d8 = fmax(D, dpp_d<0xB1>(D));
+        d8 = fmax(d8, dpp_d<0x4E>(d8));
+        d8 = fmax(d8, dpp_d<0x104>(d8));
+        if (ok && (k & 7) == 0) A.nDm8[(size_t)i * A.nb8 + (k >> 3)] = d8;
+        D = fmax(D, dpp_d<0xB1>(D));
+        D = fmax(D, dpp_d<0x4E>(D));
+        D = fmax(D, dpp_d<0x141>(D));
+        D = fmax(D, dpp_d<0x140>(D));
+        D = fmax(D, dpp_d<0x142, 0xa>(D));
+        D = fmax(D, dpp_d<0x143, 0xc>(D));
+        D = readlane_d(D, 63);
+        if (lane == 0) A.nDm64[(size_t)i * A.nb + tile] = D;
+    }
+}
+
 // ------------------------------------------------------------------------------ 3'. tree
 // The default screened sweep.  One workgroup of W waves owns 64·R consecutive states of row i
 // and searches all their candidates (every labour level, the whole feasible prefix) through a
@@ -901,13 +992,14 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
     // and fine-screen software pipelines (two register sets each) are off and the screen
     // stages four chains at a time; the best exchange reuses each wave's idle s_cand slice
     constexpr bool LEAN = W >= 2 || LAB;  // (labour: keeps 3 waves per SIMD)
+    constexpr bool kChain = R == 1 && !LAB;  // chained sweeps (BellArgs::nEV; wave 0 of a tile)
 
     // loads that do not depend on the start-up below, issued first so that their latency
     // overlaps it: the level-0 bounds of the first 64 superblocks (first labour group) and v_old
     double dm0_pre, a0_pre;
     {
         const bool oks = lane < A.nb512;
-        dm0_pre = oks ? A.Dm512[(size_t)i * A.nb512 + lane] : -__builtin_inf();
+        dm0_pre = oks ? sb_bound(A, i, lane) : -__builtin_inf();
         a0_pre = oks ? a[lane << 9] : 0.0;
     }
     double vo_pre[R];
@@ -1376,7 +1468,7 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
         auto load512 = [&](int g) __attribute__((always_inline)) {
             const int sbl = g + lane;
             const bool oks = sbl < nsb;
-            dm0 = oks ? A.Dm512[(size_t)i * A.nb512 + sbl] : -__builtin_inf();
+            dm0 = oks ? sb_bound(A, i, sbl) : -__builtin_inf();
             a0 = oks ? a[sbl << 9] : 0.0;
         };
         if (l0 == 0) {  // prefetched (lanes past nsb are masked by the bound counts below)
@@ -1467,7 +1559,10 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
             if (A.pc) A.pc[t] = cash<LAB>(x[r], y, LAB ? A.L[l] : 1.0) - kp;
             if (LAB && A.pl) A.pl[t] = A.L[l];
         }
-        A.v_new[t] = b;
+        if (kChain && A.nEV)  // write-through: the tile's last arriver reads it (chain_table_tile)
+            __hip_atomic_store(A.v_new + t, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            A.v_new[t] = b;
         if (mom && A.hint)  // this sweep's shift of the argmax, for the next sweep's start
             mom[t] = (hk0[r] >= 0 && idx[r] >= 0) ? idx[r] / Nl - hk0[r] : 0;
         const double d = fabs(b - vo);
@@ -1477,6 +1572,12 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
         }
     }
     block_max_to_slots(okd, dmax, A.diff);
+    if constexpr (kChain) {
+        if (A.nEV && wave == 0) {  // chained sweeps: the slot ring (one wave), the next table's tile
+            if (block_id == 0) chain_slots(A);
+            chain_table_tile(A, tile);
+        }
+    }
     if (INS && A.trace) {  // instrumentation (aiy_ws_set_timing bit 2): per-wave sums into wave 0
         __shared__ unsigned s_cnt[W][4];
         __shared__ unsigned s_pairs;

@@ -213,6 +213,30 @@ static int bell_args(aiy_ws* ws, const BellCall& c, BellArgs& A, hipStream_t st)
     return AIY_OK;
 }
 
+// Chained sweeps need an A1 tree kernel with one state per lane (the instantiations that carry
+// the next-table epilogue, any number of waves per tile) and the VALU expectation it restates.
+static bool bell_chain_eligible(const BellArgs& A) {
+    return A.tree && !A.labor && A.np >= 1 && A.np <= 8 && A.C <= 1 && !A.ev_mfma &&
+           A.N <= kChainMaxN && (A.variant & (1 | 8 | 64 | 1024)) == 0;
+}
+static int ws_ensure_chain(aiy_ws* ws) {
+    const size_t n = (size_t)ws->N * ws->Na, nb = (size_t)ws->N * ((ws->Na + 63) / 64);
+    if (!ws->tcnt) {
+        AIY_TRY(dalloc(&ws->cEV, n));
+        AIY_TRY(dalloc(&ws->cDt, n));
+        AIY_TRY(dalloc(&ws->cDm8, (size_t)ws->N * ((ws->Na + 7) / 8)));
+        AIY_TRY(dalloc(&ws->cDm64, nb));
+        AIY_TRY(dalloc(&ws->zsets, 3 * 2 * (size_t)kDiffSlots));
+        AIY_TRY(dalloc(&ws->tcnt, (size_t)(ws->Na + 63) / 64));
+        AIY_HIP(hipMemset(ws->zsets, 0, 3 * 2 * kDiffSlots * sizeof(unsigned long long)));
+        AIY_HIP(hipMemset(ws->tcnt, 0, (ws->Na + 63) / 64 * sizeof(unsigned)));
+    }
+    return AIY_OK;
+}
+static unsigned long long* chain_set(aiy_ws* ws, int64_t g) {
+    return ws->zsets + (size_t)(((g % 3) + 3) % 3) * 2 * kDiffSlots;
+}
+
 int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
     BellArgs A;
     AIY_TRY(bell_args(ws, c, A, st));
@@ -220,7 +244,33 @@ int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
     // by the scan itself); otherwise the bound tree (or the chunked screen, variant bit 3)
     const bool exhaustive = c.mode == 2 || A.np == 0 || (A.variant & 1024);
     const bool screened = !exhaustive;
-    AIY_TRY(launch_bell_table(A, st));  // also clears the diff slots
+    // chained sweep g: table set g & 1 (set 0 = EV/Dt/Dm8 and the 64-block maxima in Dm), the
+    // next one built into set (g+1) & 1 by the tree kernel; diff slots from the ring of three
+    const bool chained = c.chain && screened && bell_chain_eligible(A);
+    const int64_t g = c.chain_g;
+    if (chained) {
+        AIY_TRY(ws_ensure_chain(ws));
+        double* EVs[2] = {ws->EV, ws->cEV};
+        double* Dts[2] = {ws->Dt, ws->cDt};
+        double* D8s[2] = {ws->Dm8, ws->cDm8};
+        double* D64s[2] = {ws->Dm, ws->cDm64};
+        const int cs = (int)(g & 1), ns = cs ^ 1;
+        A.EV = EVs[cs]; A.Dt = Dts[cs]; A.Dm8 = D8s[cs]; A.Dm64 = D64s[cs];
+        A.diff = chain_set(ws, g);
+        if (g == 0) {  // the chain's first table: the table kernel (clears set 0, folds nothing)
+            BellArgs T = A;
+            T.Dm = D64s[cs];
+            T.fold = nullptr;
+            AIY_TRY(launch_bell_table(T, st));
+        }
+        A.nEV = EVs[ns]; A.nDt = Dts[ns]; A.nDm8 = D8s[ns]; A.nDm64 = D64s[ns];
+        A.tcnt = ws->tcnt;
+        A.fsrc = (g > 0 && A.fold) ? chain_set(ws, g - 1) : nullptr;
+        if (!A.fsrc) A.fold = nullptr;
+        A.clr = chain_set(ws, g + 1);
+    } else {
+        AIY_TRY(launch_bell_table(A, st));  // also clears the diff slots
+    }
     if (!screened) A.coarse = 0, A.hint = nullptr;
     if (screened && A.tree) {
         // tree screen: the hint (or, cold, the init kernel's candidate) sets the first bar;
@@ -247,7 +297,7 @@ int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
         AIY_TRY(launch_bell_plain(A, st));
         AIY_TRY(ws_timing_end(ws, st));
     }
-    if (c.diff_out) AIY_TRY(launch_reduce_slots(ws->diff, c.diff_out, st));
+    if (c.diff_out) AIY_TRY(launch_reduce_slots(chained ? A.diff : ws->diff, c.diff_out, st));
     return AIY_OK;
 }
 
@@ -350,6 +400,9 @@ static int bell_solve_spec(aiy_ws* ws, BellCall c, double* v_a, double* v_b, dou
             // or by a reduce launch after the batch's last sweep
             c.prev_diff_out = t ? dslot(g - 1) : nullptr;
             c.diff_out = (t == m - 1) ? reinterpret_cast<double*>(dslot(g)) : nullptr;
+            // one chain per solve: sweep g reads vslot(g-1), the previous sweep's own output
+            c.chain = ws->chain;
+            c.chain_g = g - 1;
             AIY_TRY(bell_sweep_dev(ws, c, st));
         }
         unsigned long long* h = ws->spec_hdiff + (size_t)hb_next * 2 * D;
@@ -776,6 +829,36 @@ int aiy_vfi_sweep_dev(aiy_ws* ws, const double* v_old, const double* a_grid, con
     c.sigma = sigma; c.hint = hint; c.mode = mode; c.v_new = v_new; c.idx = idx;
     c.pk = policy_k; c.pc = policy_c; c.diff_out = diff;
     return bell_sweep_dev(ws, c, (hipStream_t)stream);
+}
+
+int aiy_vfi_sweeps_dev(aiy_ws* ws, double* v_a, double* v_b, const double* a_grid,
+                       const double* s, const double* P, double r, double w, double beta,
+                       double sigma, const int32_t* hint, int64_t nsweeps, int mode, int32_t* idx,
+                       double* policy_k, double* policy_c, double* diff, void* stream) {
+    if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
+    if (nsweeps < 1) return fail(AIY_BAD_ARG, "nsweeps >= 1");
+    if (!v_a || !v_b || v_a == v_b) return fail(AIY_BAD_ARG, "two distinct value buffers");
+    if (!idx) return fail(AIY_BAD_ARG, "NULL idx (the next sweep's hint)");
+    BellCall c{};
+    c.a = a_grid; c.s = s; c.P = P; c.r = r; c.w = w; c.beta = beta; c.sigma = sigma;
+    c.mode = mode; c.idx = idx; c.pk = policy_k; c.pc = policy_c;
+    for (int64_t g = 0; g < nsweeps; ++g) {  // sweep g + 1 of the plain loop: ping-pong v_a / v_b
+        c.v_old = (g & 1) ? v_b : v_a;
+        c.v_new = (g & 1) ? v_a : v_b;
+        c.hint = g ? idx : hint;
+        c.chain = ws->chain;
+        c.chain_g = g;
+        c.diff_out = (g == nsweeps - 1) ? diff : nullptr;
+        AIY_TRY(bell_sweep_dev(ws, c, (hipStream_t)stream));
+    }
+    return AIY_OK;
+}
+
+int aiy_ws_set_chain(aiy_ws* ws, int on) {
+    if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
+    if (on != 0 && on != 1) return fail(AIY_BAD_ARG, "chain must be 0 or 1");
+    ws->chain = on != 0;
+    return AIY_OK;
 }
 
 int aiy_vfi_solve_dev(aiy_ws* ws, double* v_a, double* v_b, const double* a_grid,

@@ -144,6 +144,25 @@ struct aiy_ws {
         hslots = nullptr;
         bC = 0;
     }
+    // chained sweeps (aiy_ws_set_chain, aiy_vfi_sweeps_dev and the speculative solve): the second
+    // table set (the tree kernel of sweep g reads set g & 1 and builds set (g+1) & 1), the 64-block
+    // maxima of set 0 live in Dm; per-tile arrival counters and a ring of three diff-slot sets,
+    // all zeroed at allocation (the kernels leave them zero / cleared ahead)
+    bool chain = true;
+    double* cEV = nullptr;
+    double* cDt = nullptr;
+    double* cDm8 = nullptr;
+    double* cDm64 = nullptr;
+    unsigned* tcnt = nullptr;
+    unsigned long long* zsets = nullptr;  // [3][2*kDiffSlots]
+    void free_chain() {
+        void* ps[] = {cEV, cDt, cDm8, cDm64, tcnt, zsets};
+        for (void* p : ps)
+            if (p) (void)hipFree(p);
+        cEV = cDt = cDm8 = cDm64 = nullptr;
+        tcnt = nullptr;
+        zsets = nullptr;
+    }
     // timing of the dominant kernel
     bool timing = false, count_hits = false;
     std::vector<hipEvent_t> ev_start, ev_stop;
@@ -169,6 +188,7 @@ struct aiy_ws {
         for (void* p : ps)
             if (p) (void)hipFree(p);
         free_spec();
+        free_chain();
         free_batch();
         free_egm_spec();
         free_dist_spec();
@@ -206,6 +226,11 @@ struct BellCall {
     double* pc = nullptr;
     double* diff_out = nullptr;
     void* prev_diff_out = nullptr;  // [2] u64: the previous sweep's folded {max bits, any}
+    // chained sweeps: sweep chain_g (0-based) of a chain on this workspace — sweep 0 builds its
+    // table with the table kernel, every later one reads the table the previous sweep's tree
+    // kernel built from its v_new, so v_old MUST be the previous chained sweep's v_new, unchanged
+    bool chain = false;
+    int64_t chain_g = 0;
 };
 int ws_ensure_bell(aiy_ws* ws, size_t partial_slots);
 int ws_timing_begin(aiy_ws* ws, hipStream_t st);

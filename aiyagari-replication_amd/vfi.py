@@ -119,6 +119,11 @@ class Workspace:
         slower); results do not depend on it, see aiy_ws_set_persistent."""
         check(lib().aiy_ws_set_persistent(self._h, ip(1 if on else 0)))
 
+    def set_chain(self, on: bool):
+        """Chained sweeps (the tree kernel builds the next sweep's table; default on) or one
+        table launch per sweep; results do not depend on it, see aiy_ws_set_chain."""
+        check(lib().aiy_ws_set_chain(self._h, ip(1 if on else 0)))
+
     def set_search(self, coarse_stride=0, k_chunk=1024):
         check(lib().aiy_ws_set_search(self._h, ip(coarse_stride), ip(k_chunk)))
 
@@ -129,6 +134,15 @@ class Workspace:
                                       d(w), d(beta), d(sigma), ptr(hint), ip(mode), ptr(v_new),
                                       ptr(idx), ptr(policy_k), ptr(policy_c), ptr(diff),
                                       stream_handle(stream)))
+
+    def vfi_sweeps(self, v_a, v_b, a_grid, s, P, r, w, beta, sigma, nsweeps, idx,
+                   policy_k=None, policy_c=None, hint=None, mode=0, diff=None, stream=None):
+        """nsweeps A1 sweeps on device, ping-pong from v_a (v_new ends in v_b when nsweeps is
+        odd); sweep 1's hint is `hint`, later sweeps use idx.  See aiy_vfi_sweeps_dev."""
+        check(lib().aiy_vfi_sweeps_dev(self._h, ptr(v_a), ptr(v_b), ptr(a_grid), ptr(s), ptr(P),
+                                       d(r), d(w), d(beta), d(sigma), ptr(hint), i64(nsweeps),
+                                       ip(mode), ptr(idx), ptr(policy_k), ptr(policy_c),
+                                       ptr(diff), stream_handle(stream)))
 
     def vfi_solve(self, v_a, v_b, a_grid, s, P, r, w, beta, sigma, tol, max_iter, idx,
                   policy_k=None, policy_c=None, mode=0, stream=None):

@@ -159,6 +159,9 @@ def main():
     ap.add_argument("--no-panel", action="store_true", help="skip the KS panel (F2/F3) leg")
     ap.add_argument("--ks-depth", type=int, default=None,
                     help="KS Howard sweeps per halo exchange (default 4 on >1 rank)")
+    ap.add_argument("--no-chain", action="store_true",
+                    help="one table launch per sweep (else the timed sweeps run as one chain: "
+                         "each tree launch builds the next sweep's table)")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the labour/EGM/batch legs (D4, D5 per-GPU)")
     args = ap.parse_args()
@@ -211,6 +214,22 @@ def main():
     snap = [x.clone() for x in (v[0], v[1], idx)]
     snap_cur = cur
 
+    if args.no_chain:
+        ws.set_chain(False)
+
+    def sweeps(n):
+        """n sweeps of the solve (hint = the previous argmax): one chain through
+        aiy_vfi_sweeps_dev — the first sweep's table by the table kernel, every later one built
+        by the previous sweep's tree launch — or, with --no-chain, n table + tree launch pairs."""
+        nonlocal cur
+        if args.no_chain or args.mode != 1:
+            for _ in range(n):
+                step()
+            return
+        ws.vfi_sweeps(v[cur], v[1 - cur], a_t, s_t, P_t, r, w, cal["beta"], cal["sigma"], n,
+                      idx, pk, pc, hint=idx, mode=args.mode)
+        cur ^= n & 1
+
     def restore():
         nonlocal cur
         v[0].copy_(snap[0]); v[1].copy_(snap[1]); idx.copy_(snap[2])
@@ -226,8 +245,7 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
+        sweeps(args.steps)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
