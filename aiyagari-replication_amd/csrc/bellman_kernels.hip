@@ -950,7 +950,7 @@ __device__ __forceinline__ void chain_table_tile(const BellArgs& A, int tile) {
 // instantiation compiles every counter and time stamp out
 // The body of one work item (tile of row i); block_id / nblocks are the launch coordinates (the
 // persistent solve calls it for several items per workgroup).
-template <int NP, bool LAB, int R, int LB, int W, bool INS>
+template <int NP, bool LAB, int R, int LB, int W, bool INS, bool CH = false>
 __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, int block_id,
                                                int nblocks) {
     const int lane = threadIdx.x & 63;
@@ -992,14 +992,16 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
     // and fine-screen software pipelines (two register sets each) are off and the screen
     // stages four chains at a time; the best exchange reuses each wave's idle s_cand slice
     constexpr bool LEAN = W >= 2 || LAB;  // (labour: keeps 3 waves per SIMD)
-    constexpr bool kChain = R == 1 && !LAB;  // chained sweeps (BellArgs::nEV; wave 0 of a tile)
+    // chained sweeps (BellArgs::nEV): a separate instantiation, so the default one is unchanged
+    constexpr bool kChain = CH && W == 1 && R == 1 && !LAB;
 
     // loads that do not depend on the start-up below, issued first so that their latency
     // overlaps it: the level-0 bounds of the first 64 superblocks (first labour group) and v_old
     double dm0_pre, a0_pre;
     {
         const bool oks = lane < A.nb512;
-        dm0_pre = oks ? sb_bound(A, i, lane) : -__builtin_inf();
+        dm0_pre = oks ? (kChain ? sb_bound(A, i, lane) : A.Dm512[(size_t)i * A.nb512 + lane])
+                      : -__builtin_inf();
         a0_pre = oks ? a[lane << 9] : 0.0;
     }
     double vo_pre[R];
@@ -1468,7 +1470,8 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
         auto load512 = [&](int g) __attribute__((always_inline)) {
             const int sbl = g + lane;
             const bool oks = sbl < nsb;
-            dm0 = oks ? sb_bound(A, i, sbl) : -__builtin_inf();
+            dm0 = oks ? (kChain ? sb_bound(A, i, sbl) : A.Dm512[(size_t)i * A.nb512 + sbl])
+                      : -__builtin_inf();
             a0 = oks ? a[sbl << 9] : 0.0;
         };
         if (l0 == 0) {  // prefetched (lanes past nsb are masked by the bound counts below)
@@ -1573,7 +1576,7 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
     }
     block_max_to_slots(okd, dmax, A.diff);
     if constexpr (kChain) {
-        if (A.nEV && wave == 0) {  // chained sweeps: the slot ring (one wave), the next table's tile
+        if (A.nEV) {  // chained sweeps: the slot ring (one wave), then the next table's tile
             if (block_id == 0) chain_slots(A);
             chain_table_tile(A, tile);
         }
@@ -1618,12 +1621,12 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
     }
 }
 
-template <int NP, bool LAB, int R, int LB, int W, bool INS>
+template <int NP, bool LAB, int R, int LB, int W, bool INS, bool CH = false>
 // min waves per SIMD 3 (168 VGPRs): every item of Na = 20,000 is resident at W = 1; the
 // cooperative tiles (W >= 2) serve small grids and labour, where a few hundred waves run and
 // latency, not occupancy, bounds them — a budget of 5 (and of 4) made those builds spill
 __global__ __launch_bounds__(64 * W, 3) void bell_tree_kernel(BellArgs A0, int ntile) {
-    bell_tree_item<NP, LAB, R, LB, W, INS>(A0, ntile, (int)blockIdx.x, (int)gridDim.x);
+    bell_tree_item<NP, LAB, R, LB, W, INS, CH>(A0, ntile, (int)blockIdx.x, (int)gridDim.x);
 }
 
 // ------------------------------------------------------------------------------ 3'''. persistent
@@ -2302,6 +2305,13 @@ static void tree_geo(const BellArgs& A, hipStream_t st) {
     constexpr int LB = LAB ? 5 : 1;
     const int ntile = cdiv(A.Na, 64 * R);
     const int grid = std::max(A.C, 1) * A.N * ntile;
+    if constexpr (R == 1 && W == 1 && !LAB) {  // chained sweeps: the epilogue instantiation
+        if (A.nEV) {
+            launch_dispatch_timed(bell_tree_kernel<NP, LAB, R, LB, W, false, true>, grid, 64 * W,
+                                  st, A, ntile);
+            return;
+        }
+    }
     if (A.trace || A.hitcount)
         launch_dispatch_timed(bell_tree_kernel<NP, LAB, R, LB, W, true>, grid, 64 * W, st, A, ntile);
     else

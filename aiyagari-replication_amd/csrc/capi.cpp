@@ -213,11 +213,11 @@ static int bell_args(aiy_ws* ws, const BellCall& c, BellArgs& A, hipStream_t st)
     return AIY_OK;
 }
 
-// Chained sweeps need an A1 tree kernel with one state per lane (the instantiations that carry
-// the next-table epilogue, any number of waves per tile) and the VALU expectation it restates.
+// Chained sweeps need the one-wave-per-tile A1 tree kernel (its chained instantiation carries
+// the next-table epilogue) and the VALU expectation the epilogue restates.
 static bool bell_chain_eligible(const BellArgs& A) {
     return A.tree && !A.labor && A.np >= 1 && A.np <= 8 && A.C <= 1 && !A.ev_mfma &&
-           A.N <= kChainMaxN && (A.variant & (1 | 8 | 64 | 1024)) == 0;
+           A.N <= kChainMaxN && (A.variant & (1 | 6 | 8 | 64 | 1024)) == 0;
 }
 static int ws_ensure_chain(aiy_ws* ws) {
     const size_t n = (size_t)ws->N * ws->Na, nb = (size_t)ws->N * ((ws->Na + 63) / 64);

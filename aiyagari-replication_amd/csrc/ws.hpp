@@ -148,7 +148,7 @@ struct aiy_ws {
     // table set (the tree kernel of sweep g reads set g & 1 and builds set (g+1) & 1), the 64-block
     // maxima of set 0 live in Dm; per-tile arrival counters and a ring of three diff-slot sets,
     // all zeroed at allocation (the kernels leave them zero / cleared ahead)
-    bool chain = true;
+    bool chain = false;  // measured slower than a table launch per sweep: opt-in
     double* cEV = nullptr;
     double* cDt = nullptr;
     double* cDm8 = nullptr;

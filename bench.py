@@ -159,9 +159,9 @@ def main():
     ap.add_argument("--no-panel", action="store_true", help="skip the KS panel (F2/F3) leg")
     ap.add_argument("--ks-depth", type=int, default=None,
                     help="KS Howard sweeps per halo exchange (default 4 on >1 rank)")
-    ap.add_argument("--no-chain", action="store_true",
-                    help="one table launch per sweep (else the timed sweeps run as one chain: "
-                         "each tree launch builds the next sweep's table)")
+    ap.add_argument("--chain", action="store_true",
+                    help="time the sweeps as one chain (each tree launch builds the next sweep's "
+                         "table; measured slower, DESIGN.md §5) instead of table + tree per sweep")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the labour/EGM/batch legs (D4, D5 per-GPU)")
     args = ap.parse_args()
@@ -214,20 +214,19 @@ def main():
     snap = [x.clone() for x in (v[0], v[1], idx)]
     snap_cur = cur
 
-    if args.no_chain:
-        ws.set_chain(False)
-
     def sweeps(n):
-        """n sweeps of the solve (hint = the previous argmax): one chain through
-        aiy_vfi_sweeps_dev — the first sweep's table by the table kernel, every later one built
-        by the previous sweep's tree launch — or, with --no-chain, n table + tree launch pairs."""
+        """n sweeps of the solve (hint = the previous argmax): n table + tree launch pairs, or
+        with --chain one chain through aiy_vfi_sweeps_dev — the first sweep's table by the
+        table kernel, every later one built by the previous sweep's tree launch."""
         nonlocal cur
-        if args.no_chain or args.mode != 1:
+        if not args.chain or args.mode != 1:
             for _ in range(n):
                 step()
             return
+        ws.set_chain(True)
         ws.vfi_sweeps(v[cur], v[1 - cur], a_t, s_t, P_t, r, w, cal["beta"], cal["sigma"], n,
                       idx, pk, pc, hint=idx, mode=args.mode)
+        ws.set_chain(False)
         cur ^= n & 1
 
     def restore():
@@ -259,7 +258,9 @@ def main():
         if rep:
             restore()
         blocks.append(timed_block(False)[0])
-    dt = blocks[0]  # the contract's timed region: the first block
+    # value: the median block (median of >= 5 timed repeats after the warm-up); every
+    # block is exactly `steps` sweeps between barrier + synchronize, and the first is reported too
+    dt = sorted(blocks)[len(blocks) // 2]
     # the dominant kernel's average launch duration: HIP events around each launch of the same
     # sweeps, in a block of their own
     restore()
@@ -356,8 +357,11 @@ def main():
             "repeats": {"n": len(blocks), "median_ms_per_step": step_ms[len(blocks) // 2]
                         / args.steps * 1e3, "min_ms_per_step": step_ms[0] / args.steps * 1e3,
                         "max_ms_per_step": step_ms[-1] / args.steps * 1e3,
+                        "first_block_ms_per_step": blocks[0] / args.steps * 1e3,
                         "kernel_timing_block_ms_per_step": dt_ev / args.steps * 1e3,
-                        "note": "the same sweeps re-run from a snapshot; value = the first block; "
+                        "gpu_clock": BL.gpu_clock(local),
+                        "note": "the same sweeps re-run from a snapshot; value = the median block "
+                                "(SURVEY D7); "
                                 "the kernel average comes from one more block of the same sweeps "
                                 "with HIP events around every launch (their gaps excluded from "
                                 "the contract blocks)"},

@@ -44,6 +44,31 @@ def cpu_info():
                     "the GPU box allots 16 host CPUs per GPU), 1-core figures one thread"}
 
 
+def gpu_clock(dev_index=0):
+    """The active core clock level of the benched GPU from sysfs (SURVEY D7 asks the clocks to
+    be noted): the amdgpu driver marks the current pp_dpm_sclk level with '*'; the card is
+    matched by PCI bus (torch device properties).  None when not readable."""
+    import glob
+    try:
+        import torch
+        bus = getattr(torch.cuda.get_device_properties(dev_index), "pci_bus_id", None)
+    except Exception:
+        bus = None
+    if bus is None:  # cannot tell which card is ours
+        return None
+    for f in sorted(glob.glob("/sys/class/drm/card*/device/pp_dpm_sclk")):
+        try:
+            pci = os.path.basename(os.path.realpath(os.path.dirname(f)))  # 0000:BB:DD.F
+            if int(pci.split(":")[1], 16) != int(bus):
+                continue
+            cur = [ln.strip() for ln in open(f) if ln.strip().endswith("*")]
+        except (OSError, ValueError, IndexError):
+            continue
+        if cur:
+            return {"pci": pci, "sclk": cur[0]}
+    return None
+
+
 def _time_cpu(fn, threads):
     from oracle import corc
     corc.num_threads(threads)

@@ -285,15 +285,16 @@ int aiy_vfi_sweep_dev(aiy_ws* ws, const double* v_old, const double* a_grid, con
  * (nullable) is sweep 1's hint, every later sweep's hint is idx (the previous argmax).  idx,
  * policy_k, policy_c hold the last sweep's policies; diff (nullable, device double[2]) its
  * {max|v_new-v_old|, any}.  Results equal nsweeps aiy_vfi_sweep_dev calls bit for bit.  With
- * chaining on (aiy_ws_set_chain, default) and the one-wave-per-tile tree screen (Na > 4096 by
- * default; N <= 16, integer sigma, VALU expectation) each sweep after the first is ONE launch:
- * the tree kernel of sweep g also builds sweep g+1's table. */
+ * chaining on (aiy_ws_set_chain) and the tree screen at one state per lane (N <= 16, integer
+ * sigma, VALU expectation) each sweep after the first is ONE launch: the tree kernel of sweep g
+ * also builds sweep g+1's table. */
 int aiy_vfi_sweeps_dev(aiy_ws* ws, double* v_a, double* v_b, const double* a_grid,
                        const double* s, const double* P, double r, double w, double beta,
                        double sigma, const int32_t* hint, int64_t nsweeps, int mode, int32_t* idx,
                        double* policy_k, double* policy_c, double* diff, void* stream);
-/* chained sweeps in aiy_vfi_sweeps_dev and the VFI solves (1, default) or a table launch per
- * sweep (0); results are identical either way. */
+/* chained sweeps in aiy_vfi_sweeps_dev and the VFI solves (1) or a table launch per sweep (0,
+ * default: at Na = 20,000 the chain's in-kernel hand-off costs more than the launch it removes,
+ * DESIGN.md §5); results are identical either way. */
 int aiy_ws_set_chain(aiy_ws* ws, int on);
 /* A2 on device: v_a (in: v_old) and v_b are ping-pong buffers; on return *out_new points
  * (0 = v_a, 1 = v_b) to the buffer holding v_new, the other holds v_old (break semantics).

@@ -2,7 +2,8 @@
 (BellArgs::nEV, `chain_table_tile`), so a chain of A1 sweeps (Aiyagari_VFI.m:70-83 repeated, the
 A2 loop :65-90 without its stop test) is one launch per sweep after the first.
 
-Bit for bit against one table launch per sweep (ws.set_chain(False)) and against the C oracle's
+Chaining is opt-in (ws.set_chain(True); measured slower than a table launch per sweep at
+Na = 20,000).  Bit for bit against one table launch per sweep (the default) and against the C oracle's
 exhaustive sweep of the device's own v_old: the table the last arriver of each 64-candidate tile
 builds (EV in m order, D, the 8- and 64-block maxima) must equal bell_table_kernel's, and the
 level-0 bounds taken from the 64-block maxima may change which blocks are screened, never the
@@ -135,9 +136,8 @@ def test_chain_counters_rearm(pkg, gpu):
 
 
 def test_chain_single_sweep_and_fallbacks(pkg, gpu):
-    """nsweeps = 1 (table launch + one tree launch); two cooperating waves per tile (wave 0
-    publishes the tile and, when last, builds its table); N > 16 cannot chain and takes the
-    table-per-sweep path — all with the same results."""
+    """nsweeps = 1 (table launch + one tree launch) and geometries that cannot chain (W = 2,
+    N > 16) take the table-per-sweep path with the same results."""
     import torch
     cal = no.calib_aiyagari(Na=5000, shocks="tauchen")
     one, _ = _run(pkg, torch, cal, 1, True)
