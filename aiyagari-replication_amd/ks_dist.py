@@ -25,17 +25,20 @@ import numpy as np
 from ._capi import check, i64, lib, ptr, stream_handle, vp
 
 
-def shard_range(nK: int, rank: int, world: int):
+def shard_range(nK: int, rank: int, world: int, bounds=None):
+    if bounds is not None:
+        return int(bounds[rank]), int(bounds[rank + 1])
     return nK * rank // world, nK * (rank + 1) // world
 
 
-def shard_slices(nK: int, rank: int, world: int):
+def shard_slices(nK: int, rank: int, world: int, bounds=None):
     """(K0, K1, s0, s1): the rank's shard, K in [K0, K1) of the s blocks [s0, s1).  Up to nK
-    ranks split the K range (all four s each); up to 2·nK ranks split the (K, Z) slices —
-    s = 0, 1 share one aggregate state z, s = 2, 3 the other — half the ranks per z, each half
-    splitting the K range (the reference's K = 4 grid then uses 8 ranks)."""
+    ranks split the K range (all four s each) — evenly, or at `bounds` (world + 1 increasing
+    K boundaries from 0 to nK, e.g. `balanced_bounds`); up to 2·nK ranks split the (K, Z)
+    slices — s = 0, 1 share one aggregate state z, s = 2, 3 the other — half the ranks per z,
+    each half splitting the K range evenly (the reference's K = 4 grid then uses 8 ranks)."""
     if world <= nK:
-        K0, K1 = shard_range(nK, rank, world)
+        K0, K1 = shard_range(nK, rank, world, bounds)
         return K0, K1, 0, 4
     if world > 2 * nK:
         raise ValueError(f"{world} ranks exceed the 2·K_size = {2 * nK} (K, Z) slices")
@@ -47,9 +50,9 @@ def shard_slices(nK: int, rank: int, world: int):
     return K0, K1, 2, 4
 
 
-def owned_columns(nK: int, rank: int, world: int):
+def owned_columns(nK: int, rank: int, world: int, bounds=None):
     """Flat value columns c = s·nK + K (rows of V viewed as (4·nK, k)) the rank owns."""
-    K0, K1, s0, s1 = shard_slices(nK, rank, world)
+    K0, K1, s0, s1 = shard_slices(nK, rank, world, bounds)
     return [s * nK + K for s in range(s0, s1) for K in range(K0, K1)]
 
 
@@ -64,12 +67,12 @@ def forecast_index(K_grid, B, params):
     return out.reshape(4, Kg.size)
 
 
-def _need_plan(need, nK: int, world: int):
+def _need_plan(need, nK: int, world: int, bounds=None):
     """plan[q][p] = sorted flat columns of need[q] that rank p owns (p != q; [] on the
     diagonal)."""
     owner = np.empty(4 * nK, np.int64)
     for q in range(world):
-        owner[owned_columns(nK, q, world)] = q
+        owner[owned_columns(nK, q, world, bounds)] = q
     plan = [[[] for _ in range(world)] for _ in range(world)]
     for q in range(world):
         for c in sorted(set(int(c) for c in need[q])):
@@ -78,17 +81,17 @@ def _need_plan(need, nK: int, world: int):
     return plan
 
 
-def halo_plan(kp_idx, nK: int, world: int):
+def halo_plan(kp_idx, nK: int, world: int, bounds=None):
     """plan[q][p] = sorted flat columns (s'·nK + K') rank q reads that rank p owns (p != q;
     [] on the diagonal): for every node q owns, the forecast column K'_idx(s, K) of all four
     s' (Krusell_Smith_VFI.m:343-349)."""
     kp = np.asarray(kp_idx)
     need = []
     for q in range(world):
-        K0, K1, s0, s1 = shard_slices(nK, q, world)
+        K0, K1, s0, s1 = shard_slices(nK, q, world, bounds)
         targets = np.unique(kp[s0:s1, K0:K1])
         need.append([sn * nK + int(t) for t in targets for sn in range(4)])
-    return _need_plan(need, nK, world)
+    return _need_plan(need, nK, world, bounds)
 
 
 def ghost_rects(kp_idx, nK: int, K0: int, K1: int, s0: int, s1: int, depth: int):
@@ -111,12 +114,56 @@ def rect_columns(rect, nK: int):
     return [s * nK + K for s in range(sa, sb) for K in range(Ka, Kb)]
 
 
-def ghost_plan(kp_idx, nK: int, world: int, depth: int):
+def ghost_plan(kp_idx, nK: int, world: int, depth: int, bounds=None):
     """Exchange plan for a block of `depth` sweeps: rank q receives every column of its
     R_depth (ghost_rects) that another rank owns."""
-    need = [rect_columns(ghost_rects(kp_idx, nK, *shard_slices(nK, q, world), depth)[depth], nK)
-            for q in range(world)]
-    return _need_plan(need, nK, world)
+    need = [rect_columns(ghost_rects(kp_idx, nK, *shard_slices(nK, q, world, bounds), depth)[depth],
+                         nK) for q in range(world)]
+    return _need_plan(need, nK, world, bounds)
+
+
+def ghost_cost(kp_idx, nK: int, K0: int, K1: int, depth: int, w_slopes: float = 0.4):
+    """Column-sweeps of one block of `depth` sweeps on the K range [K0, K1) (all four s): the
+    fused Howard sweeps on R_{depth-1} .. R_0 plus the block's slopes launch over R_{depth-1},
+    weighted by `w_slopes` (a slopes column costs ~0.4 of a sweep column on gfx950:
+    DESIGN.md §6, 13.3 µs for 14 columns vs 32.5 µs for 12.5)."""
+    rects = ghost_rects(kp_idx, nK, K0, K1, 0, 4, depth)
+    w = [b - a for a, b, _, _ in rects[:depth]]
+    return sum(w) + w_slopes * w[-1]
+
+
+def balanced_bounds(kp_idx, nK: int, world: int, depth: int, w_slopes: float = 0.4):
+    """K boundaries [0 = b_0 < b_1 < ... < b_world = nK] of contiguous K ranges that minimise
+    the largest `ghost_cost` over the ranks (exact DP over the split points).  With the
+    near-identity ALM the ghost rectangles of the top ranks grow up to three K points per level
+    (the forecast moves further there), so even splits leave those ranks 30 % more work;
+    balanced ranges give them fewer own columns.  Any partition gives bit-identical results."""
+    if world > nK:
+        raise ValueError("balanced_bounds splits the K range: world <= K_size")
+    cost = {}
+
+    def c(a, b):
+        if (a, b) not in cost:
+            cost[(a, b)] = ghost_cost(kp_idx, nK, a, b, depth, w_slopes)
+        return cost[(a, b)]
+
+    INF = float("inf")
+    # best[p][b]: smallest max cost splitting [0, b) into p ranges; arg for the split point
+    best = [[INF] * (nK + 1) for _ in range(world + 1)]
+    arg = [[0] * (nK + 1) for _ in range(world + 1)]
+    best[0][0] = 0.0
+    for p in range(1, world + 1):
+        for b in range(p, nK - (world - p) + 1):
+            for a in range(p - 1, b):
+                if best[p - 1][a] == INF:
+                    continue
+                m = max(best[p - 1][a], c(a, b))
+                if m < best[p][b] - 1e-12:
+                    best[p][b], arg[p][b] = m, a
+    bounds = [nK]
+    for p in range(world, 0, -1):
+        bounds.append(arg[p][bounds[-1]])
+    return bounds[::-1]
 
 
 def _runs(cols):
@@ -237,12 +284,12 @@ class HipShard:
         return float(o[0:1].view(torch.float64)[0]) if int(o[1]) != 0 else math.nan
 
 
-def _exchange(V, rank, world, nK):
+def _exchange(V, rank, world, nK, bounds=None):
     """All-gather every rank's owned columns of V (rows of the (4·nK, k) view) into every
     rank's V, in place."""
     import torch
     import torch.distributed as dist
-    cols = [owned_columns(nK, q, world) for q in range(world)]
+    cols = [owned_columns(nK, q, world, bounds) for q in range(world)]
     m = max(len(c) for c in cols)
     flat = V.view(-1, V.shape[-1])
     mine = torch.zeros((m, flat.shape[1]), dtype=V.dtype, device=V.device)
@@ -284,8 +331,9 @@ class HowardSweeps:
     is exchanged, so the state between calls is the depth-1 schedule's.
     exchange = "allgather": every rank's owned slice to every rank after every sweep."""
 
-    def __init__(self, shard, nK, rank, world, V, depth=1, exchange="halo"):
+    def __init__(self, shard, nK, rank, world, V, depth=1, exchange="halo", bounds=None):
         self.shard, self.nK, self.rank, self.world = shard, nK, rank, world
+        self.bounds = bounds
         self.depth = max(1, int(depth)) if (world > 1 and exchange == "halo") else 1
         self.exchange = exchange
         self.halo = None
@@ -298,24 +346,24 @@ class HowardSweeps:
         self.nk = nk
         if world > 1:
             if exchange == "halo":
-                self.plan = halo_plan(shard.kp_idx, nK, world)
+                self.plan = halo_plan(shard.kp_idx, nK, world, bounds)
                 self.halo = HaloExchange(self.plan, rank, world, V.device, nk, V.dtype)
                 if self.depth > 1:
                     self.rects = ghost_rects(shard.kp_idx, nK, *self.rects[0], self.depth)
                     self.shards += [shard.ghost(*r) for r in self.rects[1:self.depth]]
                     for L in range(1, self.depth + 1):
-                        self.blocks[L] = HaloExchange(ghost_plan(shard.kp_idx, nK, world, L),
+                        self.blocks[L] = HaloExchange(ghost_plan(shard.kp_idx, nK, world, L, bounds),
                                                       rank, world, V.device, nk, V.dtype)
                     self.kx = self.blocks[self.depth - 1]   # k_opt on R_{m-1}
             elif exchange != "allgather":
                 raise ValueError(f"exchange must be 'halo' or 'allgather', not {exchange!r}")
         if exchange == "allgather" or world == 1:
             import torch
-            self.own = torch.tensor(owned_columns(nK, rank, world), device=V.device)
+            self.own = torch.tensor(owned_columns(nK, rank, world, bounds), device=V.device)
 
     def read_columns(self):
         """Every column this rank ever reads or sweeps (own, halo and ghost columns)."""
-        cols = set(owned_columns(self.nK, self.rank, self.world))
+        cols = set(owned_columns(self.nK, self.rank, self.world, self.bounds))
         if self.halo is not None:
             cols |= {c for p in range(self.world) for c in self.plan[self.rank][p]}
         if self.depth > 1:
@@ -324,7 +372,7 @@ class HowardSweeps:
 
     def kopt_columns(self):
         """Every column of k_opt this rank's sweeps read."""
-        cols = set(owned_columns(self.nK, self.rank, self.world))
+        cols = set(owned_columns(self.nK, self.rank, self.world, self.bounds))
         if self.depth > 1:
             cols |= set(rect_columns(self.rects[self.depth - 1], self.nK))
         return cols
@@ -370,7 +418,7 @@ class HowardSweeps:
                 if self.halo is not None:
                     self.halo(V)
                 elif self.world > 1:
-                    _exchange(V, self.rank, self.world, self.nK)
+                    _exchange(V, self.rank, self.world, self.nK, self.bounds)
             return V, V2
         done = 0
         dV, dV2 = self._slope_bufs(V)
@@ -397,12 +445,13 @@ class HowardSweeps:
 
 
 def ks_vfi_solve_dist(value, k_opt, shard, nK, howard_steps=50, tol=1e-6, max_vfi=10000,
-                      rank=0, world=1, exchange="halo", poison=False, depth=1):
+                      rank=0, world=1, exchange="halo", poison=False, depth=1, bounds=None):
     """Krusell_Smith_VFI.m:141-204 for the current B.  value, k_opt: (4, K, k) tensors on this
     rank's device, full arrays on every rank (in/out).  `shard` owns [K0, K1) of [s0, s1)
     (HipShard, or any object with the same improve / howard / reldiff / ghost / hints methods
     and a kp_idx table).  exchange: "halo" (point-to-point, only the columns read; `depth`
-    sweeps per exchange, HowardSweeps) or "allgather".  poison (tests): NaN every column this
+    sweeps per exchange, HowardSweeps) or "allgather".  bounds: the K partition the shards were
+    made with (`shard_slices(..., bounds)`; None = even ranges).  poison (tests): NaN every column this
     rank neither owns nor reads, proving the exchanges are sufficient.
     Returns (iters, rel_diff)."""
     import torch
@@ -411,7 +460,7 @@ def ks_vfi_solve_dist(value, k_opt, shard, nK, howard_steps=50, tol=1e-6, max_vf
     nk = V.shape[-1]
     if world > 1:
         dist.barrier()   # first collective on every rank before any point-to-point
-    hs = HowardSweeps(shard, nK, rank, world, V, depth=depth, exchange=exchange)
+    hs = HowardSweeps(shard, nK, rank, world, V, depth=depth, exchange=exchange, bounds=bounds)
     if poison and world > 1 and exchange == "halo":
         keep = hs.read_columns()
         flat = V.view(-1, nk)
@@ -437,9 +486,9 @@ def ks_vfi_solve_dist(value, k_opt, shard, nK, howard_steps=50, tol=1e-6, max_vf
     finally:
         hs.close()
     if world > 1:                                          # every rank leaves with all of both
-        _exchange(k_opt, rank, world, nK)
+        _exchange(k_opt, rank, world, nK, bounds)
         if exchange == "halo":
-            _exchange(V, rank, world, nK)
+            _exchange(V, rank, world, nK, bounds)
     if V is not value:
         value.copy_(V)
     return it, rel

@@ -24,11 +24,12 @@ sys.path.insert(0, str(ROOT))
 
 
 def ks_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, exchange="halo", reps=3,
-           depth=None):
+           depth=None, balanced=True):
     """Time one VFI iteration of the sharded solve (policy improvement + `howard` Jacobi
     sweeps with their exchanges, Krusell_Smith_VFI.m:148-192) at k = nk, K = nK, S = 4, max
     over ranks, median of `reps`.  depth: Howard sweeps per exchange (ks_dist.HowardSweeps;
-    default 4 on more than one rank).  Every rank must call it (collectives inside)."""
+    default 4 on more than one rank); balanced: K ranges cut at ks_dist.balanced_bounds (equal
+    ghost-block cost per rank) when depth > 1.  Every rank must call it (collectives inside)."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -37,14 +38,17 @@ def ks_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, exchange="halo", r
         depth = 4 if world > 1 else 1
     kg, Kg, P, V0 = pkg.calibration.krusell_smith(k_size=nk, K_size=nK)
     B = np.array([0.1, 0.97, 0.08, 0.975])
-    K0, K1, s0, s1 = kd.shard_slices(nK, rank, world)
+    bounds = None
+    if balanced and 1 < world <= nK and depth > 1 and exchange == "halo":
+        bounds = kd.balanced_bounds(kd.forecast_index(Kg, B, pkg.ks_params()), nK, world, depth)
+    K0, K1, s0, s1 = kd.shard_slices(nK, rank, world, bounds)
     sh = kd.HipShard(kg, Kg, B, P, pkg.ks_params(), K0, K1, s0, s1)
     V = torch.as_tensor(np.ascontiguousarray(V0.transpose(2, 1, 0)), device=dev)
     V2 = V.clone()
     ko = torch.ones_like(V)
     if world > 1:
         dist.barrier()
-    hs = kd.HowardSweeps(sh, nK, rank, world, V, depth=depth, exchange=exchange)
+    hs = kd.HowardSweeps(sh, nK, rank, world, V, depth=depth, exchange=exchange, bounds=bounds)
 
     def sync():
         torch.cuda.synchronize()
@@ -97,7 +101,7 @@ def ks_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, exchange="halo", r
                         f"configs[4] scaling size), ALM B={[float(b) for b in B]}, one VFI "
                         f"iteration = improvement + {howard} Howard sweeps, median of {reps}",
             "parallelism": f"(K, Z) shards over {world} ranks (rank 0: K [{K0}, {K1}), s "
-                           f"[{s0}, {s1})), {exchange} exchange "
+                           f"[{s0}, {s1}); K bounds {bounds or 'even'}), {exchange} exchange "
                            + (f"every {hs.depth} Howard sweeps (ghost rectangles of rank 0: "
                               f"{ghost} columns; {gcols} columns received per block)"
                               if hs.depth > 1 else
@@ -128,57 +132,70 @@ def ghost_model(pkg, dev, world=8, nk=32768, nK=64, depths=(1, 2, 3, 4, 6, 8), s
     blocks of `depth` (one slopes launch over what R_{L-1} reads, then one fused Howard+slopes
     launch per sweep over the ghost rectangles R_{L-1} .. R_0, ks_dist.HowardSweeps) without the
     exchanges — what each rank's GPU does between exchanges at N = world.  Returns, per depth,
-    the slowest emulated rank's ms per sweep."""
+    the slowest emulated rank's ms per sweep, for even K ranges and for the ranges of
+    ks_dist.balanced_bounds (equal ghost-block cost per rank; what ks_leg uses at depth > 1)."""
     import numpy as np
     import torch
     kd = pkg.ks_dist
     kg, Kg, P, V0 = pkg.calibration.krusell_smith(k_size=nk, K_size=nK)
     B = np.array([0.1, 0.97, 0.08, 0.975])
+    kp = kd.forecast_index(Kg, B, pkg.ks_params())
     V = torch.as_tensor(np.ascontiguousarray(V0.transpose(2, 1, 0)), device=dev)
     V2 = V.clone()
     dV, dV2 = torch.empty_like(V), torch.empty_like(V)
     ko = torch.ones_like(V)
-    out, gout = {}, {}
-    for rank in range(world):
-        K0, K1, s0, s1 = kd.shard_slices(nK, rank, world)
-        sh = kd.HipShard(kg, Kg, B, P, pkg.ks_params(), K0, K1, s0, s1)
-        sh.improve(V, ko)
+    res = {}
+    for part in ("even", "balanced"):
+        out, gout, per_rank, bnds = {}, {}, {}, {}
         for d in depths:
-            rects = kd.ghost_rects(sh.kp_idx, nK, K0, K1, s0, s1, d)
-            shards = [sh] + [sh.ghost(*r) for r in rects[1:d]]
-            shards[-1].hints(ko)
+            bounds = kd.balanced_bounds(kp, nK, world, d) if part == "balanced" else None
+            bnds[str(d)] = bounds or [nK * r // world for r in range(world + 1)]
+            per_rank[str(d)] = []
+            for rank in range(world):
+                K0, K1, s0, s1 = kd.shard_slices(nK, rank, world, bounds)
+                sh = kd.HipShard(kg, Kg, B, P, pkg.ks_params(), K0, K1, s0, s1)
+                sh.improve(V, ko)
+                rects = kd.ghost_rects(sh.kp_idx, nK, K0, K1, s0, s1, d)
+                shards = [sh] + [sh.ghost(*r) for r in rects[1:d]]
+                shards[-1].hints(ko)
 
-            def run(n):  # ks_dist.HowardSweeps' fused block schedule without the exchanges
-                nonlocal V, V2, dV, dV2
-                done = 0
-                while done < n:
-                    L = min(d, n - done)
-                    shards[L - 1].slopes(V, dV)
-                    for i in range(1, L + 1):
-                        shards[L - i].howard_fused(V, dV, ko, V2, dV2)
-                        V, V2 = V2, V
-                        dV, dV2 = dV2, dV
-                    done += L
-            run(d)
-            torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            t0 = time.perf_counter()
-            e0.record()
-            run(sweeps)
-            e1.record()
-            torch.cuda.synchronize()
-            ms = (time.perf_counter() - t0) / sweeps * 1e3
-            gms = e0.elapsed_time(e1) / sweeps
-            out[d] = max(out.get(d, 0.0), ms)
-            gout[d] = max(gout.get(d, 0.0), gms)
-            for g in shards[1:]:
-                g.close()
-            sh._ghosts.clear()
-        sh.close()
+                def run(n):  # ks_dist.HowardSweeps' fused block schedule without the exchanges
+                    nonlocal V, V2, dV, dV2
+                    done = 0
+                    while done < n:
+                        L = min(d, n - done)
+                        shards[L - 1].slopes(V, dV)
+                        for i in range(1, L + 1):
+                            shards[L - i].howard_fused(V, dV, ko, V2, dV2)
+                            V, V2 = V2, V
+                            dV, dV2 = dV2, dV
+                        done += L
+                run(d)
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                t0 = time.perf_counter()
+                e0.record()
+                run(sweeps)
+                e1.record()
+                torch.cuda.synchronize()
+                ms = (time.perf_counter() - t0) / sweeps * 1e3
+                gms = e0.elapsed_time(e1) / sweeps
+                out[d] = max(out.get(d, 0.0), ms)
+                gout[d] = max(gout.get(d, 0.0), gms)
+                per_rank[str(d)].append(gms)
+                for g in shards[1:]:
+                    g.close()
+                sh._ghosts.clear()
+                sh.close()
+        res[part] = {"ms_per_sweep_by_depth": {str(d): out[d] for d in depths},
+                     "gpu_ms_per_sweep_by_depth": {str(d): gout[d] for d in depths},
+                     "gpu_ms_per_sweep_by_rank": per_rank, "K_bounds": bnds}
     return {"world": world, "sweeps": sweeps,
-            "ms_per_sweep_by_depth": {str(d): out[d] for d in depths},
-            "gpu_ms_per_sweep_by_depth": {str(d): gout[d] for d in depths},
+            "ms_per_sweep_by_depth": res["even"]["ms_per_sweep_by_depth"],
+            "gpu_ms_per_sweep_by_depth": res["even"]["gpu_ms_per_sweep_by_depth"],
+            "even": res["even"], "balanced": res["balanced"],
             "note": "slowest emulated rank, compute only (no exchanges): ghost overhead vs depth; "
+                    "top level = even K ranges (as in round 2), `balanced` = balanced_bounds; "
                     "ms_per_sweep = host wall clock (Python issue included), gpu_ms_per_sweep = "
                     "HIP events on the stream (tools/ks_ghost_probe.py gives the per-kernel split)"}
 

@@ -86,7 +86,8 @@ def _setup(nK=4, B_alm=None):
     return cp, kg, Kg, P, V0, B
 
 
-def _worker(rank, world, port, outdir, nK, exchange="halo", depth=1, howard=3, B_alm=None):
+def _worker(rank, world, port, outdir, nK, exchange="halo", depth=1, howard=3, B_alm=None,
+            balanced=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     from oracle import corc
     corc.num_threads(1)
@@ -95,16 +96,18 @@ def _worker(rank, world, port, outdir, nK, exchange="halo", depth=1, howard=3, B
     dist.init_process_group("gloo", rank=rank, world_size=world)
     kd = _pkg().ks_dist
     cp, kg, Kg, P, V0, B = _setup(nK, B_alm)
-    K0, K1, s0, s1 = kd.shard_slices(len(Kg), rank, world)
+    kp = kd.forecast_index(Kg, B, _pkg().ks_params())  # host-only C ABI call
+    bounds = kd.balanced_bounds(kp, len(Kg), world, depth) if balanced else None
+    K0, K1, s0, s1 = kd.shard_slices(len(Kg), rank, world, bounds)
     V = torch.from_numpy(np.ascontiguousarray(V0.transpose(2, 1, 0)))
     ko = torch.ones_like(V)
     sh = OracleShard(cp, kg, Kg, B, P, K0, K1, s0, s1)
-    sh.kp_idx = kd.forecast_index(Kg, B, _pkg().ks_params())  # host-only C ABI call
+    sh.kp_idx = kp
     if depth > 1 or B_alm is not None:  # the test's geometry must need remote columns
-        assert any(c for row in kd.halo_plan(sh.kp_idx, len(Kg), world) for c in row)
+        assert any(c for row in kd.halo_plan(sh.kp_idx, len(Kg), world, bounds) for c in row)
     it, rel = kd.ks_vfi_solve_dist(V, ko, sh, len(Kg), howard_steps=howard, tol=1e-6,
                                    max_vfi=6, rank=rank, world=world, exchange=exchange,
-                                   poison=(exchange == "halo"), depth=depth)
+                                   poison=(exchange == "halo"), depth=depth, bounds=bounds)
     np.save(Path(outdir, f"V{rank}.npy"), V.numpy())
     np.save(Path(outdir, f"k{rank}.npy"), ko.numpy())
     Path(outdir, f"m{rank}.json").write_text(json.dumps(dict(it=it, rel=rel)))
@@ -132,21 +135,22 @@ def test_gloo_sharded_equals_unsharded(tmp_path, world, nK, exchange):
         assert m["it"] == R["iters"]
 
 
-@pytest.mark.parametrize("world,nK,depth,howard", [(2, 8, 1, 3), (3, 12, 1, 3), (2, 8, 2, 3),
-                                                   (3, 12, 3, 7), (4, 12, 4, 5), (5, 12, 2, 5),
-                                                   (2, 6, 6, 4), (8, 6, 3, 4)])
-def test_gloo_ghost_sweeps_equal_unsharded(tmp_path, world, nK, depth, howard):
+@pytest.mark.parametrize("world,nK,depth,howard,balanced", [
+    (2, 8, 1, 3, False), (3, 12, 1, 3, False), (2, 8, 2, 3, False), (3, 12, 3, 7, False),
+    (4, 12, 4, 5, False), (5, 12, 2, 5, False), (2, 6, 6, 4, False), (8, 6, 3, 4, False),
+    (4, 16, 4, 5, True), (3, 12, 2, 5, True)])
+def test_gloo_ghost_sweeps_equal_unsharded(tmp_path, world, nK, depth, howard, balanced):
     """Communication-avoiding Howard (HowardSweeps depth > 1: one exchange per block of `depth`
     sweeps, ghost rectangles swept redundantly) — bit-identical to the unsharded solve, with
     every value column outside own ∪ R_depth and every k_opt column outside own ∪ R_{depth-1}
     NaN-poisoned.  Blocks that do not divide the sweep count (7 = 3 + 3 + 1) and depth larger
     than the sweep count are included; (8, 6) uses (K, Z) slices; depth 1 is the per-sweep halo on
-    the same geometry."""
+    the same geometry; `balanced` cuts the K range at `balanced_bounds` instead of evenly."""
     import torch.multiprocessing as mp
     from oracle import corc
-    port = 31200 + (os.getpid() % 1500) + 11 * world + 3 * nK + depth
-    mp.spawn(_worker, args=(world, port, str(tmp_path), nK, "halo", depth, howard, B_MIXED),
-             nprocs=world, join=True)
+    port = 31200 + (os.getpid() % 1500) + 11 * world + 3 * nK + depth + 5 * balanced
+    mp.spawn(_worker, args=(world, port, str(tmp_path), nK, "halo", depth, howard, B_MIXED,
+                            balanced), nprocs=world, join=True)
     cp, kg, Kg, P, V0, B = _setup(nK, B_MIXED)
     R = corc.ks_vfi_solve(cp, kg, Kg, V0, np.ones_like(V0), B, P, howard=howard, tol=1e-6,
                           max_vfi=6)
@@ -156,6 +160,30 @@ def test_gloo_ghost_sweeps_equal_unsharded(tmp_path, world, nK, depth, howard):
         assert np.array_equal(np.load(Path(tmp_path, f"V{rank}.npy")), Vr)
         assert np.array_equal(np.load(Path(tmp_path, f"k{rank}.npy")), kr)
         assert json.loads(Path(tmp_path, f"m{rank}.json").read_text())["it"] == R["iters"]
+
+
+def test_balanced_bounds_scaling_grid():
+    """balanced_bounds (exact DP over split points) at the scaling grid's forecast map: a
+    partition of [0, 64) into 8 non-empty ranges whose largest ghost cost is no larger than the
+    even split's — and no other contiguous split does better (checked against every split
+    that moves one boundary by one)."""
+    kd = _pkg().ks_dist
+    from oracle import np_oracle as no
+    p, kg, Kg, P, V0, B = no.ks_setup(k_size=8, K_size=64)
+    kp = kd.forecast_index(Kg, np.array([0.1, 0.97, 0.08, 0.975]), _pkg().ks_params())
+    for depth in (2, 4):
+        b = kd.balanced_bounds(kp, 64, 8, depth)
+        assert b[0] == 0 and b[-1] == 64 and all(x < y for x, y in zip(b, b[1:]))
+        cost = lambda bb: max(kd.ghost_cost(kp, 64, bb[r], bb[r + 1], depth) for r in range(8))
+        even = [64 * r // 8 for r in range(9)]
+        assert cost(b) <= cost(even)
+        for r in range(1, 8):
+            for d in (-1, 1):
+                bb = list(b)
+                bb[r] += d
+                if bb[r - 1] < bb[r] < bb[r + 1]:
+                    assert cost(b) <= cost(bb)
+    assert kd.shard_slices(64, 3, 8, b) == (b[3], b[4], 0, 4)
 
 
 def test_ghost_rects_cover_reads():
