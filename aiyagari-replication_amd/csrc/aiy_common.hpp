@@ -39,6 +39,14 @@ __device__ __forceinline__ int xcd_remap(int b, int G) {
     const int q = G / 8, r = G % 8, x = b % 8, slot = b / 8;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + slot;
 }
+// the same XCD ranges, each dealt in reverse (the last-dispatched workgroups of an XCD — the
+// third waves on its SIMDs — take the first items of its range)
+__device__ __forceinline__ int xcd_remap_rev(int b, int G) {
+    const int q = G / 8, r = G % 8, x = b % 8, slot = b / 8;
+    const int start = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+    const int size = x < r ? q + 1 : q;
+    return start + (size - 1 - slot);
+}
 __device__ __forceinline__ int readlane_i(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
 // lane l's double (l wave-uniform) as a wave-uniform value: two v_readlane_b32, no memory
 __device__ __forceinline__ double readlane_d(double x, int l) {

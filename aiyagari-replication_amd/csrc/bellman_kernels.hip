@@ -962,7 +962,9 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
                  "s"(A0.variant), "s"(A0.C), "s"(A0.nb512), "s"(A0.sigma), "s"(A0.trace));
     const long long t_boot = (INS && A0.trace) ? (long long)wall_clock64() : 0;  // (instrumentation)
     const long long c_boot = (INS && A0.trace) ? (long long)__builtin_amdgcn_s_memtime() : 0;
-    int item = (A0.variant & 16) ? xcd_remap(block_id, nblocks) : block_id;
+    int item = (A0.variant & 16) ? ((A0.variant & 131072) ? xcd_remap_rev(block_id, nblocks)
+                                                          : xcd_remap(block_id, nblocks))
+                                 : block_id;
     if ((A0.variant & 8192) && A0.C <= 1) {
         // descending j: a launch larger than two waves per SIMD places its last workgroups as
         // third waves on a SIMD; with this order those are the lowest-asset tiles, whose short

@@ -784,7 +784,7 @@ int aiy_ws_invalidate(aiy_ws* ws) {
 
 int aiy_ws_set_variant(aiy_ws* ws, int variant) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
-    if (variant < -1 || variant > 65535) return fail(AIY_BAD_ARG, "variant in [-1, 65535]");
+    if (variant < -1 || variant > 262143) return fail(AIY_BAD_ARG, "variant in [-1, 262143]");
     ws->variant = variant;
     return AIY_OK;
 }

@@ -162,6 +162,9 @@ def main():
     ap.add_argument("--chain", action="store_true",
                     help="time the sweeps as one chain (each tree launch builds the next sweep's "
                          "table; measured slower, DESIGN.md §5) instead of table + tree per sweep")
+    ap.add_argument("--one-call", action="store_true",
+                    help="issue the timed sweeps with one aiy_vfi_sweeps_dev call (C++ loop) "
+                         "instead of one Python call per sweep; same kernels")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the labour/EGM/batch legs (D4, D5 per-GPU)")
     args = ap.parse_args()
@@ -219,11 +222,11 @@ def main():
         with --chain one chain through aiy_vfi_sweeps_dev — the first sweep's table by the
         table kernel, every later one built by the previous sweep's tree launch."""
         nonlocal cur
-        if not args.chain or args.mode != 1:
+        if not (args.chain or args.one_call) or args.mode != 1:
             for _ in range(n):
                 step()
             return
-        ws.set_chain(True)
+        ws.set_chain(bool(args.chain))
         ws.vfi_sweeps(v[cur], v[1 - cur], a_t, s_t, P_t, r, w, cal["beta"], cal["sigma"], n,
                       idx, pk, pc, hint=idx, mode=args.mode)
         ws.set_chain(False)

@@ -265,8 +265,8 @@ int aiy_ws_set_persistent(aiy_ws* ws, int persistent);
  * launches per step even when Na <= 1024 (default there: one fused launch); bit 12 = the one-pass
  * scatter step when Na > 1024 (default there: two launches, one chained launch per step in the
  * solve loops); bit 13 = no chaining in the solve loops; bit 14 = no interp1 segment hints.  Bit 13 = tiles in
- * descending asset order (one wave per tile).  Results are identical for every value in
- * [-1, 16383].
+ * descending asset order (one wave per tile); bit 17 = each XCD's range of tiles dealt in
+ * reverse dispatch order (with bit 4).  Results are identical for every value in [-1, 262143].
  * -1 (default): chosen by size — Na <= 4096: 2 cooperating waves per tile (A1), 4 with bit 12
  * (labour); else 16. */
 int aiy_ws_set_variant(aiy_ws* ws, int variant);
