@@ -175,3 +175,17 @@ def test_chain_solve_equals_unchained(pkg, gpu):
     assert res[0][:2] == res[1][:2]
     for x, y in zip(res[0][2:], res[1][2:]):
         assert np.array_equal(x.view(np.uint8), y.view(np.uint8))
+
+
+@pytest.mark.parametrize("Na", [5000, 20000])
+def test_reversed_xcd_order_bitwise(pkg, gpu, Na):
+    """Variant bit 17 (each XCD's tile range dealt in reverse) changes the work order only: the
+    sweeps equal the default order bit for bit, unchained and chained."""
+    import torch
+    cal = no.calib_aiyagari(Na=Na, shocks="rouwenhorst")
+    ref, _ = _run(pkg, torch, cal, 10, False, variant=16)
+    rev, _ = _run(pkg, torch, cal, 10, False, variant=16 | 131072)
+    _same(rev, ref)
+    revc, _ = _run(pkg, torch, cal, 10, True, variant=16 | 131072)
+    _same(revc, ref)
+    _oracle_last_sweep(cal, rev)
