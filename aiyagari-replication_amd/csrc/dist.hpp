@@ -12,6 +12,9 @@ constexpr int kDistChunk = 32;
 // a push wave stages its source range in LDS when it holds at most this many sources
 // (8 KB per wave on the on-grid path, 16 KB with lottery weights)
 constexpr int kDistStage = 1024;
+// the one-launch push (a wave per productivity state) takes N <= kDistPushMaxN; larger N run
+// the per-destination run gather + projection (two launches, any N)
+constexpr int kDistPushMaxN = 16;
 
 struct DistArgs {
     int N, Na;
@@ -36,7 +39,8 @@ struct DistArgs {
 // the policy's plan (keys, lottery weights, run offsets, flags) — once per policy
 int launch_dist_prepare(const DistArgs& A, hipStream_t st);
 // one push λ → λ' with max|λ'−λ| into A.diff (which the caller has cleared): one fused launch
-// on a monotone plan, the ordered-scan gather + projection otherwise
+// on a monotone plan with N <= kDistPushMaxN (which also zeroes A.diff_clear), the run gather +
+// projection for larger N, the ordered-scan gather + projection on a non-monotone plan
 int launch_dist_push(const DistArgs& A, bool fallback, hipStream_t st);
 int launch_dist_capital(const double* lam, const double* a, int N, int Na, double* part,
                         double* out, hipStream_t st);

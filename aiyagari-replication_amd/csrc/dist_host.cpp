@@ -47,7 +47,6 @@ static int dist_plan(aiy_ws* ws, const int* idx, const double* kp, const double*
                      const double* P, DistArgs* A, bool* fallback, hipStream_t st) {
     if (!ws || !a || !P || (!idx && !kp))
         return fail(AIY_BAD_ARG, "NULL argument (need policy_idx or policy_k)");
-    if (ws->N > 16) return fail(AIY_BAD_SHAPE, "histogram kernels support N <= 16");
     AIY_TRY(ensure_dist(ws));
     *A = DistArgs{};
     A->N = (int)ws->N; A->Na = (int)ws->Na; A->lottery = (idx == nullptr);
@@ -115,6 +114,7 @@ int dist_stationary_dev(aiy_ws* ws, const double* lam0, const int* idx, const do
     DistArgs A0;
     bool fb = false;
     AIY_TRY(dist_plan(ws, idx, kp, a, P, &A0, &fb, st));
+    const bool two_launch = fb || ws->N > kDistPushMaxN;  // (no diff_clear in those kernels)
     const int M = kDistSpecMax, R = 2 * M + 1;
     const size_t n = (size_t)ws->N * ws->Na, nb = n * sizeof(double);
     const int SW = 2 * kDiffSlots;
@@ -157,8 +157,8 @@ int dist_stationary_dev(aiy_ws* ws, const double* lam0, const int* idx, const do
             A.lam = slot(g - 1);
             A.out = slot(g);
             A.diff = sset(g);
-            // push g's set was zeroed by push g−1 (monotone plan) or is zeroed here
-            if (fb) AIY_HIP(hipMemsetAsync(sset(g), 0, SW * sizeof(unsigned long long), st));
+            // push g's set was zeroed by push g−1 (one-launch push) or is zeroed here
+            if (two_launch) AIY_HIP(hipMemsetAsync(sset(g), 0, SW * sizeof(unsigned long long), st));
             else A.diff_clear = sset(g + 1);
             AIY_TRY(ws_timing_begin(ws, st));
             AIY_TRY(launch_dist_push(A, fb, st));

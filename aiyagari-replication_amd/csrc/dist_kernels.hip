@@ -17,6 +17,8 @@
 // kDistChunk): runs of ≤ 32 terms are summed by their own lane; a longer run is split over the
 // wave, one chunk per lane, and its chunk sums are folded in order — so the borrowing-
 // constraint run does not serialise a lane for hundreds of dependent additions.
+// N > 16 (more states than one workgroup's waves): one thread per (i,k) sums its run(s) from
+// global memory, then a projection launch — same additions, two launches per push.
 // Fallback (non-monotone policy): one thread per (i,k) scans the row in order, same chunking.
 #include "aiy_common.hpp"
 #include "dist.hpp"
@@ -180,15 +182,15 @@ __device__ __forceinline__ double dist_mass_staged(const double* __restrict__ la
 // the additions and their order are the same either way.
 template <bool LOT>
 __global__ __launch_bounds__(1024) void dist_push_kernel(DistArgs A) {
-    __shared__ double s_mass[16][64];
+    __shared__ double s_mass[kDistPushMaxN][64];
     extern __shared__ double s_src[];  // [N][stage] λ, then [N][stage] weights (LOT)
     const int lane = threadIdx.x & 63;
     const int i = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // blockDim = 64·N
     const int N = A.N, Na = A.Na;
     const int k0 = blockIdx.x * 64, k = k0 + lane;
-    double pm[16];  // column m = i of P (the projection's weights), scalar loads issued first
+    double pm[kDistPushMaxN];  // column m = i of P (the projection's weights), loads first
 #pragma unroll
-    for (int q = 0; q < 16; ++q) pm[q] = q < N ? A.P[q * N + i] : 0.0;
+    for (int q = 0; q < kDistPushMaxN; ++q) pm[q] = q < N ? A.P[q * N + i] : 0.0;
     const bool ok = k < Na;
     // (instrumentation) shader-cycle stamps of the phases of this wave
     long long cy[6] = {0, 0, 0, 0, 0, 0};
@@ -248,11 +250,11 @@ __global__ __launch_bounds__(1024) void dist_push_kernel(DistArgs A) {
     bool okd = false;
     if (ok) {
         double acc = 0.0;
-        double ms[16];  // all LDS reads in flight before the ordered sum
+        double ms[kDistPushMaxN];  // all LDS reads in flight before the ordered sum
 #pragma unroll
-        for (int q = 0; q < 16; ++q) ms[q] = q < N ? s_mass[q][lane] : 0.0;
+        for (int q = 0; q < kDistPushMaxN; ++q) ms[q] = q < N ? s_mass[q][lane] : 0.0;
 #pragma unroll
-        for (int q = 0; q < 16; ++q)
+        for (int q = 0; q < kDistPushMaxN; ++q)
             if (q < N) acc = acc + pm[q] * ms[q];
         const size_t t = (size_t)m * Na + k;
         A.out[t] = acc;
@@ -291,6 +293,35 @@ __global__ void dist_gather_scan_kernel(DistArgs A) {
         else if (A.lottery && q + 1 == k) x = lam[j] * wr[j];
         else continue;
         part = part + x;
+        if (++n == kDistChunk) {
+            total = total + part;
+            part = 0.0;
+            n = 0;
+        }
+    }
+    if (n) total = total + part;
+    A.mass[t] = total;
+}
+
+// monotone plan with N > 16 (more states than the push workgroup's 16 waves): one thread per
+// destination (i,k) sums its run(s) [jb, je) from global memory in the A10 order (ascending j,
+// chunks of kDistChunk, chunk sums in order — the same additions as dist_mass), into A.mass;
+// dist_project_kernel then forms λ' for any N.
+template <bool LOT>
+__global__ void dist_gather_runs_kernel(DistArgs A) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= A.N * A.Na) return;
+    const int Na = A.Na;
+    const int i = t / Na, k = t - i * Na;
+    const int* __restrict__ off = A.off + (size_t)i * (Na + 1);
+    const double* __restrict__ lam = A.lam + (size_t)i * Na;
+    const double* __restrict__ wr = LOT ? A.wr + (size_t)i * Na : nullptr;
+    const int js = off[k], je = off[k + 1];
+    const int jb = (LOT && k > 0) ? off[k - 1] : js;
+    double total = 0.0, part = 0.0;
+    int n = 0;
+    for (int j = jb; j < je; ++j) {
+        part = part + dist_term<LOT>(lam, wr, j, js, 0);
         if (++n == kDistChunk) {
             total = total + part;
             part = 0.0;
@@ -350,9 +381,14 @@ int launch_dist_prepare(const DistArgs& A, hipStream_t st) {
 }
 
 int launch_dist_push(const DistArgs& A, bool fallback, hipStream_t st) {
-    if (A.N < 1 || A.N > 16) return fail(AIY_BAD_SHAPE, "histogram kernels support N <= 16");
+    if (A.N < 1) return fail(AIY_BAD_SHAPE, "histogram kernels need N >= 1");
     const int n = A.N * A.Na;
-    if (!fallback) {
+    if (!fallback && A.N > kDistPushMaxN) {  // general N: run gather + projection
+        const int g = (n + 255) / 256;
+        if (A.lottery) dist_gather_runs_kernel<true><<<g, 256, 0, st>>>(A);
+        else dist_gather_runs_kernel<false><<<g, 256, 0, st>>>(A);
+        dist_project_kernel<<<g, 256, 0, st>>>(A);
+    } else if (!fallback) {
         const int g = (A.Na + 63) / 64;
         // staging budget 64 KB per workgroup (two resident per CU beside s_mass)
         const int per = A.N * (A.lottery ? 16 : 8);

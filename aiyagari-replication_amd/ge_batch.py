@@ -8,7 +8,8 @@ evaluates every node of the next L levels of that tree (2^L - 1 candidate rates,
 computed from its parent bracket exactly as the sequential loop would, bit for bit), spread
 round-robin over the ranks; one all-gather of (K_s, K_d) per round (the only collective,
 8 bytes x 2 per candidate) lets every rank walk the path the sequential loop would take, with
-its early stop |K_s - K_d| < 1e-5.  Two rounds of L = 6 cover the reference's 10 steps.
+its early stop |K_s - K_d| < 1e-5.  The all-gather is one float64 tensor collective
+(all_gather_into_tensor over RCCL).  Two rounds of L = 6 cover the reference's 10 steps.
 
 Path independence: a node's result must not depend on which nodes were solved before it on
 the same rank.  Every candidate therefore starts its VFI from the same value function (the
@@ -82,8 +83,8 @@ def multisection(evaluate, r_low, r_high, max_steps=10, levels=6, tol=1e-5, rank
                  allgather=None) -> Trace:
     """evaluate(node) -> (K_s, K_d, iters) for the nodes this rank owns (index % world == rank),
     or, when `evaluate` has an `many` attribute, evaluate.many(nodes) -> list of triples for all
-    of them at once (the batched device path); allgather(list) -> list over ranks of lists
-    (None when world == 1)."""
+    of them at once (the batched device path); allgather(mine, n_nodes) -> list over ranks of
+    lists (None when world == 1; torch_allgather: one tensor all-gather per round)."""
     tr = Trace()
     lo, hi, done, step = r_low, r_high, False, 0
     while not done and step < max_steps:
@@ -95,7 +96,7 @@ def multisection(evaluate, r_low, r_high, max_steps=10, levels=6, tol=1e-5, rank
         else:
             mine = [(q, evaluate(nodes[q])) for q in own]
         if world > 1:
-            parts = allgather(mine)
+            parts = allgather(mine, len(nodes))
             allres = [x for part in parts for x in part]
         else:
             allres = mine
@@ -128,13 +129,27 @@ def bisection(evaluate, r_low, r_high, max_steps=10, tol=1e-5) -> Trace:
     return tr
 
 
-def torch_allgather(obj):
-    """All-gather of small Python objects over the default process group (RCCL on GPU ranks,
-    gloo on CPU): one collective per round."""
+def torch_allgather(mine, n_nodes):
+    """The round's one collective (Aiyagari_VFI.m:193-204's decision inputs): every rank's
+    (q, K_s, K_d, iters) rows as one float64 tensor [ceil(n_nodes / world), 4] (padding rows
+    q = -1), gathered with all_gather_into_tensor — RCCL on GPU ranks (the tensor lives on the
+    rank's current device), gloo on CPU.  All four fields are exact in float64 (q, iters are
+    small integers).  Returns the list over ranks of [(q, (K_s, K_d, iters)), ...]."""
+    import torch
     import torch.distributed as dist
-    out = [None] * dist.get_world_size()
-    dist.all_gather_object(out, obj)
-    return out
+    world = dist.get_world_size()
+    rows = -(-n_nodes // world)
+    if len(mine) > rows:
+        raise ValueError(f"{len(mine)} results on one rank, at most {rows} expected")
+    dev = (torch.device("cuda", torch.cuda.current_device())
+           if dist.get_backend() == "nccl" else torch.device("cpu"))
+    buf = torch.full((rows, 4), -1.0, dtype=torch.float64)
+    for n, (q, (ks, kd, it)) in enumerate(mine):
+        buf[n] = torch.tensor([q, ks, kd, it], dtype=torch.float64)
+    out = torch.empty((world * rows, 4), dtype=torch.float64, device=dev)
+    dist.all_gather_into_tensor(out, buf.to(dev))
+    got = out.cpu().view(world, rows, 4).tolist()
+    return [[(int(q), (ks, kd, int(it))) for q, ks, kd, it in part if q >= 0] for part in got]
 
 
 # ------------------------------------------------------------------------------ evaluators

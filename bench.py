@@ -167,15 +167,25 @@ def main():
                          "instead of one Python call per sweep; same kernels")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the labour/EGM/batch legs (D4, D5 per-GPU)")
+    ap.add_argument("--detail", default=str(ROOT / "gpurun_out" / "bench_detail.json"),
+                    help="file for the full result (every leg); stdout's last line is the "
+                         "compact contract line")
+    ap.add_argument("--dry-run-cpu", action="store_true",
+                    help="launcher/contract check without a GPU: gloo ranks, a trivial timed "
+                         "CPU loop, the same barrier/max-over-ranks/contract line")
     args = ap.parse_args()
+
+    import bench_launch
+    # --gpus N without a launcher: start N ranks (child torch.distributed.run), exit with its rc
+    bench_launch.relaunch(args.gpus, str(Path(__file__).resolve()), sys.argv[1:])
+    world, rank, local = bench_launch.check_world(args.gpus)
+    if args.dry_run_cpu:
+        return dry_run_cpu(args, world, rank)
 
     import torch
     import torch.distributed as dist
     import bench_legs as BL
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)  # before the process group: RCCL binds the current device
     if world > 1:
         dist.init_process_group("nccl")
@@ -296,12 +306,14 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt, kern_avg_ms = float(tt[0]), float(tt[1])
 
+    progress(f"headline: {dt / args.steps * 1e3:.4f} ms/step")
     legs = {}
     if not args.no_ks:   # BASELINE configs[4]: KS VFI sharded over the same ranks (strong)
         import bench_ks
         legs["ks_sharded"] = bench_ks.ks_leg(pkg, world, rank, dev, depth=args.ks_depth)
         if world == 1 and not args.no_extra:  # compute side of the N = 8 schedule, on this GPU
             legs["ks_sharded"]["ghost_model"] = bench_ks.ghost_model(pkg, dev)
+        progress("ks_sharded done")
     if not args.no_ge:   # BASELINE configs[3]: multisection GE over the same ranks
         legs["ge_batch"] = BL.ge_batch_leg(pkg, world, rank, dev)
 
@@ -404,7 +416,9 @@ def main():
             out["solve_to_tol"] = solve_wall(pkg, ws, cal, r, w, a_t, s_t, P_t, dev)
         if world == 1 and not args.no_extra:
             out["batch_config4_share"] = BL.batch_leg(pkg, dev)
-            out["dist"] = BL.dist_leg(pkg, dev)
+            progress("batch_config4_share done")
+            out["dist"] = BL.dist_leg(pkg, dev, cpu_threads=threads)
+            progress("dist done")
             # counter passes of these kernels (tools/pmc_workloads.py under tools/pmc.sh)
             pm = lambda n: ((_json_profile(f"r03_pmc_{n}.json") or {}).get("derived"))
             tr = lambda n: ((_json_profile(f"r03_traffic_{n}.json") or {}).get("bytes_per_launch"))
@@ -419,6 +433,7 @@ def main():
                                 "Na20000": BL.labor_leg(pkg, dev, 20000, steps=5, reps=3, cpu=False)}
             out["egm"] = {"Na20000": BL.egm_leg(pkg, dev, 20000, cpu_threads=threads),
                           "Na400": BL.egm_leg(pkg, dev, 400, cpu_threads=threads)}
+            progress("labor_vfi, egm done")
             out["labor_egm"] = {"Na20000": BL.egm_leg(pkg, dev, 20000, labor=True,
                                                       cpu_threads=threads)}
             out["labor_vfi"]["Na400"]["roofline"]["pmc"] = pm("labor_na400")
@@ -429,9 +444,11 @@ def main():
                 pmc_source="profiles/r03_pmc_egm_{rhs,interp}.json, r03_traffic_egm_*.json")
         if not args.no_panel and world == 1:   # F3/F2: KS shock panel + agent simulation
             import bench_panel
-            out["ks_panel"] = bench_panel.panel_leg(pkg, dev)
+            out["ks_panel"] = bench_panel.panel_leg(pkg, dev, cpu_threads=threads)
+            progress("ks_panel done")
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cal, r, w, args.cpu_sweeps, threads, info)
+            progress("cpu_baseline done")
             if "ks_sharded" in out and world == 1:
                 out["ks_sharded"]["cpu_baseline"] = BL.ks_cpu_baseline(pkg, threads=threads)
         if not args.no_ge and world == 1:
@@ -444,9 +461,56 @@ def main():
                     "sample": "the whole sequential bisection of Aiyagari_VFI.m at its defaults "
                               "(C restatement oracle/aiy_oracle.c, OpenMP over states), the "
                               "same r trace"}
-        print(json.dumps(out), flush=True)
+        import bench_report
+        detail = None
+        try:
+            bench_report.write_detail(out, args.detail)
+            detail = os.path.relpath(args.detail, ROOT)
+        except OSError as e:
+            progress(f"detail file not written: {e}")
+        print(bench_report.contract_line(out, detail), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def dry_run_cpu(args, world, rank):
+    """The multi-rank plumbing of main() on CPU (gloo): barrier + timed steps + barrier, MAX
+    over ranks, rank 0 prints the contract line.  No GPU, no kernels: tests only."""
+    import torch
+    import torch.distributed as dist
+    import bench_report
+    if world > 1:
+        dist.init_process_group("gloo")
+    x = np.random.RandomState(rank).random_sample(1 << 15)
+    for _ in range(args.warmup):
+        np.sort(x)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        np.sort(x)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt[0])
+    if rank == 0:
+        out = {"metric": "dry-run steps/s", "value": world * args.steps / dt, "unit": "steps/s",
+               "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+               "data": "dry run (CPU, gloo): launcher and contract-line check, no GPU work",
+               "config": {"workload": "dry-run", "parallelism": f"{world} gloo ranks"}}
+        print(bench_report.contract_line(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def progress(msg):
+    """Progress to stderr (stdout carries only the contract line)."""
+    print(f"# bench: {msg}", file=sys.stderr, flush=True)
 
 
 if __name__ == "__main__":

@@ -27,14 +27,15 @@ def main():
     ap.add_argument("--levels", type=int, default=6,
                     help="bisection-tree levels per round (6: BASELINE's 63+1 candidates; 0: auto)")
     ap.add_argument("--no-sequential", action="store_true")
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (started here when no launcher)")
     args = ap.parse_args()
+    import bench_launch
+    bench_launch.relaunch(args.gpus, str(Path(__file__).resolve()), sys.argv[1:])
+    world, rank, local = bench_launch.check_world(args.gpus)
     import numpy as np
     import torch
     import torch.distributed as dist
     import bench
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)  # before the process group: RCCL binds the current device
     if world > 1:
         dist.init_process_group("nccl")

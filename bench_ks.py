@@ -209,13 +209,14 @@ def main():
     ap.add_argument("--depth", type=int, default=None, help="Howard sweeps per exchange")
     ap.add_argument("--ghost-model", action="store_true",
                     help="one GPU: compute time per sweep vs depth for emulated 8-rank shards")
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (started here when no launcher)")
     args = ap.parse_args()
+    import bench_launch
+    bench_launch.relaunch(args.gpus, str(Path(__file__).resolve()), sys.argv[1:])
+    world, rank, local = bench_launch.check_world(args.gpus)
     import torch
     import torch.distributed as dist
     import bench
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)  # before the process group: RCCL binds the current device
     if world > 1:
         dist.init_process_group("nccl")

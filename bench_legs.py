@@ -380,7 +380,7 @@ def batch_leg(pkg, dev, Na=20000, C=8, sweeps=25):
 DIST_BYTES_PER_STATE = 20  # λ in (8), run offset (4), λ' out (8) per state and push
 
 
-def dist_leg(pkg, dev, Na=20000, pushes=320, cpu_pushes=600):
+def dist_leg(pkg, dev, Na=20000, pushes=320, cpu_pushes=600, cpu_threads=1):
     """A10 histogram pushes (csrc/dist_kernels.hip dist_push_kernel) on the config-2 policy
     (Na = 20,000, Rouwenhorst, r = 0.04, the device VFI solve's argmax): `pushes` pushes from
     the uniform distribution through aiy_dist_stationary_dev with tol = 0 (plan once, batches of
@@ -431,8 +431,12 @@ def dist_leg(pkg, dev, Na=20000, pushes=320, cpu_pushes=600):
     gbs = DIST_BYTES_PER_STATE * states / (kern_ms * 1e-3) / 1e9
     idx_np = idx.cpu().numpy()
     lam_np = lam0.cpu().numpy()
-    dt = _time_cpu(lambda: corc.dist_stationary(lam_np, cal["a_grid"], cal["P"], idx=idx_np,
-                                                tol=0.0, max_iter=cpu_pushes), 1)
+    cpu_dt = {}
+    for th in sorted({1, cpu_threads}):  # OpenMP over productivity rows (same sum order)
+        cpu_dt[th] = _time_cpu(lambda: corc.dist_stationary(lam_np, cal["a_grid"], cal["P"],
+                                                            idx=idx_np, tol=0.0,
+                                                            max_iter=cpu_pushes), th)
+    dt = cpu_dt[cpu_threads]
     return {"workload": f"A10 histogram pushes, Na={Na} Nz={N} Rouwenhorst, policy = argmax of "
                         f"the r=0.04 VFI solve ({iters} sweeps); {pushes} pushes from uniform "
                         f"lambda, device tier (aiy_dist_stationary_dev, tol=0)",
@@ -446,11 +450,13 @@ def dist_leg(pkg, dev, Na=20000, pushes=320, cpu_pushes=600):
                          "kernel_avg_ms": kern_ms, "launches": nl,
                          "basis": f"{DIST_BYTES_PER_STATE} B algorithmic per state and push "
                                   f"(lambda in, run offset, lambda' out) x {states} states"},
-            "cpu_baseline": {"value": cpu_pushes / dt, "unit": "pushes/s", "cores": 1,
+            "cpu_baseline": {"value": cpu_pushes / dt, "unit": "pushes/s", "cores": cpu_threads,
                              "kind": "port", "states_per_s": cpu_pushes * states / dt,
-                             "sample": f"{cpu_pushes} pushes of orc_dist_stationary (sequential "
-                                       f"scatter, oracle/aiy_oracle.c) on the same policy: "
-                                       f"{dt:.2f} s"}}
+                             "one_core": cpu_pushes / cpu_dt[1],
+                             "sample": f"{cpu_pushes} pushes of orc_dist_stationary (scatter in "
+                                       f"source order, OpenMP over productivity rows, "
+                                       f"oracle/aiy_oracle.c) on the same policy: {dt:.2f} s on "
+                                       f"{cpu_threads} threads, {cpu_dt[1]:.2f} s on 1"}}
 
 
 def ge_batch_leg(pkg, world, rank, dev, Na=400, levels=6, sequential=True):

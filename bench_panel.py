@@ -48,7 +48,10 @@ def _time(fn, reps):
     return ms[len(ms) // 2]
 
 
-def panel_leg(pkg, dev, T=1100, pop=10000, big_T=200, big_pop=1_000_000, reps=5):
+def panel_leg(pkg, dev, T=1100, pop=10000, big_T=200, big_pop=1_000_000, reps=5, cpu_threads=None):
+    """Both panel sizes on the GPU; with cpu_threads set, the restatement's CPU figure on the
+    script's panel as `cpu_baseline` (numpy, one thread — it vectorises over agents, not
+    cores), and `value` = the script-size panel's agent-periods/s (shocks + simulation)."""
     import numpy as np
     import torch
     kp = pkg.ks_panel
@@ -96,8 +99,19 @@ def panel_leg(pkg, dev, T=1100, pop=10000, big_T=200, big_pop=1_000_000, reps=5)
         }
         del U, zi, eps, sim
         torch.cuda.empty_cache()
-    return {"metric": "Krusell-Smith panel agent-periods/s (shocks + capital simulation, fp64)",
-            "workload": "Krusell_Smith_VFI.m:57-94 and :206-248", **out}
+    ref = out["reference"]
+    res = {"metric": "Krusell-Smith panel agent-periods/s (shocks + capital simulation, fp64)",
+           "workload": "Krusell_Smith_VFI.m:57-94 and :206-248", **out,
+           "value": ref["T"] * ref["population"] / ((ref["shocks_ms"] + ref["simulate_ms"]) * 1e-3),
+           "unit": "agent-periods/s (script panel, shocks + simulation)"}
+    if cpu_threads is not None:
+        c = cpu_leg(T, pop)
+        res["cpu_baseline"] = {"value": c["agent_periods_per_s"], "unit": "agent-periods/s",
+                               "cores": 1, "kind": "port", **c,
+                               "sample": f"the script's panel (T={T}, {pop} agents): numpy "
+                                         f"restatement (oracle/np_oracle.py ks_shocks + "
+                                         f"ks_panel_simulate), one thread"}
+    return res
 
 
 def cpu_leg(T=1100, pop=10000):

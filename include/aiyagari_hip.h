@@ -116,7 +116,10 @@ int aiy_sim_capital(const double* policy_k, int vfi_layout, const double* a_grid
  * On-grid policy (policy_idx, 1-based; pass policy_k = NULL) or off-grid lottery between
  * the bracketing nodes (policy_k; policy_idx = NULL).  All arrays in the script's layout:
  * N x Na if vfi_layout, else Na x N.  lambda in/out (in = initial guess).  Iterates until
- * max|Δλ| < tol or max_iter; returns K = Σ_ij λ(i,j)·a_j, iters, final max|Δλ|. */
+ * max|Δλ| < tol or max_iter; returns K = Σ_ij λ(i,j)·a_j, iters, final max|Δλ|.
+ * Any N >= 1: a monotone policy with N <= 16 pushes in one launch (a wave per state), larger
+ * N in two (run gather + projection); a non-monotone policy takes the ordered-scan gather.
+ * The additions are the same on every path (bit-identical λ). */
 int aiy_dist_stationary(const int32_t* policy_idx, const double* policy_k, int vfi_layout,
                         const double* a_grid, const double* P, int64_t N, int64_t Na,
                         double tol, int64_t max_iter, double* lambda, double* k_supply,

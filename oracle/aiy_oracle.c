@@ -381,8 +381,10 @@ static void mass_acc_add(orc_mass_acc* m, int64_t q, double x) {
 /* finish the chunks and project: out(m,k) = sum_i P(i,m) mass(i,k), i ascending */
 static void mass_acc_project(orc_mass_acc* m, int64_t N, int64_t Na, const double* P,
                              double* out) {
+#pragma omp parallel for schedule(static)
     for (int64_t q = 0; q < N * Na; ++q)
         if (m->cnt[q]) m->tot[q] = m->tot[q] + m->part[q];
+#pragma omp parallel for schedule(static)
     for (int64_t c = 0; c < N; ++c)
         for (int64_t k = 0; k < Na; ++k) {
             double acc = 0.0;
@@ -400,6 +402,9 @@ int orc_dist_update_ongrid(int64_t N, int64_t Na, const double* lam, const int32
                            const double* P, double* out) {
     orc_mass_acc m;
     if (mass_acc_init(&m, N * Na)) { mass_acc_free(&m); return 1; }
+    /* rows are independent (source row i lands in destination row i): threads over rows keep
+     * every destination's term order */
+#pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < N; ++i)
         for (int64_t j = 0; j < Na; ++j) mass_acc_add(&m, i * Na + idx[i * Na + j], lam[i * Na + j]);
     mass_acc_project(&m, N, Na, P, out);
@@ -411,6 +416,7 @@ int orc_dist_update_lottery(int64_t N, int64_t Na, const double* lam, const doub
                             const double* a_grid, const double* P, double* out) {
     orc_mass_acc m;
     if (mass_acc_init(&m, N * Na)) { mass_acc_free(&m); return 1; }
+#pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < N; ++i)
         for (int64_t j = 0; j < Na; ++j) {
             double x = kp[i * Na + j];

@@ -160,3 +160,44 @@ def test_staged_push_shapes_bitwise(pkg, gpu, N, Na):
     lam, _, _, _ = pkg.dist_stationary(a, P, policy_k=kp, lam0=lam0, tol=0.0, max_iter=2)
     lo, _, _, _ = corc.dist_stationary(lam0, a, P, kp=kp, tol=0.0, max_iter=2)
     assert np.array_equal(lam, lo)
+
+
+@pytest.mark.parametrize("N,Na", [(17, 900), (32, 2000), (48, 401)])
+def test_push_more_than_16_states_bitwise(pkg, gpu, N, Na):
+    """N > 16 (Rouwenhorst Nz = 32/48, the MFMA EV calibrations): the run gather + projection
+    path, on-grid and lottery, against the C restatement — and through the host tier's
+    speculative fixed-point loop (diff slots cleared per push on this path)."""
+    rng = np.random.default_rng(N * 7 + Na)
+    a = np.linspace(0.0, 30.0, Na) ** 2 / 30.0
+    P = rng.random((N, N)); P /= P.sum(1, keepdims=True)
+    steps = rng.choice([0, 1, 1, 1, 2, 0, 0, 40], size=(N, Na))  # incl. runs > one chunk
+    idx = np.minimum(np.cumsum(steps, 1) // 3, Na - 1).astype(np.int64)
+    lam0 = rng.random((N, Na)); lam0 /= lam0.sum()
+    lam, _, it, _ = pkg.dist_stationary(a, P, policy_idx=idx + 1, lam0=lam0, tol=0.0, max_iter=3)
+    lo, _, _, _ = corc.dist_stationary(lam0, a, P, idx=idx, tol=0.0, max_iter=3)
+    assert it == 3 and np.array_equal(lam, lo)
+    kp = np.sort(rng.uniform(-1.0, a[-1] * 0.8, (N, Na)), 1)
+    lam, _, _, _ = pkg.dist_stationary(a, P, policy_k=kp, lam0=lam0, tol=0.0, max_iter=2)
+    lo, _, _, _ = corc.dist_stationary(lam0, a, P, kp=kp, tol=0.0, max_iter=2)
+    assert np.array_equal(lam, lo)
+    lam, K, it, d = pkg.dist_stationary(a, P, policy_idx=idx + 1, lam0=lam0, tol=1e-12,
+                                        max_iter=400)
+    lo, Ko, ito, do = corc.dist_stationary(lam0, a, P, idx=idx, tol=1e-12, max_iter=400)
+    assert it == ito and d == do and np.array_equal(lam, lo)
+
+
+def test_ge_pipeline_rouwenhorst_32(pkg, gpu):
+    """VFI at Nz = 32 (MFMA EV) followed by dist_stationary on its policy — the
+    combination ge() runs — succeeds and matches the C restatement's histogram on that policy."""
+    from oracle import np_oracle as no2
+    cal = no2.calib_aiyagari(Na=300, shocks="rouwenhorst", N=32)
+    w = no2.wage(0.04, 0.36, 0.08)
+    R = pkg.vfi_solve(np.zeros((32, 300)), cal["a_grid"], cal["s"], cal["P"], 0.04, w, 0.96, 5.0,
+                      1e-5, 400)
+    lam0 = np.full((32, 300), 1.0 / (32 * 300))
+    lam, K, it, _ = pkg.dist_stationary(cal["a_grid"], cal["P"], policy_idx=R["idx"], lam0=lam0,
+                                        tol=1e-12, max_iter=3000)
+    lo, Ko, ito, _ = corc.dist_stationary(lam0, cal["a_grid"], cal["P"], idx=R["idx"] - 1,
+                                          tol=1e-12, max_iter=3000)
+    assert it == ito and np.array_equal(lam, lo)
+    assert abs(K - Ko) <= 1e-12 * abs(Ko)

@@ -92,14 +92,17 @@ def _worker(rank, world, port, outdir):
     dist.destroy_process_group()
 
 
-def test_gloo_two_ranks_equal_sequential(tmp_path):
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_ranks_equal_sequential(tmp_path, world):
+    """The tensor all-gather (all_gather_into_tensor of [ceil(63/world), 4] float64 rows; 3
+    ranks leave padding rows) reproduces the sequential trace on every rank."""
     import torch.multiprocessing as mp
-    port = 29500 + (os.getpid() % 2000)
-    mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    port = 29500 + (os.getpid() % 2000) + 7 * world
+    mp.spawn(_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
     gb = _pkg().ge_batch
     ev, cal = _oracle_evaluator()
     S = gb.bisection(ev, -0.05, 1 / cal["beta"] - 1)
-    for rank in range(2):
+    for rank in range(world):
         R = json.loads(Path(tmp_path, f"r{rank}.json").read_text())
         assert R["r"] == S.r_history and R["ks"] == S.k_supply and R["it"] == S.iters
         assert R["final"] == S.r
