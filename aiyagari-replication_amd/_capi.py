@@ -10,7 +10,9 @@ import re
 from pathlib import Path
 
 PKG_DIR = Path(__file__).resolve().parent
-LIB_PATH = PKG_DIR / "libaiyagari_hip.so"
+# AIY_HIP_LIB: another build of the same library (A/B timing of a kernel change on one box);
+# the product default is the in-tree build
+LIB_PATH = Path(os.environ.get("AIY_HIP_LIB") or (PKG_DIR / "libaiyagari_hip.so"))
 HEADER = PKG_DIR.parent / "include" / "aiyagari_hip.h"
 
 STATUS = {0: "AIY_OK", 1: "AIY_BAD_SHAPE", 2: "AIY_NON_FINITE", 3: "AIY_HIP_ERROR",

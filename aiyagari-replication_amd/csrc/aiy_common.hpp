@@ -39,14 +39,6 @@ __device__ __forceinline__ int xcd_remap(int b, int G) {
     const int q = G / 8, r = G % 8, x = b % 8, slot = b / 8;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + slot;
 }
-// the same XCD ranges, each dealt in reverse (the last-dispatched workgroups of an XCD — the
-// third waves on its SIMDs — take the first items of its range)
-__device__ __forceinline__ int xcd_remap_rev(int b, int G) {
-    const int q = G / 8, r = G % 8, x = b % 8, slot = b / 8;
-    const int start = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
-    const int size = x < r ? q + 1 : q;
-    return start + (size - 1 - slot);
-}
 __device__ __forceinline__ int readlane_i(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
 // lane l's double (l wave-uniform) as a wave-uniform value: two v_readlane_b32, no memory
 __device__ __forceinline__ double readlane_d(double x, int l) {
@@ -151,6 +143,24 @@ __device__ __forceinline__ void block_max_to_slots(bool ok, double d,
             atomicMax(sl, k);
             atomicOr(sl + 1, 1ull);
         }
+    }
+}
+
+// the same for a one-wave workgroup: the wave's maximum goes straight from lane 0 to the slot —
+// no LDS, no workgroup barrier (whose release fence would make the wave wait for all of its
+// output stores before the atomics could issue)
+__device__ __forceinline__ void wave_max_to_slots(bool ok, double d,
+                                                  unsigned long long* __restrict__ slots) {
+    unsigned long long key = ok ? (unsigned long long)aiy_dbits(d) : 0ull;
+    const bool any = __ballot(ok) != 0ull;
+    key = wave_max_u64_lane63(key);
+    const unsigned lo = __builtin_amdgcn_readlane((int)(unsigned)key, 63);
+    const unsigned hi = __builtin_amdgcn_readlane((int)(unsigned)(key >> 32), 63);
+    key = ((unsigned long long)hi << 32) | lo;
+    if (any && (threadIdx.x & 63) == 0) {
+        unsigned long long* sl = slots + 2 * (blockIdx.x % kDiffSlots);
+        atomicMax(sl, key);
+        atomicOr(sl + 1, 1ull);
     }
 }
 

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 
+#include "dispatch.hpp"
+
 namespace aiy {
 
 struct BellArgs {
@@ -59,22 +61,7 @@ struct BellArgs {
     const double* wv;  // [C] device: w of each candidate
     const int* stop;   // [C] device: nonzero = stopped at that sweep (skipped from then on)
     int parity;
-    // Chained sweeps (A1 tree screen, one wave per tile): the tree kernel also builds the NEXT
-    // sweep's table from the v_new it writes, so a chain of sweeps is one launch per sweep.
-    // Each wave stores its v_new write-through and adds to its tile's arrival counter; the wave
-    // whose add completes the tile's N rows computes EV, D, the 8-block and 64-block maxima of
-    // that tile's 64 candidates for every row (bell_table_kernel's values, bit for bit).
-    const double* Dm64;  // nullable: level-0 superblock bounds = max of 8 64-block maxima (Dm512 unused)
-    double* nEV;         // nullable (chain off): the next sweep's EV / Dt / Dm8 / Dm64
-    double* nDt;
-    double* nDm8;
-    double* nDm64;
-    unsigned* tcnt;                  // [ntile] arrival counters, zero between launches
-    const unsigned long long* fsrc;  // nullable: the previous sweep's slot set, folded into fold[]
-    unsigned long long* clr;         // nullable: slot set cleared for the sweep after next
 };
-// rows per chained table tile (the last arriver holds one V column of the tile in registers)
-constexpr int kChainMaxN = 16;
 
 // EV by fp64 MFMA from this productivity-grid size up (the variant bits 14 / 15 force VALU /
 // MFMA); below it the table kernel's sequential VALU sum, which the C oracle restates bit for
@@ -92,36 +79,12 @@ int launch_bell_kf(const BellArgs& A, hipStream_t st);
 int launch_bell_init(const BellArgs& A, hipStream_t st);
 int launch_bell_screen(const BellArgs& A, hipStream_t st);
 int launch_bell_tree(const BellArgs& A, hipStream_t st);
-// Timing of the dominant kernel: when set, the next tree-kernel launch on this host thread
-// records these events as part of its own dispatch (hipExtLaunchKernelGGL), so their elapsed
-// time is the kernel's execution — the figure rocprofv3 reports — without the scheduling gaps
-// of separate event records.  The launch clears them.
-struct DispatchEvents {
-    hipEvent_t start = nullptr, stop = nullptr;
-};
-extern thread_local DispatchEvents g_dispatch_ev;
+// Timing of the dominant kernel: dispatch.hpp (events recorded by the tree launch itself).
 int launch_bell_plain(const BellArgs& A, hipStream_t st);
 int launch_bell_merge(const BellArgs& A, int use_partial, hipStream_t st);
 int launch_bell_table_batch(const BellArgs& A, unsigned long long* slots, int sweep, double tol,
                             hipStream_t st);
 size_t bell_partial_slots(const BellArgs& A);
 
-// Persistent small-grid solve (A2 for A1 with the tree screen): sweeps g0+1 .. max_iter of the
-// plain loop in ONE cooperative launch — table phase, grid barrier, tree phase, grid barrier,
-// the stop test on the device — so no sweep pays a kernel boundary or a host round trip.
-// A holds the sweeps' common arguments (hint = idx); V[g & 1] is sweep g's output.
-struct PersistArgs {
-    BellArgs A;
-    double* V0;
-    double* V1;
-    const unsigned long long* first;  // [2*kDiffSlots] sweep g0's diff slots
-    unsigned long long* slots;        // [2][2*kDiffSlots]
-    unsigned* bar;                    // [4] barrier counter, generation, registrations, tickets (zeroed)
-    long long* result;                // [2] sweeps done (g*), status: 0 exhausted, 1 stop, 2 barrier timeout
-    double tol;
-    long long g0, max_iter;
-};
-int launch_bell_persist(const PersistArgs& PA, hipStream_t st);
-bool bell_persist_eligible(const BellArgs& A);
 
 }  // namespace aiy

@@ -835,97 +835,6 @@ __global__ __launch_bounds__(256, MINW) void bell_screen_kernel(BellArgs A, int 
     }
 }
 
-// ------------------------------------------------------------------------------ chained tables
-// Level-0 bound of superblock sb of row i: the table kernel's 512-block maximum, or — chained
-// sweeps — the maximum of its eight 64-block maxima (the same blocks; any upper bound of the
-// superblock's keys is a valid bound, so the screen's result cannot depend on which)
-__device__ __forceinline__ double sb_bound(const BellArgs& A, int i, int sb) {
-    if (!A.Dm64) return A.Dm512[(size_t)i * A.nb512 + sb];
-    const double* __restrict__ p = A.Dm64 + (size_t)i * A.nb + 8 * sb;
-    const int n = A.nb - 8 * sb;
-    double v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = u < n ? p[u] : -__builtin_inf();  // all loads in flight
-    return fmax(fmax(fmax(v[0], v[1]), fmax(v[2], v[3])), fmax(fmax(v[4], v[5]), fmax(v[6], v[7])));
-}
-
-// Chained sweeps, the slot ring: sweep g writes slot set g mod 3; one wave of sweep g folds set
-// g − 1 (complete: its launch has ended) into fold[0..1] and clears set g + 1 (folded or
-// reduced by an earlier launch), so no sweep of a chain needs a memset or a reduce launch.
-__device__ __forceinline__ void chain_slots(const BellArgs& A) {
-    const int l = threadIdx.x & 63;
-    static_assert(kDiffSlots == 64, "one wave folds the slots");
-    if (A.fsrc && A.fold) {  // reduce_slots_kernel's fold
-        unsigned long long m = A.fsrc[2 * l];
-        const int any = __ballot((A.fsrc[2 * l + 1] & 1ull) != 0ull) != 0ull;
-        for (int off = 32; off > 0; off >>= 1) {
-            const unsigned long long o = __shfl_xor(m, off);
-            m = o > m ? o : m;
-        }
-        if (l == 0) {
-            A.fold[0] = m;
-            A.fold[1] = any ? 1ull : 0ull;
-        }
-    }
-    if (A.clr) {
-        A.clr[l] = 0ull;
-        A.clr[l + 64] = 0ull;
-    }
-}
-
-// The next sweep's table on tile `tile` (candidates k = 64·tile + lane), built by the wave whose
-// arrival completes the tile: every wave of the launch has stored its v_new write-through (sc1)
-// and waited for the stores (vmcnt 0) before its lane 0 adds to the tile's agent-scope counter,
-// so the wave that draws N − 1 reads the tile's N rows of v_new with sc1 loads after its add
-// has returned (MI355X_MICROARCH.md, inter-workgroup visibility: the counter hand-off row).
-// EV(i,k) = Σ_m (β·P(i,m))·V(m,k) in m order, D, and the 8- and 64-block maxima: the operations
-// of table_ev / table_D / bell_table_kernel on the same values, so the table is bit-identical.
-__device__ __forceinline__ void chain_table_tile(const BellArgs& A, int tile) {
-    const int lane = threadIdx.x & 63;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's v_new stores are complete
-    unsigned old = 0;
-    if (lane == 0)
-        old = __hip_atomic_fetch_add(A.tcnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    old = __builtin_amdgcn_readfirstlane(old);
-    if (old != (unsigned)(A.N - 1)) return;  // wave-uniform
-    if (lane == 0)  // re-armed for the next launch (every other wave of the tile has arrived)
-        __hip_atomic_store(A.tcnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int N = A.N, Na = A.Na;
-    const int k = tile * 64 + lane;
-    const bool ok = k < Na;
-    double vv[kChainMaxN];
-#pragma unroll
-    for (int m = 0; m < kChainMaxN; ++m)
-        vv[m] = (m < N && ok) ? __hip_atomic_load(A.v_new + (size_t)m * Na + k, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT)
-                              : 0.0;
-    for (int i = 0; i < N; ++i) {
-        double D = -__builtin_inf();
-        if (ok) {
-            const size_t t = (size_t)i * Na + k;
-            double acc = 0.0;
-#pragma unroll
-            for (int m = 0; m < kChainMaxN; ++m)
-                if (m < N) acc = acc + (A.beta * A.P[i * N + m]) * vv[m];
-            A.nEV[t] = acc;
-            D = table_D(acc, A.np);
-            A.nDt[t] = D;
-        }
-        double d8 = fmax(D, dpp_d<0xB1>(D));
-        d8 = fmax(d8, dpp_d<0x4E>(d8));
-        d8 = fmax(d8, dpp_d<0x104>(d8));
-        if (ok && (k & 7) == 0) A.nDm8[(size_t)i * A.nb8 + (k >> 3)] = d8;
-        D = fmax(D, dpp_d<0xB1>(D));
-        D = fmax(D, dpp_d<0x4E>(D));
-        D = fmax(D, dpp_d<0x141>(D));
-        D = fmax(D, dpp_d<0x140>(D));
-        D = fmax(D, dpp_d<0x142, 0xa>(D));
-        D = fmax(D, dpp_d<0x143, 0xc>(D));
-        D = readlane_d(D, 63);
-        if (lane == 0) A.nDm64[(size_t)i * A.nb + tile] = D;
-    }
-}
-
 // ------------------------------------------------------------------------------ 3'. tree
 // The default screened sweep.  One workgroup of W waves owns 64·R consecutive states of row i
 // and searches all their candidates (every labour level, the whole feasible prefix) through a
@@ -948,9 +857,8 @@ __device__ __forceinline__ void chain_table_tile(const BellArgs& A, int tile) {
 // start — the init kernel's candidate (best0/idx0).
 // INS: the instrumented build (per-state work counters, per-item trace); the production
 // instantiation compiles every counter and time stamp out
-// The body of one work item (tile of row i); block_id / nblocks are the launch coordinates (the
-// persistent solve calls it for several items per workgroup).
-template <int NP, bool LAB, int R, int LB, int W, bool INS, bool CH = false>
+// The body of one work item (tile of row i); block_id / nblocks are the launch coordinates.
+template <int NP, bool LAB, int R, int LB, int W, bool INS>
 __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, int block_id,
                                                int nblocks) {
     const int lane = threadIdx.x & 63;
@@ -962,16 +870,7 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
                  "s"(A0.variant), "s"(A0.C), "s"(A0.nb512), "s"(A0.sigma), "s"(A0.trace));
     const long long t_boot = (INS && A0.trace) ? (long long)wall_clock64() : 0;  // (instrumentation)
     const long long c_boot = (INS && A0.trace) ? (long long)__builtin_amdgcn_s_memtime() : 0;
-    int item = (A0.variant & 16) ? ((A0.variant & 131072) ? xcd_remap_rev(block_id, nblocks)
-                                                          : xcd_remap(block_id, nblocks))
-                                 : block_id;
-    if ((A0.variant & 8192) && A0.C <= 1) {
-        // descending j: a launch larger than two waves per SIMD places its last workgroups as
-        // third waves on a SIMD; with this order those are the lowest-asset tiles, whose short
-        // feasible prefixes make them the cheapest
-        const int q = block_id / A0.N;
-        item = (block_id - q * A0.N) * ntile + (ntile - 1 - q);
-    }
+    int item = (A0.variant & 16) ? xcd_remap(block_id, nblocks) : block_id;
     BellArgs A = A0;
     if (A0.C > 1) {  // batched candidates: blocks [c·N·ntile, (c+1)·N·ntile) are candidate c's
         const int c = item / (A0.N * ntile);
@@ -994,16 +893,13 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
     // and fine-screen software pipelines (two register sets each) are off and the screen
     // stages four chains at a time; the best exchange reuses each wave's idle s_cand slice
     constexpr bool LEAN = W >= 2 || LAB;  // (labour: keeps 3 waves per SIMD)
-    // chained sweeps (BellArgs::nEV): a separate instantiation, so the default one is unchanged
-    constexpr bool kChain = CH && W == 1 && R == 1 && !LAB;
 
     // loads that do not depend on the start-up below, issued first so that their latency
     // overlaps it: the level-0 bounds of the first 64 superblocks (first labour group) and v_old
     double dm0_pre, a0_pre;
     {
         const bool oks = lane < A.nb512;
-        dm0_pre = oks ? (kChain ? sb_bound(A, i, lane) : A.Dm512[(size_t)i * A.nb512 + lane])
-                      : -__builtin_inf();
+        dm0_pre = oks ? A.Dm512[(size_t)i * A.nb512 + lane] : -__builtin_inf();
         a0_pre = oks ? a[lane << 9] : 0.0;
     }
     double vo_pre[R];
@@ -1120,6 +1016,16 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
             best[r] = A.best0[t];
             idx[r] = A.idx0[t] == -2 ? -1 : A.idx0[t];
         }
+    }
+    // the start-up's argmax and its a_k, loaded now: the output needs a(argmax) for policy_k,
+    // and the tree rarely moves the argmax once the start-up has climbed to it, so the output
+    // phase usually skips that dependent load (it reloads when some lane's argmax moved)
+    int q_su[R];
+    double kp_su[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        q_su[r] = idx[r];
+        kp_su[r] = a[idx[r] >= 0 ? idx[r] / Nl : 0];
     }
     unsigned nhits = 0, nsup = 0, nblk = 0, nfine = 0, lane_pairs = 0;
     const long long t_start = (INS && A.trace) ? (long long)wall_clock64() : 0;
@@ -1472,8 +1378,7 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
         auto load512 = [&](int g) __attribute__((always_inline)) {
             const int sbl = g + lane;
             const bool oks = sbl < nsb;
-            dm0 = oks ? (kChain ? sb_bound(A, i, sbl) : A.Dm512[(size_t)i * A.nb512 + sbl])
-                      : -__builtin_inf();
+            dm0 = oks ? A.Dm512[(size_t)i * A.nb512 + sbl] : -__builtin_inf();
             a0 = oks ? a[sbl << 9] : 0.0;
         };
         if (l0 == 0) {  // prefetched (lanes past nsb are masked by the bound counts below)
@@ -1558,16 +1463,14 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
                 b = __builtin_nan("");
             }
             const int l = q % Nl, k = q / Nl;
-            const double kp = a[k];
+            double kp = kp_su[r];
+            if (__ballot(q != q_su[r]) != 0ull) kp = a[k];  // (wave-uniform: usually skipped)
             A.idx[t] = q;
             if (A.pk) A.pk[t] = kp;
             if (A.pc) A.pc[t] = cash<LAB>(x[r], y, LAB ? A.L[l] : 1.0) - kp;
             if (LAB && A.pl) A.pl[t] = A.L[l];
         }
-        if (kChain && A.nEV)  // write-through: the tile's last arriver reads it (chain_table_tile)
-            __hip_atomic_store(A.v_new + t, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
-            A.v_new[t] = b;
+        A.v_new[t] = b;
         if (mom && A.hint)  // this sweep's shift of the argmax, for the next sweep's start
             mom[t] = (hk0[r] >= 0 && idx[r] >= 0) ? idx[r] / Nl - hk0[r] : 0;
         const double d = fabs(b - vo);
@@ -1576,13 +1479,8 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
             okd = true;
         }
     }
-    block_max_to_slots(okd, dmax, A.diff);
-    if constexpr (kChain) {
-        if (A.nEV) {  // chained sweeps: the slot ring (one wave), then the next table's tile
-            if (block_id == 0) chain_slots(A);
-            chain_table_tile(A, tile);
-        }
-    }
+    if constexpr (W == 1) wave_max_to_slots(okd, dmax, A.diff);
+    else block_max_to_slots(okd, dmax, A.diff);
     if (INS && A.trace) {  // instrumentation (aiy_ws_set_timing bit 2): per-wave sums into wave 0
         __shared__ unsigned s_cnt[W][4];
         __shared__ unsigned s_pairs;
@@ -1623,422 +1521,12 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
     }
 }
 
-template <int NP, bool LAB, int R, int LB, int W, bool INS, bool CH = false>
+template <int NP, bool LAB, int R, int LB, int W, bool INS>
 // min waves per SIMD 3 (168 VGPRs): every item of Na = 20,000 is resident at W = 1; the
 // cooperative tiles (W >= 2) serve small grids and labour, where a few hundred waves run and
 // latency, not occupancy, bounds them — a budget of 5 (and of 4) made those builds spill
 __global__ __launch_bounds__(64 * W, 3) void bell_tree_kernel(BellArgs A0, int ntile) {
-    bell_tree_item<NP, LAB, R, LB, W, INS, CH>(A0, ntile, (int)blockIdx.x, (int)gridDim.x);
-}
-
-// ------------------------------------------------------------------------------ 3'''. persistent
-// A2 for small grids (the script's Na = 400 GE solves): at 2,800 states a sweep's two kernels
-// take ~5 + ~9 us, mostly launch ramp and the dependency gap between them, and the speculative
-// host loop still pays a read per batch.  Here one cooperative launch of one-wave workgroups
-// runs the sweeps itself: the table phase (EV, D, 8- and 512-block maxima: the table kernel's
-// values, 64 lanes x 8 passes per 512-candidate chunk), a grid barrier, the tree phase (the tree
-// kernel's item body, unchanged), a grid barrier, then every workgroup folds the same diff
-// slots and takes the same stop decision (Aiyagari_VFI.m:85-86).  Sweep g reads V[(g-1) & 1]
-// and writes V[g & 1], the plain loop's buffers; idx (= the next hint), pk and pc are
-// rewritten in place by each state's own lane.  The grid barrier: one counter and a
-// generation word, vector atomics, all working workgroups on one XCD (below); a waiter gives
-// up after ~2^25 short sleeps, reports status 2 and leaves the kernel, so a
-// lost workgroup cannot hang the device (co-residency itself is guaranteed by the cooperative
-// launch, which fails instead of running a grid that does not fit).
-// Barrier fences: agent scope (L2 write-back on release, invalidate on acquire), as a kernel
-// boundary does.  The workers all run on XCD 0 (below), so only its L2 is involved; lighter
-// same-XCD fences (vmcnt + L1 invalidate) were tried and were not sufficient on gfx950.
-// Measured at Na = 400: 31 us per sweep against 15 us for two ordinary launches per sweep in
-// the speculative loop — the barriers and the cold caches they leave cost more than the launch
-// gaps they remove — so the path is off by default (aiy_ws_set_persistent).
-__device__ __forceinline__ void xcd_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent"); }
-__device__ __forceinline__ void xcd_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); }
-// a coherent read of a word other workgroups update with atomics: an atomic RMW is performed
-// where the atomics are, never from a stale cache line
-__device__ __forceinline__ unsigned atomic_peek(unsigned* p) {
-    return __hip_atomic_fetch_or(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ bool grid_barrier(unsigned* bar, unsigned nblocks, long long* result) {
-    bool ok = true;
-    xcd_release();
-    if ((threadIdx.x & 63) == 0) {
-        const unsigned gen = atomic_peek(bar + 1);
-        if (__hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-            nblocks - 1) {
-            __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            xcd_release();
-            __hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            unsigned spins = 0;
-            while (atomic_peek(bar + 1) == gen) {
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins == (1u << 25)) {
-                    __hip_atomic_store(result + 1, 2ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok = false;
-                    break;
-                }
-            }
-        }
-    }
-    xcd_acquire();
-    return __builtin_amdgcn_readfirstlane(ok ? 1 : 0) != 0;
-}
-
-// one 512-candidate chunk of row i: EV, Dt, Dm8 and Dm512 exactly as bell_table_kernel
-__device__ __forceinline__ void persist_table_chunk(const BellArgs& A,
-                                                    const double* __restrict__ V, int i,
-                                                    int chunk) {
-    const int lane = threadIdx.x & 63;
-    const int N = A.N, Na = A.Na;
-    double m512 = -__builtin_inf();
-    for (int u = 0; u < 8; ++u) {
-        const int k = chunk * 512 + u * 64 + lane;
-        const bool ok = k < Na;
-        double D = -__builtin_inf();
-        if (ok) {
-            const size_t t = (size_t)i * Na + k;
-            const double acc = table_ev(N, Na, A.P, V, A.beta, i, k);
-            A.EV[t] = acc;
-            D = table_D(acc, A.np);
-            A.Dt[t] = D;
-        }
-        double d8 = fmax(D, dpp_d<0xB1>(D));  // lane ^ 1
-        d8 = fmax(d8, dpp_d<0x4E>(d8));         // lane ^ 2
-        d8 = fmax(d8, dpp_d<0x104>(d8));        // lane + 4: the 8-block maximum at lanes 8j
-        if (ok && (k & 7) == 0) A.Dm8[(size_t)i * A.nb8 + (k >> 3)] = d8;
-        m512 = fmax(m512, D);
-    }
-    for (int off = 32; off > 0; off >>= 1) m512 = fmax(m512, __shfl_xor(m512, off));
-    if (lane == 0) A.Dm512[(size_t)i * A.nb512 + chunk] = m512;
-}
-
-template <int NP>
-__global__ __launch_bounds__(64) void bell_persist_kernel(PersistArgs PA) {
-    // The grid is 8x the working set.  Every workgroup registers; those running on XCD 0 (the
-    // hardware XCC id) draw tickets, the first gmax of them work and share XCD 0's L2, all others
-    // leave.  Workers wait until every workgroup has registered (the cooperative launch makes
-    // them all resident), so the worker count G is final before the first barrier.
-    const int lane = threadIdx.x & 63;
-    unsigned* reg = PA.bar + 2;  // [0] registered workgroups, [1] XCD-0 tickets
-    const unsigned gmax = gridDim.x / 8;
-    unsigned ticket = ~0u;
-    if (lane == 0) {
-        const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & 15;
-        if (xcc == 0) ticket = __hip_atomic_fetch_add(reg + 1, 1u, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT);
-        xcd_release();
-        __hip_atomic_fetch_add(reg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    ticket = __builtin_amdgcn_readfirstlane(ticket);
-    if (ticket >= gmax) return;
-    if (lane == 0) {
-        unsigned spins = 0;
-        while (atomic_peek(reg) < gridDim.x) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins == (1u << 25)) {
-                __hip_atomic_store(PA.result + 1, 2ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-        }
-    }
-    const unsigned G = min(gmax, __builtin_amdgcn_readfirstlane(atomic_peek(reg + 1)));
-    const unsigned b = ticket;
-    xcd_acquire();
-    BellArgs A = PA.A;
-    const int ntile = (A.Na + 63) / 64, nitem = A.N * ntile, ntab = A.N * A.nb512;
-    // the stop test of a sweep from its diff slots (reduce_slots_kernel's fold)
-    auto stop_of = [&](const unsigned long long* sl) __attribute__((always_inline)) {
-        unsigned long long m = sl[2 * lane];
-        const bool any = __ballot((sl[2 * lane + 1] & 1ull) != 0ull) != 0ull;
-        for (int off = 32; off > 0; off >>= 1) {
-            const unsigned long long o = __shfl_xor(m, off);
-            m = o > m ? o : m;
-        }
-        return any && aiy_bitsd(m) < PA.tol;  // NaN-only: no stop (MATLAB max omits NaN)
-    };
-    long long g = PA.g0;
-    if (stop_of(PA.first)) {  // sweep g0 (the caller's ordinary launches) already stops
-        if (b == 0 && lane == 0) {
-            PA.result[0] = g;
-            PA.result[1] = 1;
-        }
-        return;
-    }
-    bool stopped = false;
-    for (g = PA.g0 + 1; g <= PA.max_iter; ++g) {
-        const double* Vold = (g & 1) ? PA.V0 : PA.V1;
-        double* Vnew = (g & 1) ? PA.V1 : PA.V0;
-        unsigned long long* sl = PA.slots + (size_t)(g & 1) * 2 * kDiffSlots;
-        if (b == 0) {  // (this set was last read by sweep g-2's stop test, two barriers ago)
-            sl[lane] = 0ull;
-            sl[64 + lane] = 0ull;
-        }
-        for (int q = (int)b; q < ntab; q += (int)G)
-            persist_table_chunk(A, Vold, q / A.nb512, q % A.nb512);
-        if (!grid_barrier(PA.bar, G, PA.result)) return;
-        A.v_old = Vold;
-        A.v_new = Vnew;
-        A.diff = sl;
-        for (int q = (int)b; q < nitem; q += (int)G)
-            bell_tree_item<NP, false, 1, 1, 1, false>(A, ntile, q, nitem);
-        if (!grid_barrier(PA.bar, G, PA.result)) return;
-        if (stop_of(sl)) {  // the same slots, the same decision in every workgroup
-            stopped = true;
-            break;
-        }
-    }
-    if (b == 0 && lane == 0) {
-        PA.result[0] = stopped ? g : PA.max_iter;
-        if (PA.result[1] != 2) PA.result[1] = stopped ? 1 : 0;
-    }
-}
-
-// ------------------------------------------------------------------------------ 3''. quad
-// The bound tree with four lanes per state (A1; the default for integer sigma).  A wave owns
-// 16 consecutive states of row i; lane = st + 16·q holds state st and is sub-lane q of it.
-// Every level of the tree splits its tests over the four sub-lanes — two of each group of eight
-// bounds (superblocks, 64-blocks, 8-blocks) and two of each eight candidates per sub-lane — so
-// one wave-instruction performs 64 state-tests where the one-lane-per-state tree performs 64
-// with a 4x wider union of argmax ranges over its 64 states.  Per-wave latency drops ~4x and
-// four times as many waves fill the SIMDs.  Candidates that pass are evaluated exactly by the
-// lane that tested them (no wave-uniform exact loop).  Each sub-lane keeps its own running
-// (best, first index); the bars are merged across the four sub-lanes between superblocks and
-// at the end with the same order-independent rule, so the result is the plain exhaustive
-// scan's bit for bit (the same exactness argument as the tree: every bound is an upper bound of
-// t_k over its block in floating point, and a candidate whose exact value reaches a lane's
-// running best passes that lane's test).
-template <int NP>
-__global__ __launch_bounds__(64) void bell_quad_kernel(BellArgs A0, int ntile) {
-    const int lane = threadIdx.x & 63;
-    const int st = lane & 15, q4 = lane >> 4;
-    int item = (A0.variant & 16) ? xcd_remap((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
-    BellArgs A = A0;
-    if (A0.C > 1) {
-        const int c = item / (A0.N * ntile);
-        if (A0.stop[c]) return;
-        A = bell_cand(A0, c);
-        item -= c * A0.N * ntile;
-    }
-    const int tile = item % ntile;
-    const int i = item / ntile;
-    const int Na = A.Na;
-    const double* __restrict__ a = A.a;
-    const double* __restrict__ Drow = A.Dt + (size_t)i * Na;
-    const double* __restrict__ ev = A.EV + (size_t)i * Na;
-    const double y = A.w * A.s[i];
-    const int j = tile * 16 + st;
-    const bool ok = j < Na;
-    const size_t t = (size_t)i * Na + (ok ? j : 0);
-    __shared__ double2 s_cand[512];  // the current superblock's staged candidates (a_k, D_k)
-
-    const double x = ok ? (1 + A.r) * a[j] : 0.0;
-    const double coh = x + y;  // Aiyagari_VFI.m:72
-    const int kf = ok ? A.kf[t] : 0;
-    double best = __builtin_nan("");
-    int idx = -1;
-    unsigned nhits = 0, nsup = 0, nblk = 0, nfine = 0;
-    const long long t_start = A.trace ? (long long)wall_clock64() : 0;
-
-    // (max value, first index) over the four sub-lanes of each state
-    auto merge4 = [&]() __attribute__((always_inline)) {
-#pragma unroll
-        for (int off = 16; off <= 32; off <<= 1) {
-            const double ob = __shfl_xor(best, off);
-            const int oq = __shfl_xor(idx, off);
-            if (oq >= 0) lexi_take(ob, oq, best, idx);
-        }
-    };
-    auto evalk = [&](int k) __attribute__((always_inline)) {
-        return bell_val<NP, false>(coh - a[k], ev[k], A.sigma, 0.0);
-    };
-    if (A.hint) {
-        const int h = ok ? A.hint[t] : -1;
-        const int hk = (h >= 0 && kf > 0) ? min(h, kf - 1) : -1;
-        if (hk >= 0) {  // sub-lanes 0..2 evaluate hint-1, hint, hint+1
-            const int k = hk - 1 + q4;
-            if (q4 < 3 && k >= 0 && k < kf) lexi_take(evalk(k), k, best, idx);
-        }
-        merge4();
-        if (hk >= 0 && idx >= 0 && idx != hk && !(A.variant & 32)) {
-            // climb (see bell_tree_kernel), redundantly in the four sub-lanes
-            const int dir = idx > hk ? 1 : -1;
-            int k = idx, step = 2;
-            for (;;) {
-                const int kn = min(max(k + dir * step, 0), kf - 1);
-                if (kn == k || !lexi_take(evalk(kn), kn, best, idx)) break;
-                k = kn;
-                step <<= 1;
-            }
-            for (int s2 = step >> 1; s2 >= 1; s2 >>= 1) {
-                const int c0 = idx;
-                if (c0 + s2 < kf) lexi_take(evalk(c0 + s2), c0 + s2, best, idx);
-                if (c0 - s2 >= 0) lexi_take(evalk(c0 - s2), c0 - s2, best, idx);
-            }
-        }
-    } else if (ok) {
-        best = A.best0[t];
-        idx = A.idx0[t] == -2 ? -1 : A.idx0[t];
-    }
-    double B;
-    auto set_B = [&]() __attribute__((always_inline)) {
-        B = ok ? screen_B(best, idx, 0.0, NP) : __builtin_nan("");  // invalid: every test false
-    };
-    set_B();
-
-    int kg = kf;  // the wave's feasible range
-    for (int off = 1; off < 16; off <<= 1) kg = max(kg, __shfl_xor(kg, off));
-    kg = readfirst(kg);
-
-    // Eight bounds per call, two per sub-lane: position u = q4 + 4p (p = 0, 1) reads lane
-    // base + stride·u of (dv, av) = (Dmax, a at the block start).  Bit u of the result is set
-    // when some state passes bound u (u < cnt).
-    auto qmask8 = [&](double dv, double av, int base, int stride, int cnt, unsigned& ctr)
-                      __attribute__((always_inline)) {
-        double tm[2];
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            const int u = q4 + 4 * p;
-            const int ln = min(base + stride * u, 63);
-            const double dmax = __shfl(dv, ln), a0 = __shfl(av, ln);
-            const double tt = (dmax - B) * aiy_ipow(fmax(coh - a0, 0.0), NP);
-            tm[p] = u < cnt ? tt : -__builtin_inf();
-        }
-        if (A.hitcount && ok) ctr += (q4 < cnt) + (q4 + 4 < cnt);
-        const unsigned long long b0 = __ballot(tm[0] >= kThr), b1 = __ballot(tm[1] >= kThr);
-        unsigned m = 0;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            m |= ((b0 >> (16 * s)) & 0xffffull) ? 1u << s : 0u;
-            m |= ((b1 >> (16 * s)) & 0xffffull) ? 1u << (s + 4) : 0u;
-        }
-        return m;
-    };
-    // candidates [k0, k1), k1 - k0 <= 8, staged in LDS: sub-lane q4 tests k0 + 2·q4 + {0, 1};
-    // a candidate that passes is evaluated exactly by its own lane (MATLAB order) and merged
-    auto fine = [&](int sbase, int k0, int k1) __attribute__((always_inline)) {
-        double tm[2], cc[2];
-        int kk[2];
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            kk[p] = k0 + 2 * q4 + p;
-            const double2 tk = s_cand[min(kk[p], k1 - 1) - sbase];
-            cc[p] = coh - tk.x;
-            const double tt = (tk.y - B) * aiy_ipow(fmax(cc[p], 0.0), NP);
-            tm[p] = (kk[p] >= k1 || kk[p] == idx) ? -__builtin_inf() : tt;
-        }
-        if (A.hitcount && ok) nfine += (kk[0] < k1) + (kk[1] < k1);
-        if (!__any(tm[0] >= kThr || tm[1] >= kThr)) return;
-        bool upd = false;
-#pragma unroll
-        for (int p = 0; p < 2; ++p)
-            if (tm[p] >= kThr && cc[p] > 0) {
-                ++nhits;
-                upd |= lexi_take(bell_val<NP, false>(cc[p], ev[kk[p]], A.sigma, 0.0), kk[p], best, idx);
-            }
-        if (upd) set_B();
-    };
-    auto superblock = [&](int sb) __attribute__((always_inline)) {
-        const int sbase = sb << 9;
-        const int sub = (sbase >> 3) + lane;
-        const bool oku = sub < A.nb8;
-        const double dm8 = oku ? A.Dm8[(size_t)i * A.nb8 + sub] : -__builtin_inf();
-        const double a8 = oku ? a[sub << 3] : 0.0;
-        double dm64 = dm8;
-        dm64 = fmax(dm64, __shfl_xor(dm64, 1));
-        dm64 = fmax(dm64, __shfl_xor(dm64, 2));
-        dm64 = fmax(dm64, __shfl_xor(dm64, 4));
-        const int nblock = min(8, (kg - sbase + 63) >> 6);
-        const unsigned bpass = qmask8(dm64, a8, 0, 8, nblock, nblk);
-        unsigned long long pass = 0;  // bit 8b+u: sub-block u of block b passes
-        for (unsigned bm = bpass; bm; bm &= bm - 1) {
-            const int b = __builtin_ctz(bm);
-            const int nsub = min(8, (kg - (sbase + (b << 6)) + 7) >> 3);
-            pass |= (unsigned long long)qmask8(dm8, a8, 8 * b, 1, nsub, nblk) << (8 * b);
-        }
-        if (!pass) return;
-#pragma unroll
-        for (int b = 0; b < 8; ++b)  // all loads issued before any is used
-            if ((pass >> (8 * b)) & 0xffull) {
-                const int k = min(sbase + (b << 6) + lane, Na - 1);
-                s_cand[(b << 6) + lane] = make_double2(a[k], Drow[k]);
-            }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        for (unsigned long long pm = pass; pm; pm &= pm - 1) {
-            const int k0 = sbase + (__builtin_ctzll(pm) << 3);
-            fine(sbase, k0, min(k0 + 8, kg));
-        }
-        __builtin_amdgcn_wave_barrier();  // reads done before the next superblock's writes
-        merge4();
-        set_B();
-    };
-
-    if (kg > 0) {
-        const int nsb = (kg + 511) >> 9;
-        int sfirst = -1;  // best first: the superblock holding the first state's current argmax
-        {
-            const unsigned long long m = __ballot(idx >= 0);
-            if (m) sfirst = min(readlane_i(idx, __builtin_ctzll(m)) >> 9, nsb - 1);
-        }
-        if (sfirst >= 0) superblock(sfirst);
-        for (int g = 0; g < nsb; g += 64) {
-            const int sbl = g + lane;
-            const bool oks = sbl < nsb;
-            const double dm0 = oks ? A.Dm512[(size_t)i * A.nb512 + sbl] : -__builtin_inf();
-            const double a0 = oks ? a[sbl << 9] : 0.0;
-            const int ns = min(64, nsb - g);
-            for (int s8 = 0; s8 < ns; s8 += 8) {
-                const int cnt = min(8, ns - s8);
-                unsigned m = qmask8(dm0, a0, s8, 1, cnt, nsup);
-                if (sfirst >= g + s8 && sfirst < g + s8 + 8) m &= ~(1u << (sfirst - g - s8));
-                for (; m; m &= m - 1) superblock(g + s8 + __builtin_ctz(m));
-            }
-        }
-    }
-    merge4();
-
-    // outputs (sub-lane 0): Aiyagari_VFI.m:79-81
-    bool okd = false;
-    double dmax = 0.0;
-    if (ok && q4 == 0) {
-        double b = best;
-        int qq = idx;
-        if (qq < 0) {  // all candidates NaN: max returns NaN at index 1
-            qq = 0;
-            b = __builtin_nan("");
-        }
-        const double kp = a[qq];
-        A.idx[t] = qq;
-        if (A.pk) A.pk[t] = kp;
-        if (A.pc) A.pc[t] = coh - kp;
-        A.v_new[t] = b;
-        const double d = fabs(b - A.v_old[t]);
-        if (d == d) {
-            dmax = d;
-            okd = true;
-        }
-    }
-    block_max_to_slots(okd, dmax, A.diff);
-    if (A.hitcount || A.trace) {  // instrumentation: per-state test counts, summed over the wave
-        unsigned c4[4] = {nhits, nsup, nblk, nfine};
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-            for (int off = 32; off > 0; off >>= 1) c4[c] += __shfl_xor(c4[c], off);
-        if (A.hitcount && lane == 0) {
-            unsigned long long* hc = A.hitcount + 4 * (blockIdx.x % kDiffSlots);
-            for (int c = 0; c < 4; ++c)
-                if (c4[c]) atomicAdd(hc + c, (unsigned long long)c4[c]);
-        }
-        if (A.trace && lane == 0) {
-            long long* tr = A.trace + 16 * (size_t)item;
-            tr[0] = t_start;
-            tr[1] = (long long)wall_clock64();
-            tr[2] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));  // HW_REG_XCC_ID
-            for (int c = 0; c < 4; ++c) tr[3 + c] = c4[(c + 1) & 3];
-            tr[7] = blockIdx.x;
-            for (int c = 8; c < 16; ++c) tr[c] = 0;
-        }
-    }
+    bell_tree_item<NP, LAB, R, LB, W, INS>(A0, ntile, (int)blockIdx.x, (int)gridDim.x);
 }
 
 // ------------------------------------------------------------------------------ 4. merge
@@ -2189,17 +1677,7 @@ __global__ __launch_bounds__(256) void bell_plain_kernel(BellArgs A) {
 // ------------------------------------------------------------------------------ launchers
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
-thread_local DispatchEvents g_dispatch_ev;
-template <class K, class... Args>
-static void launch_dispatch_timed(K kernel, int grid, int block, hipStream_t st, Args... args) {
-    if (g_dispatch_ev.start) {
-        hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(block), 0, st, g_dispatch_ev.start,
-                              g_dispatch_ev.stop, 0, args...);
-        g_dispatch_ev = DispatchEvents{};
-    } else {
-        kernel<<<grid, block, 0, st>>>(args...);
-    }
-}
+thread_local DispatchEvents g_dispatch_ev;  // (dispatch.hpp)
 
 int launch_bell_ev_mfma(const BellArgs& A, hipStream_t st) {
     const dim3 grid(cdiv(A.Na, 64), cdiv(A.N, 16), std::max(A.C, 1));
@@ -2234,41 +1712,6 @@ int launch_bell_kf(const BellArgs& A, hipStream_t st) {
 #ifndef AIY_BELL_R
 #define AIY_BELL_R 2
 #endif
-bool bell_persist_eligible(const BellArgs& A) {
-    return A.np >= 1 && A.np <= 8 && !A.labor && A.C <= 1 && A.tree && A.Na <= 4096 && !A.ev_mfma &&
-           A.Dt && A.Dm8 && A.Dm512 && !A.hitcount && !A.trace;
-}
-
-template <int NP>
-static int persist_go(const PersistArgs& PA, hipStream_t st) {
-    const int ntile = (PA.A.Na + 63) / 64;
-    const int items = std::max(PA.A.N * ntile, PA.A.N * PA.A.nb512);
-    int dev = 0, cus = 0, per_cu = 0;
-    AIY_HIP(hipGetDevice(&dev));
-    AIY_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    AIY_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bell_persist_kernel<NP>, 64, 0));
-    const int grid = std::min(items, std::max(1, per_cu * cus / 8));  // workgroups on XCD 0
-    PersistArgs a = PA;
-    void* args[] = {&a};
-    AIY_HIP(hipLaunchCooperativeKernel((const void*)bell_persist_kernel<NP>, dim3(8 * grid),
-                                       dim3(64), args, 0, st));
-    return AIY_OK;
-}
-
-int launch_bell_persist(const PersistArgs& PA, hipStream_t st) {
-    if (!bell_persist_eligible(PA.A)) return fail(AIY_BAD_ARG, "persistent solve: ineligible sweep");
-    switch (PA.A.np) {
-        case 1: return persist_go<1>(PA, st);
-        case 2: return persist_go<2>(PA, st);
-        case 3: return persist_go<3>(PA, st);
-        case 4: return persist_go<4>(PA, st);
-        case 5: return persist_go<5>(PA, st);
-        case 6: return persist_go<6>(PA, st);
-        case 7: return persist_go<7>(PA, st);
-        default: return persist_go<8>(PA, st);
-    }
-}
-
 template <int NP, bool LAB>
 struct Geo {
     static constexpr int R = LAB ? 1 : AIY_BELL_R;
@@ -2307,18 +1750,12 @@ static void tree_geo(const BellArgs& A, hipStream_t st) {
     constexpr int LB = LAB ? 5 : 1;
     const int ntile = cdiv(A.Na, 64 * R);
     const int grid = std::max(A.C, 1) * A.N * ntile;
-    if constexpr (R == 1 && W == 1 && !LAB) {  // chained sweeps: the epilogue instantiation
-        if (A.nEV) {
-            launch_dispatch_timed(bell_tree_kernel<NP, LAB, R, LB, W, false, true>, grid, 64 * W,
-                                  st, A, ntile);
-            return;
-        }
-    }
     if (A.trace || A.hitcount)
-        launch_dispatch_timed(bell_tree_kernel<NP, LAB, R, LB, W, true>, grid, 64 * W, st, A, ntile);
+        launch_dispatch_timed(bell_tree_kernel<NP, LAB, R, LB, W, true>, dim3(grid), dim3(64 * W),
+                              0, st, A, ntile);
     else
-        launch_dispatch_timed(bell_tree_kernel<NP, LAB, R, LB, W, false>, grid, 64 * W, st, A,
-                              ntile);
+        launch_dispatch_timed(bell_tree_kernel<NP, LAB, R, LB, W, false>, dim3(grid),
+                              dim3(64 * W), 0, st, A, ntile);
 }
 // variant bit 0: 2 states per lane (A1 only); bits 1-2: waves per tile 1 (default), 2, 4, 8
 template <int NP, bool LAB, int R>
@@ -2332,14 +1769,6 @@ static void tree_w(const BellArgs& A, hipStream_t st) {
 }
 template <int NP, bool LAB>
 static void run_tree(const BellArgs& A, hipStream_t st) {
-    if constexpr (NP > 0 && !LAB) {
-        if (A.variant & 64) {  // four lanes per state, 16 states per wave
-            const int ntile = cdiv(A.Na, 16);
-            launch_dispatch_timed(bell_quad_kernel<NP>, std::max(A.C, 1) * A.N * ntile, 64, st, A,
-                                  ntile);
-            return;
-        }
-    }
     if constexpr (NP > 0) {
         // the tuning geometries are instantiated for the reference sigma = 5 (NP = 4) only
         if constexpr (!LAB && NP == 4) {

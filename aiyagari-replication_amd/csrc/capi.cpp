@@ -97,6 +97,19 @@ int ws_timing_end(aiy_ws* ws, hipStream_t st) {
     ws->ev_used++;
     return AIY_OK;
 }
+// dispatch-recorded events (dispatch.hpp) for the next timed launch on this thread; call
+// ws_dispatch_commit after the launch whatever it returned
+int ws_dispatch_arm(aiy_ws* ws) {
+    if (!ws->timing) return AIY_OK;
+    if (ws->ev_used == (int)ws->ev_start.size()) AIY_TRY(ws_timing_drain(ws));
+    g_dispatch_ev = DispatchEvents{ws->ev_start[ws->ev_used], ws->ev_stop[ws->ev_used]};
+    return AIY_OK;
+}
+void ws_dispatch_commit(aiy_ws* ws) {
+    if (!ws->timing) return;
+    if (!g_dispatch_ev.start) ws->ev_used++;  // the launch consumed (recorded) them
+    g_dispatch_ev = DispatchEvents{};
+}
 int ws_timing_drain(aiy_ws* ws) {
     for (int q = 0; q < ws->ev_used; ++q) {
         AIY_HIP(hipEventSynchronize(ws->ev_stop[q]));
@@ -213,30 +226,6 @@ static int bell_args(aiy_ws* ws, const BellCall& c, BellArgs& A, hipStream_t st)
     return AIY_OK;
 }
 
-// Chained sweeps need the one-wave-per-tile A1 tree kernel (its chained instantiation carries
-// the next-table epilogue) and the VALU expectation the epilogue restates.
-static bool bell_chain_eligible(const BellArgs& A) {
-    return A.tree && !A.labor && A.np >= 1 && A.np <= 8 && A.C <= 1 && !A.ev_mfma &&
-           A.N <= kChainMaxN && (A.variant & (1 | 6 | 8 | 64 | 1024)) == 0;
-}
-static int ws_ensure_chain(aiy_ws* ws) {
-    const size_t n = (size_t)ws->N * ws->Na, nb = (size_t)ws->N * ((ws->Na + 63) / 64);
-    if (!ws->tcnt) {
-        AIY_TRY(dalloc(&ws->cEV, n));
-        AIY_TRY(dalloc(&ws->cDt, n));
-        AIY_TRY(dalloc(&ws->cDm8, (size_t)ws->N * ((ws->Na + 7) / 8)));
-        AIY_TRY(dalloc(&ws->cDm64, nb));
-        AIY_TRY(dalloc(&ws->zsets, 3 * 2 * (size_t)kDiffSlots));
-        AIY_TRY(dalloc(&ws->tcnt, (size_t)(ws->Na + 63) / 64));
-        AIY_HIP(hipMemset(ws->zsets, 0, 3 * 2 * kDiffSlots * sizeof(unsigned long long)));
-        AIY_HIP(hipMemset(ws->tcnt, 0, (ws->Na + 63) / 64 * sizeof(unsigned)));
-    }
-    return AIY_OK;
-}
-static unsigned long long* chain_set(aiy_ws* ws, int64_t g) {
-    return ws->zsets + (size_t)(((g % 3) + 3) % 3) * 2 * kDiffSlots;
-}
-
 int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
     BellArgs A;
     AIY_TRY(bell_args(ws, c, A, st));
@@ -244,48 +233,16 @@ int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
     // by the scan itself); otherwise the bound tree (or the chunked screen, variant bit 3)
     const bool exhaustive = c.mode == 2 || A.np == 0 || (A.variant & 1024);
     const bool screened = !exhaustive;
-    // chained sweep g: table set g & 1 (set 0 = EV/Dt/Dm8 and the 64-block maxima in Dm), the
-    // next one built into set (g+1) & 1 by the tree kernel; diff slots from the ring of three
-    const bool chained = c.chain && screened && bell_chain_eligible(A);
-    const int64_t g = c.chain_g;
-    if (chained) {
-        AIY_TRY(ws_ensure_chain(ws));
-        double* EVs[2] = {ws->EV, ws->cEV};
-        double* Dts[2] = {ws->Dt, ws->cDt};
-        double* D8s[2] = {ws->Dm8, ws->cDm8};
-        double* D64s[2] = {ws->Dm, ws->cDm64};
-        const int cs = (int)(g & 1), ns = cs ^ 1;
-        A.EV = EVs[cs]; A.Dt = Dts[cs]; A.Dm8 = D8s[cs]; A.Dm64 = D64s[cs];
-        A.diff = chain_set(ws, g);
-        if (g == 0) {  // the chain's first table: the table kernel (clears set 0, folds nothing)
-            BellArgs T = A;
-            T.Dm = D64s[cs];
-            T.fold = nullptr;
-            AIY_TRY(launch_bell_table(T, st));
-        }
-        A.nEV = EVs[ns]; A.nDt = Dts[ns]; A.nDm8 = D8s[ns]; A.nDm64 = D64s[ns];
-        A.tcnt = ws->tcnt;
-        A.fsrc = (g > 0 && A.fold) ? chain_set(ws, g - 1) : nullptr;
-        if (!A.fsrc) A.fold = nullptr;
-        A.clr = chain_set(ws, g + 1);
-    } else {
-        AIY_TRY(launch_bell_table(A, st));  // also clears the diff slots
-    }
+    AIY_TRY(launch_bell_table(A, st));  // also clears the diff slots
     if (!screened) A.coarse = 0, A.hint = nullptr;
     if (screened && A.tree) {
         // tree screen: the hint (or, cold, the init kernel's candidate) sets the first bar;
         // the tree kernel writes the outputs itself
         if (!A.hint) AIY_TRY(launch_bell_init(A, st));
-        if (ws->timing) {  // events recorded by the dispatch itself (g_dispatch_ev)
-            if (ws->ev_used == (int)ws->ev_start.size()) AIY_TRY(ws_timing_drain(ws));
-            g_dispatch_ev = DispatchEvents{ws->ev_start[ws->ev_used], ws->ev_stop[ws->ev_used]};
-            const int rc = launch_bell_tree(A, st);
-            g_dispatch_ev = DispatchEvents{};
-            AIY_TRY(rc);
-            ws->ev_used++;
-        } else {
-            AIY_TRY(launch_bell_tree(A, st));
-        }
+        AIY_TRY(ws_dispatch_arm(ws));  // events recorded by the dispatch itself
+        const int rc = launch_bell_tree(A, st);
+        ws_dispatch_commit(ws);
+        AIY_TRY(rc);
     } else if (screened) {
         AIY_TRY(launch_bell_init(A, st));
         AIY_TRY(ws_timing_begin(ws, st));
@@ -297,7 +254,7 @@ int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
         AIY_TRY(launch_bell_plain(A, st));
         AIY_TRY(ws_timing_end(ws, st));
     }
-    if (c.diff_out) AIY_TRY(launch_reduce_slots(chained ? A.diff : ws->diff, c.diff_out, st));
+    if (c.diff_out) AIY_TRY(launch_reduce_slots(ws->diff, c.diff_out, st));
     return AIY_OK;
 }
 
@@ -313,7 +270,7 @@ int ws_read_diff(aiy_ws* ws, hipStream_t st, double* d) {
 // A2 with speculative batches.  The one-sweep-at-a-time loop pays a stream synchronisation per
 // sweep to read max|Δv| (at the script's Na = 400 that round trip costs more than the sweep).
 // Here sweeps are enqueued m at a time: sweep g reads ring slot (g−1) mod R and writes slot
-// g mod R (R = spec_max + 1 value buffers), its policies go to set g mod spec_max, its folded
+// g mod R (R = 2·spec_max + 1 value buffers), its policies go to set g mod 2·spec_max, its folded
 // diff to its own slot, and one D2H read per batch finds the first sweep below tol.  Sweeps
 // are deterministic and each depends only on its predecessor, so sweeps 1..g* are exactly the
 // ones the plain loop runs; later sweeps of the batch are discarded and the ring still holds
@@ -400,9 +357,6 @@ static int bell_solve_spec(aiy_ws* ws, BellCall c, double* v_a, double* v_b, dou
             // or by a reduce launch after the batch's last sweep
             c.prev_diff_out = t ? dslot(g - 1) : nullptr;
             c.diff_out = (t == m - 1) ? reinterpret_cast<double*>(dslot(g)) : nullptr;
-            // one chain per solve: sweep g reads vslot(g-1), the previous sweep's own output
-            c.chain = ws->chain;
-            c.chain_g = g - 1;
             AIY_TRY(bell_sweep_dev(ws, c, st));
         }
         unsigned long long* h = ws->spec_hdiff + (size_t)hb_next * 2 * D;
@@ -452,67 +406,15 @@ static int bell_solve_spec(aiy_ws* ws, BellCall c, double* v_a, double* v_b, dou
     return AIY_OK;
 }
 
-// A2 on small grids: sweep 1 through the ordinary launches (cold start, cached feasible
-// prefixes), then sweeps 2..max_iter in one persistent cooperative launch that tests the stop
-// rule itself (bell_persist_kernel).  Same buffers and results as the plain loop: sweep g
-// writes buf[g & 1] (buf = {v_a, v_b}), idx/pk/pc hold the stopping sweep's policies, and on
-// exhaustion v_old = v_new.  Returns kNotApplicable when the sweep is not eligible.
-static constexpr int kNotApplicable = -1;
-static int bell_solve_persist(aiy_ws* ws, const BellCall& c, double* v_a, double* v_b,
-                              double tol, int64_t max_iter, int64_t* iters, int* out_new,
-                              hipStream_t st) {
-    BellCall c1 = c;
-    c1.keep_incoming = true;
-    c1.v_old = v_a;
-    c1.v_new = v_b;
-    BellArgs A;
-    AIY_TRY(bell_args(ws, c1, A, st));
-    if (c.mode == 2 || !bell_persist_eligible(A)) return kNotApplicable;
-    if (!ws->pers) AIY_TRY(dalloc(&ws->pers, 4 * (size_t)kDiffSlots + 8));
-    AIY_TRY(bell_sweep_dev(ws, c1, st));  // sweep 1
-    PersistArgs PA{};
-    PA.A = A;
-    PA.A.hint = c.idx;  // sweep g >= 2: the previous sweep's argmax
-    PA.A.keep_incoming = false;
-    PA.A.fold = nullptr;
-    PA.V0 = v_a;
-    PA.V1 = v_b;
-    PA.first = ws->diff;
-    PA.slots = ws->pers;
-    PA.bar = reinterpret_cast<unsigned*>(ws->pers + 4 * kDiffSlots);
-    PA.result = reinterpret_cast<long long*>(ws->pers + 4 * kDiffSlots + 2);
-    PA.tol = tol;
-    PA.g0 = 1;
-    PA.max_iter = max_iter;
-    AIY_HIP(hipMemsetAsync(ws->pers + 4 * kDiffSlots, 0, 8 * sizeof(unsigned long long), st));
-    AIY_TRY(launch_bell_persist(PA, st));
-    long long res[2] = {0, 0};
-    AIY_HIP(hipMemcpyAsync(res, PA.result, sizeof res, hipMemcpyDeviceToHost, st));
-    AIY_HIP(hipStreamSynchronize(st));
-    if (res[1] == 2) return fail(AIY_HIP_ERROR, "persistent solve: grid barrier timed out");
-    const int64_t g = res[0];
-    double* vnew = (g & 1) ? v_b : v_a;
-    if (res[1] == 0)  // exhausted: v_old = v_new after the last sweep (Aiyagari_VFI.m:88)
-        AIY_HIP(hipMemcpyAsync((g & 1) ? v_a : v_b, vnew, sizeof(double) * ws->N * ws->Na,
-                               hipMemcpyDeviceToDevice, st));
-    *iters = g;
-    *out_new = (g & 1) ? 1 : 0;
-    return AIY_OK;
-}
-
 int bell_solve_dev(aiy_ws* ws, BellCall c, double* v_a, double* v_b, double tol,
                    int64_t max_iter, int64_t* iters, int* out_new, hipStream_t st) {
     if (max_iter < 1) return fail(AIY_BAD_ARG, "max_iter must be >= 1");
     if (!c.idx) return fail(AIY_BAD_ARG, "NULL device pointer");
-    if (ws && ws->spec_max > 1 && !c.diff_out && ws->variant < 0 && ws->persist &&
-        !ws->timing && !ws->count_hits && !ws->tracing && !c.labor) {
-        const int rc = bell_solve_persist(ws, c, v_a, v_b, tol, max_iter, iters, out_new, st);
-        if (rc != kNotApplicable) return rc;
-    }
     if (ws && ws->spec_max > 1 && !c.diff_out) {
-        // rings: (spec_max + 1) value buffers + spec_max sets of idx and 3 policies
-        const size_t n = (size_t)ws->N * ws->Na;
-        const size_t bytes = ((size_t)ws->spec_max * 4 + 1) * n * sizeof(double);
+        // rings (two batches in flight, bell_solve_spec): 2M + 1 value buffers, 2M idx slots
+        // and 2M x 3 policy slots, M = spec_max
+        const size_t n = (size_t)ws->N * ws->Na, M2 = 2 * (size_t)ws->spec_max;
+        const size_t bytes = ((M2 + 1) + 3 * M2) * n * sizeof(double) + M2 * n * sizeof(int);
         if (bytes <= ((size_t)8 << 30)) {
             int rc = bell_solve_spec(ws, c, v_a, v_b, tol, max_iter, iters, out_new, st);
             if (rc != AIY_NO_MEMORY) return rc;
@@ -784,15 +686,8 @@ int aiy_ws_invalidate(aiy_ws* ws) {
 
 int aiy_ws_set_variant(aiy_ws* ws, int variant) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
-    if (variant < -1 || variant > 262143) return fail(AIY_BAD_ARG, "variant in [-1, 262143]");
+    if (variant < -1 || variant >= (1 << 21)) return fail(AIY_BAD_ARG, "variant in [-1, 2^21)");
     ws->variant = variant;
-    return AIY_OK;
-}
-
-int aiy_ws_set_persistent(aiy_ws* ws, int persistent) {
-    if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
-    if (persistent != 0 && persistent != 1) return fail(AIY_BAD_ARG, "persistent must be 0 or 1");
-    ws->persist = persistent != 0;
     return AIY_OK;
 }
 
@@ -846,18 +741,9 @@ int aiy_vfi_sweeps_dev(aiy_ws* ws, double* v_a, double* v_b, const double* a_gri
         c.v_old = (g & 1) ? v_b : v_a;
         c.v_new = (g & 1) ? v_a : v_b;
         c.hint = g ? idx : hint;
-        c.chain = ws->chain;
-        c.chain_g = g;
         c.diff_out = (g == nsweeps - 1) ? diff : nullptr;
         AIY_TRY(bell_sweep_dev(ws, c, (hipStream_t)stream));
     }
-    return AIY_OK;
-}
-
-int aiy_ws_set_chain(aiy_ws* ws, int on) {
-    if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
-    if (on != 0 && on != 1) return fail(AIY_BAD_ARG, "chain must be 0 or 1");
-    ws->chain = on != 0;
     return AIY_OK;
 }
 

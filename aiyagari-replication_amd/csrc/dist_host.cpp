@@ -160,9 +160,10 @@ int dist_stationary_dev(aiy_ws* ws, const double* lam0, const int* idx, const do
             // push g's set was zeroed by push g−1 (one-launch push) or is zeroed here
             if (two_launch) AIY_HIP(hipMemsetAsync(sset(g), 0, SW * sizeof(unsigned long long), st));
             else A.diff_clear = sset(g + 1);
-            AIY_TRY(ws_timing_begin(ws, st));
-            AIY_TRY(launch_dist_push(A, fb, st));
-            AIY_TRY(ws_timing_end(ws, st));
+            AIY_TRY(ws_dispatch_arm(ws));  // the push's own duration (one-launch push)
+            const int rc = launch_dist_push(A, fb, st);
+            ws_dispatch_commit(ws);
+            AIY_TRY(rc);
         }
         unsigned long long* h = ws->dist_hslots + (size_t)hb_next * R * SW;
         AIY_HIP(hipMemcpyAsync(h, ws->dist_slots, SB, hipMemcpyDeviceToHost, st));

@@ -21,6 +21,7 @@
 // global memory, then a projection launch — same additions, two launches per push.
 // Fallback (non-monotone policy): one thread per (i,k) scans the row in order, same chunking.
 #include "aiy_common.hpp"
+#include "dispatch.hpp"
 #include "dist.hpp"
 
 #include <algorithm>
@@ -395,8 +396,8 @@ int launch_dist_push(const DistArgs& A, bool fallback, hipStream_t st) {
         DistArgs B = A;
         B.stage = std::min(kDistStage, (65536 / per) & ~63);
         const size_t lds = (size_t)B.stage * per;
-        if (A.lottery) dist_push_kernel<true><<<g, 64 * A.N, lds, st>>>(B);
-        else dist_push_kernel<false><<<g, 64 * A.N, lds, st>>>(B);
+        if (A.lottery) launch_dispatch_timed(dist_push_kernel<true>, dim3(g), dim3(64 * A.N), lds, st, B);
+        else launch_dispatch_timed(dist_push_kernel<false>, dim3(g), dim3(64 * A.N), lds, st, B);
     } else {
         const int g = (n + 255) / 256;
         dist_gather_scan_kernel<<<g, 256, 0, st>>>(A);

@@ -23,10 +23,7 @@ struct EgmArgs {
     unsigned* flags;           // bit 0: a_hat not increasing (small-grid fused step: bit 1 of
                                // the diff slots' second word instead, see egm_fused_kernel)
     bool fused;                // Na <= 1024: one launch per step (egm_fused_kernel)
-    bool onepass;              // Na > 1024: one launch per step (egm_scatter_kernel); `diff`
-                               // must be zero at launch (the previous step cleared it, see
-                               // diff_clear), the flag rides in bit 1 of the slots' second words
-    unsigned long long* diff_clear;  // onepass / chain: the next step's slot set (kEgmSlotWords
+    unsigned long long* diff_clear;  // chain: the next step's slot set (kEgmSlotWords
                                      // words), zeroed by this launch's first workgroup (nullable)
     double* ahat_next;               // chain: step t+1's â and c̃ (the other scratch pair)
     double* cnext_next;

@@ -52,11 +52,6 @@ static int ensure_egm(aiy_ws* ws) {
         AIY_HIP(hipMalloc((void**)&ws->egm_seg, n * sizeof(int)));
         AIY_HIP(hipMemset(ws->egm_seg, 0xff, n * sizeof(int)));  // -1: no hint yet
     }
-    if (!ws->egm_d2) {
-        AIY_HIP(hipMalloc((void**)&ws->egm_d2, 2 * kEgmSlotWords * sizeof(unsigned long long)));
-        AIY_HIP(hipMemset(ws->egm_d2, 0, 2 * kEgmSlotWords * sizeof(unsigned long long)));
-        ws->egm_par = 0;
-    }
     return AIY_OK;
 }
 
@@ -76,15 +71,12 @@ static EgmArgs egm_args(aiy_ws* ws, const double* c, const double* a, const doub
     A.diff = ws->diff;
     A.flags = (unsigned*)ws->gi;
     A.trace = ws->tracing ? ws->trace : nullptr;  // (instrumentation; see ensure_egm)
-    // interp1 segment hints (verified in the kernel; variant bit 14 turns them off, A/B only)
-    A.seg = (ws->variant >= 0 && (ws->variant & 16384)) ? nullptr : ws->egm_seg;
-    // small grids: one launch per step (egm_fused_kernel) unless the tuning variant sets bit 11;
-    // large grids: the two-launch step, or the one-pass egm_scatter_kernel with variant bit 12
-    // (opt-in: a segment owns its queries, and where â_j falls into the dense low end of the
-    // quadratic a_grid one wave owns thousands of them — 35.6 vs 12.1 us per step at
-    // Na = 20,000, profiles/r03_s3b_egm_ab.json)
-    A.fused = !(ws->variant >= 0 && (ws->variant & 2048));
-    A.onepass = A.Na > kEgmFusedMaxNa && ws->variant >= 0 && (ws->variant & 4096);
+    // interp1 segment hints (verified in the kernel; kEgmNoHints turns them off, A/B only)
+    A.seg = egm_knob(ws, kEgmNoHints) ? nullptr : ws->egm_seg;
+    // small grids: one launch per step (egm_fused_kernel) unless kEgmTwoLaunch; large grids:
+    // the two-launch step (the solve loop chains it, egm_solve_spec).  (A one-pass scatter step
+    // was measured slower — 35.6 vs 12.1 us at Na = 20,000, DESIGN.md §5 — and removed.)
+    A.fused = !egm_knob(ws, kEgmTwoLaunch);
     return A;
 }
 
@@ -96,34 +88,20 @@ int egm_step_dev(aiy_ws* ws, const double* c, const double* a, const double* s, 
     if (labor && !(phi == phi && theta == theta)) return fail(AIY_NON_FINITE, "phi/theta");
     AIY_TRY(ensure_egm(ws));
     EgmArgs A = egm_args(ws, c, a, s, P, r, w, beta, sigma, amin, labor, phi, theta, cout, pk, pl);
-    // the two-launch and small-grid steps clear ws->diff and the flag word themselves; the
-    // one-pass scatter step accumulates from its first wave into a slot set the previous
-    // one-pass step (or the allocation) zeroed, and zeroes the other set for the next step
-    ws->egm_cur = ws->diff;
-    if (A.onepass) {
-        ws->egm_cur = ws->egm_d2 + (size_t)ws->egm_par * kEgmSlotWords;
-        A.diff = ws->egm_cur;
-        A.flags = (unsigned*)(ws->egm_cur + 2 * kDiffSlots);
-        A.diff_clear = ws->egm_d2 + (size_t)(ws->egm_par ^ 1) * kEgmSlotWords;
-        ws->egm_par ^= 1;
-    }
+    // the two-launch and small-grid steps clear ws->diff and the flag word themselves
     AIY_TRY(ws_timing_begin(ws, st));
     AIY_TRY(launch_egm_step(A, st));
     AIY_TRY(ws_timing_end(ws, st));
-    if (diff_out) AIY_TRY(launch_reduce_slots(ws->egm_cur, diff_out, st));
+    if (diff_out) AIY_TRY(launch_reduce_slots(ws->diff, diff_out, st));
     return AIY_OK;
 }
 
 // dist of the last step + the non-monotone-grid flag (synchronises)
 static int read_egm(aiy_ws* ws, hipStream_t st, double* d) {
     unsigned long long* h = ws->hdiff;
-    const unsigned long long* src = ws->egm_cur ? ws->egm_cur : ws->diff;
-    AIY_HIP(hipMemcpyAsync(h, src, 2 * kDiffSlots * sizeof(unsigned long long),
+    AIY_HIP(hipMemcpyAsync(h, ws->diff, 2 * kDiffSlots * sizeof(unsigned long long),
                            hipMemcpyDeviceToHost, st));
-    if (src == ws->diff)  // the two-launch step's flag word (one-pass: in the slots)
-        AIY_HIP(hipMemcpyAsync(h + 2 * kDiffSlots, ws->gi, sizeof(int), hipMemcpyDeviceToHost, st));
-    else
-        h[2 * kDiffSlots] = 0;
+    AIY_HIP(hipMemcpyAsync(h + 2 * kDiffSlots, ws->gi, sizeof(int), hipMemcpyDeviceToHost, st));
     AIY_HIP(hipStreamSynchronize(st));
     *d = fold_slots_host(h);
     if (egm_nonmonotone(h, (unsigned)h[2 * kDiffSlots])) return fail_nonmonotone();
@@ -133,8 +111,8 @@ static int read_egm(aiy_ws* ws, hipStream_t st, double* d) {
 // The solve loop (Aiyagari_EGM.m:74-108, labour :67-105) with speculative batches, as the VFI
 // solve (capi.cpp, bell_solve_spec): steps are deterministic, so batches of m steps are
 // enqueued between reads — step g reads ring slot (g−1) mod R and writes slot g mod R, its
-// dist lands in slot set g mod R with its flag word (a one-pass or chained step zeroes set
-// (g+1) mod R for the next step; the sets are zeroed once per solve) — and each batch ends with
+// dist lands in slot set g mod R with its flag word (a chained step zeroes set (g+1) mod R for
+// the next step; the other steps clear their own) — and each batch ends with
 // one D2H copy of the slot sets and an event.  Two batches are in flight: the host reads batch
 // k's dists while batch k+1 runs, so the device never idles at a read; with R = 2M + 1 slots
 // the stopping step's policy_c survives the next batch's writes.  Its policy_k (and policy_l)
@@ -160,11 +138,9 @@ static int egm_solve_spec(aiy_ws* ws, const EgmArgs& A0, double* c0, double tol,
     auto slot = [&](int64_t g) { return ws->egm_ring + (size_t)(g % R) * n; };
     auto sset = [&](int64_t g) { return ws->egm_slots + (size_t)(g % R) * SW; };
     AIY_HIP(hipMemcpyAsync(slot(0), c0, nb, hipMemcpyDeviceToDevice, st));
-    if (A0.onepass) AIY_HIP(hipMemsetAsync(ws->egm_slots, 0, SB, st));
     // chained steps (the default for Na > 1,024): the RHS of step 1 here, then one launch per
     // step — interp1 of step g on â/c̃ pair (g−1) & 1, the RHS of step g+1 into pair g & 1
-    const bool chain = !A0.onepass && !(A0.fused && A0.Na <= kEgmFusedMaxNa) &&
-                       !(ws->variant >= 0 && (ws->variant & 8192));
+    const bool chain = !(A0.fused && A0.Na <= kEgmFusedMaxNa) && !egm_knob(ws, kEgmNoChain);
     if (chain) {
         if (!ws->egm_x2) AIY_HIP(hipMalloc((void**)&ws->egm_x2, nb));
         if (!ws->egm_y2) AIY_HIP(hipMalloc((void**)&ws->egm_y2, nb));
@@ -177,14 +153,17 @@ static int egm_solve_spec(aiy_ws* ws, const EgmArgs& A0, double* c0, double tol,
         A.cout = slot(g);
         A.diff = sset(g);
         A.flags = (unsigned*)(sset(g) + 2 * kDiffSlots);
-        A.diff_clear = A0.onepass ? sset(g + 1) : nullptr;
+        A.diff_clear = nullptr;
         if (!chain) return launch_egm_step(A, st);
         A.ahat = xs[(g - 1) & 1];
         A.cnext = ys[(g - 1) & 1];
         A.ahat_next = xs[g & 1];
         A.cnext_next = ys[g & 1];
         A.diff_clear = sset(g + 1);
-        return launch_egm_chain(A, st);
+        AIY_TRY(ws_dispatch_arm(ws));  // (timing) the chained launch's own duration
+        const int rc = launch_egm_chain(A, st);
+        ws_dispatch_commit(ws);
+        return rc;
     };
     if (chain) {  // step 1's RHS from slot 0; it clears step 1's slot set and flag word
         EgmArgs A = A0;
@@ -257,7 +236,7 @@ static int egm_solve_spec(aiy_ws* ws, const EgmArgs& A0, double* c0, double tol,
         A.cout = slot(g);
         A.diff = sset(g);
         A.flags = (unsigned*)(sset(g) + 2 * kDiffSlots);
-        A.diff_clear = A0.onepass ? sset(g + 1) : nullptr;
+        A.diff_clear = nullptr;
         AIY_TRY(launch_egm_step(A, st));
     }
     *cur_out = g > 0 ? slot(g) : slot(0);

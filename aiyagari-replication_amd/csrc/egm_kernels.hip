@@ -13,6 +13,7 @@
 //   non-increasing â_j (MATLAB's interp1 would sort or error there).
 // HBM-bound: 24 B per state per iteration (c in, c_next out, policy_k out), +8 B with labour.
 #include "aiy_common.hpp"
+#include "dispatch.hpp"
 #include "egm.hpp"
 
 namespace aiy {
@@ -67,7 +68,7 @@ __global__ __launch_bounds__(1024) void egm_rhs_kernel(EgmArgs A) {
         ah = ((cn + ag) - ws) / (1 + A.r);
     }
     A.ahat[(size_t)j * Na + a_i] = ah;
-    A.cnext[(size_t)j * Na + a_i] = cn;
+    if (A.labor) A.cnext[(size_t)j * Na + a_i] = cn;  // (A4 interpolates a_grid, not c̃)
 }
 
 // #{k in [lo, hi) : x[k] <= q} + lo for a per-lane query (binary search, global memory)
@@ -91,10 +92,16 @@ __device__ __forceinline__ int count_le(const double* __restrict__ x, int lo, in
 // the count — and everything after it — is the plain binary search's.
 // interp1 of row j's 64 queries a_grid(a0 .. a0+63), a0 = 64·tile (one wave): writes
 // policy_c_next (cout), policy_k (and policy_l), flags a non-increasing â; returns whether the
-// lane holds a query and sets its |Δc| (d) and policy_c_next (cn).  s_xw: the wave's 256-double
-// LDS window.
+// lane holds a query and sets its |Δc| (d) and policy_c_next (cn).  s_xw / s_yw: the wave's
+// 256-double LDS windows of x = â_j and y (a_grid in A4, c̃_j in A5).
+// Dependent memory rounds per wave (round 4): (1) the two segment hints, with every load that
+// does not depend on them in flight beside them (the query, policy_c for |Δc|, the monotonicity
+// pair); (2) the window of x AND y around the hinted segments; everything after the count comes
+// from LDS.  (Round 3 re-read x[sgi], x[sgi+1], y[sgi], y[sgi+1] from memory after the count —
+// a third dependent round per step.)  Same values, same operations: bit for bit the plain
+// binary search + interpolation.
 __device__ __forceinline__ bool egm_interp_wave(const EgmArgs& A, int j, int tile,
-                                                double* s_xw, double& d, double& cn,
+                                                double* s_xw, double* s_yw, double& d, double& cn,
                                                 long long* cy = nullptr) {
     const int lane = threadIdx.x & 63;
     const int Na = A.Na;
@@ -105,30 +112,42 @@ __device__ __forceinline__ bool egm_interp_wave(const EgmArgs& A, int j, int til
     const size_t t = (size_t)j * Na + (okl ? a_i : a0);
     const double* __restrict__ x = A.ahat + (size_t)j * Na;
     const double* __restrict__ y = A.labor ? A.cnext + (size_t)j * Na : A.a;
+    // round 1: independent loads together
     const double q = A.a[okl ? a_i : a0 + last];
-    // the previous step's segments as hints: the wave stages x over [h_first − 16, h_last + 18)
-    // (h = the first and the last lane's segment) in LDS in one round trip and every lane checks
-    // that its count #{k : x_k <= q} lies inside — x_{lo−1} <= q < x_{hi} — before finishing it
-    // there; if any lane's does not (segments moved further, or no hints yet), the wave runs
-    // the full 64-ary search below.  The count, hence everything after it, is the search's.
-    int sgi = -1;
+    const double c_old = A.c[t];
+    int h0 = -1, h1 = -1;
     if (A.seg) {
-        const int h0 = A.seg[(size_t)j * Na + a0], h1 = A.seg[(size_t)j * Na + a0 + last];
+        h0 = A.seg[(size_t)j * Na + a0];
+        h1 = A.seg[(size_t)j * Na + a0 + last];
+    }
+    // the previous step's segments as hints: the wave stages x and y over [h_first − 16,
+    // h_last + 18) (h = the first and the last lane's segment) in LDS in one round trip and every
+    // lane checks that its count #{k : x_k <= q} lies inside — x_{lo−1} <= q < x_{hi} — before
+    // finishing it there; if any lane's does not (segments moved further, or no hints yet), the
+    // wave runs the full 64-ary search below.  The count, hence everything after it, is the
+    // search's.
+    int sgi = -1, e0 = -1;  // e0: the segment's index in the LDS windows (window path)
+    if (A.seg) {
         const int wlo = max(min(h0, h1) - 16, 0), whi = min(max(h0, h1) + 18, Na);
         if (h0 >= 0 && h1 >= 0 && h0 <= Na - 2 && h1 <= Na - 2 && whi - wlo + 2 <= 256) {
             // s_xw[0] = x_{wlo−1} (−inf at 0), s_xw[1 + u] = x_{wlo+u}, s_xw[n−1] = x_{whi} (+inf
-            // at Na): all loads in flight, then the LDS writes
+            // at Na), s_yw the same y: all loads in flight, then the LDS writes
             const int n = whi - wlo + 2;
-            double v[4];
+            double v[4], vy[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int k = wlo - 1 + u * 64 + lane;
-                v[u] = (u * 64 + lane < n && k >= 0 && k < Na) ? x[k] : 0.0;
+                const bool in = u * 64 + lane < n && k >= 0 && k < Na;
+                v[u] = in ? x[k] : 0.0;
+                vy[u] = in ? y[k] : 0.0;
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int e = u * 64 + lane, k = wlo - 1 + e;
-                if (e < n) s_xw[e] = k < 0 ? -__builtin_inf() : (k >= Na ? __builtin_inf() : v[u]);
+                if (e < n) {
+                    s_xw[e] = k < 0 ? -__builtin_inf() : (k >= Na ? __builtin_inf() : v[u]);
+                    s_yw[e] = vy[u];
+                }
             }
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -144,8 +163,8 @@ __device__ __forceinline__ bool egm_interp_wave(const EgmArgs& A, int j, int til
                 int c = wlo + lo - 1 - 1;  // count − 1
                 c = c < 0 ? 0 : c;
                 sgi = c > Na - 2 ? Na - 2 : c;
+                e0 = sgi - wlo + 1;  // in [0, n − 2]; e0 and e0 + 1 hold real x and y (see DESIGN)
             }
-            __builtin_amdgcn_wave_barrier();  // window reads done before any reuse of s_xw
         }
     }
     if (cy) cy[1] = (long long)__builtin_amdgcn_s_memtime();
@@ -173,6 +192,7 @@ __device__ __forceinline__ bool egm_interp_wave(const EgmArgs& A, int j, int til
     // every lane's count is in [lo0, lo1] (increasing â and queries)
     int cnt;
     const int span = lo1 - lo0;
+    __builtin_amdgcn_wave_barrier();  // (window reads above, if any, are done)
     if (span >= 0 && span <= 256) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -195,14 +215,26 @@ __device__ __forceinline__ bool egm_interp_wave(const EgmArgs& A, int j, int til
     sgi = sgi < 0 ? 0 : sgi;
     sgi = sgi > Na - 2 ? Na - 2 : sgi;
     }
-    if (A.seg && okl) A.seg[t] = sgi;
+    // the hints of the next step: only the tile's first and last lanes' segments are read
+    if (A.seg && okl && (lane == 0 || lane == last)) A.seg[t] = sgi;
     if (cy) cy[2] = (long long)__builtin_amdgcn_s_memtime();
     d = 0.0;
     cn = 0.0;
     if (!okl) return false;
-    const double tt = (q - x[sgi]) / (x[sgi + 1] - x[sgi]);
-    double g = y[sgi] + tt * (y[sgi + 1] - y[sgi]);
-    if (a_i > 0 && !(x[a_i - 1] < x[a_i])) atomicOr(A.flags, 1u);
+    double x0, x1, y0, y1;
+    if (e0 >= 0) {  // from the LDS windows
+        x0 = s_xw[e0];
+        x1 = s_xw[e0 + 1];
+        y0 = s_yw[e0];
+        y1 = s_yw[e0 + 1];
+    } else {
+        x0 = x[sgi];
+        x1 = x[sgi + 1];
+        y0 = y[sgi];
+        y1 = y[sgi + 1];
+    }
+    const double tt = (q - x0) / (x1 - x0);
+    double g = y0 + tt * (y1 - y0);
     const double ws = A.w * A.s[j];
     if (A.labor) {
         if (q < A.amin) g = A.amin;  // :91 (a no-op for a_grid >= amin)
@@ -217,7 +249,7 @@ __device__ __forceinline__ bool egm_interp_wave(const EgmArgs& A, int j, int til
         cn = ((1 + A.r) * q + ws) - g;  // :102
     }
     A.cout[t] = cn;
-    d = fabs(cn - A.c[t]);
+    d = fabs(cn - c_old);
     if (cy) {
         __builtin_amdgcn_s_waitcnt(0);  // (instrumentation) the loads above have landed
         cy[3] = (long long)__builtin_amdgcn_s_memtime();
@@ -239,8 +271,18 @@ __device__ __forceinline__ void egm_trace(const EgmArgs& A, int rec, long long t
     tr[2 + ncy] = now - cy[ncy - 1];
 }
 
+// interp1 needs an increasing â_j: a non-increasing adjacent pair of the wave's 64 nodes sets
+// the flag word (the reference's interp1 would sort or fail, Aiyagari_EGM.m:95).  Issued at the
+// end of the kernels, off the interpolation's dependent rounds.
+__device__ __forceinline__ void egm_flag_order(const EgmArgs& A, int j, int tile) {
+    const int a_i = tile * 64 + (threadIdx.x & 63);
+    const double* __restrict__ x = A.ahat + (size_t)j * A.Na;
+    if (a_i > 0 && a_i < A.Na && !(x[a_i - 1] < x[a_i])) atomicOr(A.flags, 1u);
+}
+
 __global__ __launch_bounds__(256) void egm_interp_kernel(EgmArgs A, int ntile) {
     __shared__ double s_x[4][256];
+    __shared__ double s_y[4][256];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wv = blockIdx.x * 4 + wave;
     bool ok = false;
@@ -250,7 +292,9 @@ __global__ __launch_bounds__(256) void egm_interp_kernel(EgmArgs A, int ntile) {
     if (wv < A.N * ntile) {  // wave-uniform
         const int j = wv / ntile, tile = wv - j * ntile;
         double cn;
-        ok = egm_interp_wave(A, j, tile, s_x[wave], d, cn, A.trace ? cy : nullptr) && d == d;
+        ok = egm_interp_wave(A, j, tile, s_x[wave], s_y[wave], d, cn, A.trace ? cy : nullptr) &&
+             d == d;
+        egm_flag_order(A, j, tile);
     }
     block_max_to_slots(ok, d, A.diff);
     if (A.trace && wv < A.N * ntile) egm_trace(A, wv, t_in, cy, 4);
@@ -264,8 +308,13 @@ __global__ __launch_bounds__(256) void egm_interp_kernel(EgmArgs A, int ntile) {
 // interp1 of step t+1 then runs in the next launch, after every â of step t+1 exists.  Same
 // operations on the same values as rhs + interp, so bit for bit the two-launch step.  The first
 // workgroup clears step t+1's slot set and flag word (diff_clear) for the next launch.
+// TR: the instrumented instantiation (per-wave phase trace, aiy_ws_set_timing bit 2); the
+// production one has no trace plumbing at all — a runtime-selected pointer to the cycle stamps
+// had put them (and 144 B per lane) in scratch memory.
+template <bool TR>
 __global__ __launch_bounds__(1024) void egm_chain_kernel(EgmArgs A) {
     __shared__ double s_x[16][256];
+    __shared__ double s_y[16][256];
     __shared__ double s_up[16][64];
     const int lane = threadIdx.x & 63;
     const int m = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // blockDim = 64·N
@@ -279,8 +328,8 @@ __global__ __launch_bounds__(1024) void egm_chain_kernel(EgmArgs A) {
     for (int q = 0; q < 16; ++q) pj[q] = q < N ? coef0 * A.P[j * N + q] : 0.0;
     double d, cn;
     long long cy[4] = {0, 0, 0, 0};
-    const long long t_in = A.trace ? (long long)wall_clock64() : 0;
-    const bool okl = egm_interp_wave(A, j, blockIdx.x, s_x[m], d, cn, A.trace ? cy : nullptr);
+    const long long t_in = TR ? (long long)wall_clock64() : 0;
+    const bool okl = egm_interp_wave(A, j, blockIdx.x, s_x[m], s_y[m], d, cn, TR ? cy : nullptr);
     const bool ok = okl && d == d;
     // step t+1's Euler RHS on this tile: u'(policy_c_next) of every row through LDS
     const int a_i = blockIdx.x * 64 + lane;
@@ -293,7 +342,7 @@ __global__ __launch_bounds__(1024) void egm_chain_kernel(EgmArgs A) {
             if (q < N) acc = acc + pj[q] * s_up[q][lane];
         const double c2 = aiy_pow(acc, -1.0 / A.sigma);  // :88
         const double ws = A.w * A.s[j];
-        const double ag = A.a[a_i];
+        const double ag = A.a[a_i];  // (the interp query: an L1 hit)
         double ah;
         if (A.labor) {
             const double ls = labor_dev(c2, ws, A.sigma, A.ns, A.phi, A.theta);
@@ -302,10 +351,11 @@ __global__ __launch_bounds__(1024) void egm_chain_kernel(EgmArgs A) {
             ah = ((c2 + ag) - ws) / (1 + A.r);
         }
         A.ahat_next[(size_t)j * Na + a_i] = ah;
-        A.cnext_next[(size_t)j * Na + a_i] = c2;
+        if (A.labor) A.cnext_next[(size_t)j * Na + a_i] = c2;  // (A4 interpolates a_grid, not c̃)
     }
     block_max_to_slots(ok, d, A.diff);
-    if (A.trace) egm_trace(A, blockIdx.x * N + j, t_in, cy, 4);
+    egm_flag_order(A, j, blockIdx.x);
+    if constexpr (TR) egm_trace(A, blockIdx.x * N + j, t_in, cy, 4);
 }
 
 // Small grids (the scripts' Na = 400, up to 1,024): one launch per step, one workgroup per productivity
@@ -416,216 +466,6 @@ __global__ __launch_bounds__(1024) void egm_fused_kernel(EgmArgs A) {
     }
 }
 
-// Large grids: one launch per step by inverting the search.  interp1's segment of query a_i
-// in the monotone â_j is k iff â_k <= a_i < â_{k+1} (k = 0 takes every a_i < â_1, k = Na−2
-// every a_i >= â_{Na−2}: the clamps of seg_of_dev), so the queries of segment k are the index
-// range [B_k, B_{k+1}) with B_k = #{i : a_i < â_k} — a search of the FIXED a_grid, not of
-// â_j.  A workgroup owns 64 consecutive nodes k (stride 63: lane 63 only supplies â_{k+1}
-// of lane 62) for all N rows, exactly as egm_rhs_kernel computes â there (u'(c_m) once per
-// (m, k) in LDS, the Euler sum in m order, one pow per (j, k)); each wave then finds B_k of
-// its 64 increasing â (two 64-ary ballot searches of a_grid and an LDS window), and lane k
-// writes the outputs of its queries with its own (â_k, â_{k+1}, y_k, y_{k+1}) — the same
-// formulas, on the same segment, as egm_interp_kernel, so bit for bit the two-launch step.
-// The two end segments hold the long runs: segment 0 takes every query below â_1 (the
-// borrowing-constraint region, thousands of nodes for low productivity at Na = 20,000) and
-// segment Na−2 every query from â_{Na−2} up.  Their owners would walk those runs serially, so
-// instead every workgroup recomputes the four end nodes â_j(0, 1, Na−2, Na−1) of every row
-// (4N u′ evaluations in parallel lanes, the Euler sums in m order, four pows per wave) and
-// answers the end-segment queries among its own query indices i ∈ [63b, 63b + 63) — query i
-// is in segment 0 iff a_i < â_1 and in segment Na−2 iff a_i >= â_{Na−2}, the same tests that
-// define B_1 and B_{Na−2}.  Another segment with more than 4 queries is finished by the whole
-// wave, 64 queries at a time.  â_j not strictly increasing (an adjacent pair checked per
-// lane) sets bit 1 of the slot's second word: the host fails the call, as the two-launch step
-// does.  diff must be zero at launch; the first workgroup zeroes the next step's slot set
-// (diff_clear), so a step is one launch.
-__global__ __launch_bounds__(1024) void egm_scatter_kernel(EgmArgs A) {
-    __shared__ double s_up[16][64];
-    __shared__ double s_a[16][256];
-    const int lane = threadIdx.x & 63;
-    const int m = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // blockDim = 64·N
-    const int N = A.N, Na = A.Na;
-    const int k = blockIdx.x * 63 + lane;
-    const bool okk = k < Na;
-    const double* __restrict__ ag = A.a;
-    if (blockIdx.x == 0 && A.diff_clear)  // the next step's slots (a different set)
-        for (int q = threadIdx.x; q < kEgmSlotWords; q += blockDim.x) A.diff_clear[q] = 0ull;
-    // u'(c_q) at the end nodes {0, 1, Na−2, Na−1}: lane 4q + e of every wave (N <= 16)
-    const int e_end = lane & 3, q_end = lane >> 2;
-    const int k_end = e_end < 2 ? e_end : Na - 4 + e_end;
-    const double up_end =
-        q_end < N ? uprime_dev(A.c[(size_t)q_end * Na + k_end], A.sigma, A.ns) : 0.0;
-    s_up[m][lane] = okk ? uprime_dev(A.c[(size_t)m * Na + k], A.sigma, A.ns) : 0.0;
-    __syncthreads();
-    const int j = m;
-    const double coef0 = A.beta * (1 + A.r);
-    const double ws = A.w * A.s[j];
-    // â_j and y_j at the end nodes (lanes 0-3), the same operations as the owners' below
-    double ahe = 0.0, ye = 0.0;
-    {
-        double acc = 0.0;
-        for (int q = 0; q < N; ++q)
-            acc = acc + (coef0 * A.P[j * N + q]) * __shfl(up_end, 4 * q + e_end);
-        if (lane < 4) {
-            const double cn = aiy_pow(acc, -1.0 / A.sigma);  // :88
-            const double akv = ag[k_end];
-            if (A.labor) {
-                const double ls = labor_dev(cn, ws, A.sigma, A.ns, A.phi, A.theta);
-                ahe = ((cn + akv) - ws * ls) / (1 + A.r);
-            } else {
-                ahe = ((cn + akv) - ws) / (1 + A.r);
-            }
-            ye = A.labor ? cn : akv;
-        }
-    }
-    const double xe0 = readlane_d(ahe, 0), xe1 = readlane_d(ahe, 1);
-    const double ye0 = readlane_d(ye, 0), ye1 = readlane_d(ye, 1);
-    const double xt0 = readlane_d(ahe, 2), xt1 = readlane_d(ahe, 3);
-    const double yt0 = readlane_d(ye, 2), yt1 = readlane_d(ye, 3);
-    double ah = 0.0, yk = 0.0;
-    if (okk) {
-        double acc = 0.0;
-        for (int q = 0; q < N; ++q) acc = acc + (coef0 * A.P[j * N + q]) * s_up[q][lane];
-        const double cn = aiy_pow(acc, -1.0 / A.sigma);  // :88
-        const double akv = ag[k];
-        if (A.labor) {
-            const double ls = labor_dev(cn, ws, A.sigma, A.ns, A.phi, A.theta);
-            ah = ((cn + akv) - ws * ls) / (1 + A.r);
-        } else {
-            ah = ((cn + akv) - ws) / (1 + A.r);
-        }
-        yk = A.labor ? cn : akv;
-    }
-    // neighbour k + 1 (lane 63 of the next tile is this tile's lane 63)
-    const double ah1 = __shfl_down(ah, 1), yk1 = __shfl_down(yk, 1);
-    const bool own = lane < 63 && okk && k <= Na - 2;  // segment k is this lane's
-    const bool bad = own && !(ah < ah1);               // interp1 needs increasing â
-    // B_k = #{i : a_i < â_k} for every valid lane (lane 63 supplies B_{k+1} of lane 62)
-    const int last = min(63, Na - 1 - blockIdx.x * 63);
-    const double q0 = readlane_d(ah, 0), q1 = readlane_d(ah, last);
-    int lo0 = 0, hi0 = Na, lo1 = 0, hi1 = Na;
-    while (lo0 < hi0 || lo1 < hi1) {  // wave-uniform 64-ary lower bounds of q0 and q1
-        const int st0 = max((hi0 - lo0 + 63) >> 6, 1), st1 = max((hi1 - lo1 + 63) >> 6, 1);
-        const int k0 = lo0 + (lane + 1) * st0 - 1, k1 = lo1 + (lane + 1) * st1 - 1;
-        const bool v0 = k0 < hi0, v1 = k1 < hi1;
-        const double x0 = v0 ? ag[k0] : 0.0, x1 = v1 ? ag[k1] : 0.0;
-        const int c0 = __popcll(__ballot(v0 && x0 < q0));
-        const int c1 = __popcll(__ballot(v1 && x1 < q1));
-        if (lo0 < hi0) {
-            const int nh = lo0 + (c0 + 1) * st0 - 1;
-            lo0 += c0 * st0;
-            hi0 = nh < hi0 ? nh : hi0;
-        }
-        if (lo1 < hi1) {
-            const int nh = lo1 + (c1 + 1) * st1 - 1;
-            lo1 += c1 * st1;
-            hi1 = nh < hi1 ? nh : hi1;
-        }
-    }
-    int Bk;
-    const int span = lo1 - lo0;
-    if (span >= 0 && span <= 256) {  // increasing â: every B_k in [lo0, lo1]
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (u * 64 + lane < span) s_a[m][u * 64 + lane] = ag[lo0 + u * 64 + lane];
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        int lo = 0, hi = span;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (s_a[m][mid] < ah) lo = mid + 1;
-            else hi = mid;
-        }
-        Bk = lo0 + lo;
-    } else {  // not increasing (flagged) or a wide spread: per-lane search of the range
-        int lo = min(lo0, lo1), hi = max(lo0, lo1);
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (ag[mid] < ah) lo = mid + 1;
-            else hi = mid;
-        }
-        Bk = lo;
-    }
-    const int Bk1 = __shfl_down(Bk, 1);
-    // segments 0 and Na−2 are answered per query index below, not by their owners
-    const bool mid = own && k != 0 && k != Na - 2;
-    int b = mid ? Bk : 0, e = mid ? Bk1 : 0;
-    b = min(max(b, 0), Na);
-    e = min(max(e, b), Na);
-    const double r1 = 1 + A.r;
-    unsigned long long key = 0ull;
-    bool any = false;
-    const double* __restrict__ crow = A.c + (size_t)j * Na;
-    auto query = [&](int i, double x0, double x1, double y0, double y1) {
-        const size_t t = (size_t)j * Na + i;
-        const double q = ag[i];
-        const double tt = (q - x0) / (x1 - x0);
-        double g = y0 + tt * (y1 - y0);
-        double cn;
-        if (A.labor) {
-            if (q < A.amin) g = A.amin;  // :91
-            cn = g;
-            const double l = labor_dev(g, ws, A.sigma, A.ns, A.phi, A.theta);  // :95
-            const double kk = (r1 * q + ws * l) - g;                            // :98
-            A.pk[t] = kk < 0 ? 0.0 : kk;                                         // :99
-            if (A.pl) A.pl[t] = l;
-        } else {
-            if (g < A.amin) g = A.amin;  // :98
-            A.pk[t] = g;
-            cn = (r1 * q + ws) - g;  // :102
-        }
-        A.cout[t] = cn;
-        const double d = fabs(cn - crow[i]);
-        if (d == d) {
-            const unsigned long long kb = (unsigned long long)aiy_dbits(d);
-            key = kb > key ? kb : key;
-            any = true;
-        }
-    };
-    {  // end segments among this workgroup's query indices (lane 63 only in the last one)
-        const int i = blockIdx.x * 63 + lane;
-        if (i < Na && (lane < 63 || blockIdx.x == gridDim.x - 1)) {
-            const double qa = ag[i];
-            if (qa < xe1) query(i, xe0, xe1, ye0, ye1);           // i < B_1: segment 0
-            else if (qa >= xt0) query(i, xt0, xt1, yt0, yt1);     // i >= B_{Na−2}
-        }
-    }
-    constexpr int kShort = 4;
-    for (int u = 0; u < kShort; ++u)
-        if (b + u < e) query(b + u, ah, ah1, yk, yk1);
-    unsigned long long lm = __ballot(e - b > kShort);
-    while (lm) {  // long segments: the wave takes their remaining queries 64 at a time
-        const int ql = __builtin_ctzll(lm);
-        lm &= lm - 1;
-        const int qb = readlane_i(b, ql) + kShort, qe = readlane_i(e, ql);
-        const double x0 = readlane_d(ah, ql), x1 = readlane_d(ah1, ql);
-        const double y0 = readlane_d(yk, ql), y1 = readlane_d(yk1, ql);
-        for (int i = qb + lane; i < qe; i += 64) query(i, x0, x1, y0, y1);
-    }
-    // block max|Δc| into slot blockIdx % 64; the non-monotone flag in bit 1 of its second word
-    key = wave_max_u64_lane63(key);
-    const unsigned lo32 = __builtin_amdgcn_readlane((int)(unsigned)key, 63);
-    const unsigned hi32 = __builtin_amdgcn_readlane((int)(unsigned)(key >> 32), 63);
-    const int fl = (__ballot(any) != 0ull ? 1 : 0) | (__ballot(bad) != 0ull ? 2 : 0);
-    __shared__ unsigned long long s_key[16];
-    __shared__ int s_fl[16];
-    if (lane == 0) {
-        s_key[m] = ((unsigned long long)hi32 << 32) | lo32;
-        s_fl[m] = fl;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long kk = 0ull;
-        int f = 0;
-        for (int v = 0; v < N; ++v) {
-            kk = s_key[v] > kk ? s_key[v] : kk;
-            f |= s_fl[v];
-        }
-        unsigned long long* sl = A.diff + 2 * (blockIdx.x % kDiffSlots);
-        if (f & 1) atomicMax(sl, kk);
-        if (f) atomicOr(sl + 1, (unsigned long long)f);
-    }
-}
-
 int launch_egm_rhs(const EgmArgs& A, hipStream_t st) {
     if (A.N > 16) return fail(AIY_BAD_SHAPE, "EGM kernels support N <= 16 productivity states");
     egm_rhs_kernel<<<(A.Na + 63) / 64, 64 * A.N, 0, st>>>(A);
@@ -635,7 +475,10 @@ int launch_egm_rhs(const EgmArgs& A, hipStream_t st) {
 
 int launch_egm_chain(const EgmArgs& A, hipStream_t st) {
     if (A.N > 16) return fail(AIY_BAD_SHAPE, "EGM kernels support N <= 16 productivity states");
-    egm_chain_kernel<<<(A.Na + 63) / 64, 64 * A.N, 0, st>>>(A);
+    if (A.trace)
+        launch_dispatch_timed(egm_chain_kernel<true>, dim3((A.Na + 63) / 64), dim3(64 * A.N), 0, st, A);
+    else
+        launch_dispatch_timed(egm_chain_kernel<false>, dim3((A.Na + 63) / 64), dim3(64 * A.N), 0, st, A);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }
@@ -644,11 +487,6 @@ int launch_egm_step(const EgmArgs& A, hipStream_t st) {
     if (A.N > 16) return fail(AIY_BAD_SHAPE, "EGM kernels support N <= 16 productivity states");
     if (A.fused && A.Na >= 2 && A.Na <= kEgmFusedMaxNa) {
         egm_fused_kernel<<<A.N, 1024, 0, st>>>(A);
-        AIY_HIP(hipGetLastError());
-        return AIY_OK;
-    }
-    if (A.onepass) {
-        egm_scatter_kernel<<<(A.Na - 1 + 62) / 63, 64 * A.N, 0, st>>>(A);
         AIY_HIP(hipGetLastError());
         return AIY_OK;
     }

@@ -13,7 +13,7 @@ struct aiy_ws {
     // search knobs (aiy_ws_set_search)
     int coarse = 512;
     int CK = 1024;
-    int variant = -1;  // -1: by size (see bell_sweep_dev)
+    int variant = -1;  // -1: by size (see bell_sweep_dev); EGM knobs: bits 18-20 (egm_knob)
     // VFI scratch
     double* EV = nullptr;
     double2* T = nullptr;
@@ -85,9 +85,6 @@ struct aiy_ws {
     unsigned long long* spec_diff = nullptr;    // device [2 * 2*spec_max]: a pair per sweep
     unsigned long long* spec_hdiff = nullptr;   // pinned host, two copies (batches in flight)
     hipEvent_t spec_ev[2] = {nullptr, nullptr};
-    // persistent small-grid solve: diff slots [2][2*kDiffSlots], barrier words, result
-    unsigned long long* pers = nullptr;
-    bool persist = false;  // aiy_ws_set_persistent (measured slower: off by default)
     // speculative EGM solve: ring of spec_max + 1 policy_c buffers, per-step diff slots + flag
     size_t egm_spec_n = 0;
     int egm_spec_m = 0;
@@ -95,11 +92,6 @@ struct aiy_ws {
     unsigned long long* egm_slots = nullptr;    // device [2 spec_max + 1][2*kDiffSlots + 2]
     unsigned long long* egm_hslots = nullptr;   // pinned host, two copies (batches in flight)
     hipEvent_t egm_ev[2] = {nullptr, nullptr};  // end of each in-flight batch's slot copy
-    // single EGM steps on the one-pass path: two slot sets (step t writes set t & 1 and clears
-    // the other), zeroed at allocation; egm_cur = the set of the last step
-    unsigned long long* egm_d2 = nullptr;
-    unsigned long long* egm_cur = nullptr;
-    int egm_par = 0;
     // chained EGM solve (Na > 1,024): the second â / c̃ pair (step parity)
     double* egm_x2 = nullptr;
     double* egm_y2 = nullptr;
@@ -144,25 +136,6 @@ struct aiy_ws {
         hslots = nullptr;
         bC = 0;
     }
-    // chained sweeps (aiy_ws_set_chain, aiy_vfi_sweeps_dev and the speculative solve): the second
-    // table set (the tree kernel of sweep g reads set g & 1 and builds set (g+1) & 1), the 64-block
-    // maxima of set 0 live in Dm; per-tile arrival counters and a ring of three diff-slot sets,
-    // all zeroed at allocation (the kernels leave them zero / cleared ahead)
-    bool chain = false;  // measured slower than a table launch per sweep: opt-in
-    double* cEV = nullptr;
-    double* cDt = nullptr;
-    double* cDm8 = nullptr;
-    double* cDm64 = nullptr;
-    unsigned* tcnt = nullptr;
-    unsigned long long* zsets = nullptr;  // [3][2*kDiffSlots]
-    void free_chain() {
-        void* ps[] = {cEV, cDt, cDm8, cDm64, tcnt, zsets};
-        for (void* p : ps)
-            if (p) (void)hipFree(p);
-        cEV = cDt = cDm8 = cDm64 = nullptr;
-        tcnt = nullptr;
-        zsets = nullptr;
-    }
     // timing of the dominant kernel
     bool timing = false, count_hits = false;
     std::vector<hipEvent_t> ev_start, ev_stop;
@@ -184,11 +157,10 @@ struct aiy_ws {
     }
     void free_all() {
         void* ps[] = {EV, T, T32, Dm, Dm8, Dt, Dm512, touched, best0, idx0, mom, dis, kf, partial, diff, hitcount, trace, g0, g1, g2, gi,
-                      d_key, d_off, d_wr, d_mass, d_part, pers, egm_d2, egm_x2, egm_y2, egm_seg};
+                      d_key, d_off, d_wr, d_mass, d_part, egm_x2, egm_y2, egm_seg};
         for (void* p : ps)
             if (p) (void)hipFree(p);
         free_spec();
-        free_chain();
         free_batch();
         free_egm_spec();
         free_dist_spec();
@@ -196,8 +168,7 @@ struct aiy_ws {
         EV = nullptr; T = nullptr; T32 = nullptr; Dm = nullptr; Dm8 = nullptr; Dt = nullptr; Dm512 = nullptr; touched = nullptr; best0 = nullptr; dis = nullptr; kf = nullptr; kf_cap = 0;
         kf_ok = false;
         idx0 = nullptr; mom = nullptr; partial = nullptr; diff = nullptr; hitcount = nullptr; trace = nullptr; trace_cap = 0; hdiff = nullptr;
-        g0 = g1 = g2 = nullptr; gi = nullptr; pers = nullptr;
-        egm_d2 = egm_cur = nullptr; egm_par = 0;
+        g0 = g1 = g2 = nullptr; gi = nullptr;
         egm_x2 = egm_y2 = nullptr;
         egm_seg = nullptr;
         d_key = d_off = nullptr; d_wr = d_mass = d_part = nullptr;
@@ -206,6 +177,12 @@ struct aiy_ws {
 };
 
 namespace aiy {
+// EGM A/B knobs on the workspace's variant word, above the VFI geometry bits (0-17), so a VFI
+// variant never changes the EGM path on a shared workspace
+constexpr int kEgmTwoLaunch = 1 << 18;  // the two-launch step even for Na <= 1,024
+constexpr int kEgmNoChain = 1 << 19;    // solve loop: two launches per step, no chaining
+constexpr int kEgmNoHints = 1 << 20;    // interp1 without the previous step's segment windows
+inline bool egm_knob(const aiy_ws* ws, int bit) { return ws->variant >= 0 && (ws->variant & bit); }
 struct BellCall {
     bool labor = false;
     int64_t Nl = 1;
@@ -226,16 +203,13 @@ struct BellCall {
     double* pc = nullptr;
     double* diff_out = nullptr;
     void* prev_diff_out = nullptr;  // [2] u64: the previous sweep's folded {max bits, any}
-    // chained sweeps: sweep chain_g (0-based) of a chain on this workspace — sweep 0 builds its
-    // table with the table kernel, every later one reads the table the previous sweep's tree
-    // kernel built from its v_new, so v_old MUST be the previous chained sweep's v_new, unchanged
-    bool chain = false;
-    int64_t chain_g = 0;
 };
 int ws_ensure_bell(aiy_ws* ws, size_t partial_slots);
 int ws_timing_begin(aiy_ws* ws, hipStream_t st);
 int ws_timing_end(aiy_ws* ws, hipStream_t st);
 int ws_timing_drain(aiy_ws* ws);
+int ws_dispatch_arm(aiy_ws* ws);
+void ws_dispatch_commit(aiy_ws* ws);
 int ws_read_diff(aiy_ws* ws, hipStream_t st, double* d);
 int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st);
 int bell_solve_dev(aiy_ws* ws, BellCall c, double* v_a, double* v_b, double tol,

@@ -114,16 +114,6 @@ class Workspace:
         results do not depend on it, see aiy_ws_set_speculation."""
         check(lib().aiy_ws_set_speculation(self._h, ip(max_batch)))
 
-    def set_persistent(self, on: bool):
-        """Small-grid solves in one persistent cooperative launch (default off: measured
-        slower); results do not depend on it, see aiy_ws_set_persistent."""
-        check(lib().aiy_ws_set_persistent(self._h, ip(1 if on else 0)))
-
-    def set_chain(self, on: bool):
-        """Chained sweeps (the tree kernel builds the next sweep's table; default on) or one
-        table launch per sweep; results do not depend on it, see aiy_ws_set_chain."""
-        check(lib().aiy_ws_set_chain(self._h, ip(1 if on else 0)))
-
     def set_search(self, coarse_stride=0, k_chunk=1024):
         check(lib().aiy_ws_set_search(self._h, ip(coarse_stride), ip(k_chunk)))
 

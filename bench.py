@@ -159,9 +159,6 @@ def main():
     ap.add_argument("--no-panel", action="store_true", help="skip the KS panel (F2/F3) leg")
     ap.add_argument("--ks-depth", type=int, default=None,
                     help="KS Howard sweeps per halo exchange (default 4 on >1 rank)")
-    ap.add_argument("--chain", action="store_true",
-                    help="time the sweeps as one chain (each tree launch builds the next sweep's "
-                         "table; measured slower, DESIGN.md §5) instead of table + tree per sweep")
     ap.add_argument("--one-call", action="store_true",
                     help="issue the timed sweeps with one aiy_vfi_sweeps_dev call (C++ loop) "
                          "instead of one Python call per sweep; same kernels")
@@ -228,18 +225,15 @@ def main():
     snap_cur = cur
 
     def sweeps(n):
-        """n sweeps of the solve (hint = the previous argmax): n table + tree launch pairs, or
-        with --chain one chain through aiy_vfi_sweeps_dev — the first sweep's table by the
-        table kernel, every later one built by the previous sweep's tree launch."""
+        """n sweeps of the solve (hint = the previous argmax): n table + tree launch pairs, one
+        Python call per sweep, or with --one-call one aiy_vfi_sweeps_dev call (C++ loop)."""
         nonlocal cur
-        if not (args.chain or args.one_call) or args.mode != 1:
+        if not args.one_call or args.mode != 1:
             for _ in range(n):
                 step()
             return
-        ws.set_chain(bool(args.chain))
         ws.vfi_sweeps(v[cur], v[1 - cur], a_t, s_t, P_t, r, w, cal["beta"], cal["sigma"], n,
                       idx, pk, pc, hint=idx, mode=args.mode)
-        ws.set_chain(False)
         cur ^= n & 1
 
     def restore():

@@ -196,7 +196,7 @@ def egm_leg(pkg, dev, Na, labor=False, steps=50, reps=5, cpu_threads=1, variant=
     t = lambda x: torch.as_tensor(np.ascontiguousarray(x), device=dev)
     a_t, s_t, P_t = t(a), t(cal["s"]), t(cal["P"])
     ws = pkg.Workspace(N, Na)
-    if variant >= 0:  # (bit 11: the two-launch step even on small grids — A/B only)
+    if variant >= 0:  # (EGM knob bit 18: the two-launch step even on small grids — A/B only)
         ws.set_variant(variant)
     c = [t(pc0), torch.zeros((N, Na), dtype=torch.float64, device=dev)]
     pk = torch.zeros_like(c[0])
@@ -244,9 +244,19 @@ def egm_leg(pkg, dev, Na, labor=False, steps=50, reps=5, cpu_threads=1, variant=
         torch.cuda.synchronize()
         sms.append((time.perf_counter() - t0) * 1e3 / 200)
     step_ms = _median(sms)
+    # the chained launch's own duration (events recorded by its dispatch, no gaps): one more
+    # pass of the same steps with timing on; Na <= 1,024 runs the fused kernel (not timed)
+    ws2.set_timing(True)
+    c2.copy_(t(pc0))
+    solve_dev(200)
+    torch.cuda.synchronize()
+    km, nl, _ = ws2.timing()
+    ws2.set_timing(False)
+    kern_ms = km / nl if nl else None
     bps = 32 if labor else 24
     states = N * Na
-    gbs = states * bps / (step_ms * 1e-3) / 1e9
+    gbs_step = states * bps / (step_ms * 1e-3) / 1e9
+    gbs = states * bps / ((kern_ms or step_ms) * 1e-3) / 1e9
     pcs = c[cur].cpu().numpy()
     solve = corc.labor_egm_step if labor else corc.egm_step
     args = ((1.0, 1.0, cal["amin"]) if labor else (cal["amin"],))
@@ -272,11 +282,9 @@ def egm_leg(pkg, dev, Na, labor=False, steps=50, reps=5, cpu_threads=1, variant=
         walls.append(time.perf_counter() - t0)
         iters = R["iters"]
     solve_s = _median(walls)
-    if Na <= 1024 and not (variant >= 0 and variant & 2048):
+    if Na <= 1024 and not (variant >= 0 and variant & (1 << 18)):
         path = "1 launch per step: egm_fused_kernel, a workgroup per z-state)"
-    elif Na > 1024 and variant >= 0 and variant & 4096:
-        path = "1 launch per step: egm_scatter_kernel, segments -> query ranges of a_grid)"
-    elif Na > 1024 and not (variant >= 0 and variant & 8192):
+    elif Na > 1024 and not (variant >= 0 and variant & (1 << 19)):
         path = ("1 launch per step in the solve loop: egm_chain_kernel, interp1 of step t + "
                 "the Euler RHS of step t+1 on the same tiles)")
     else:
@@ -294,7 +302,12 @@ def egm_leg(pkg, dev, Na, labor=False, steps=50, reps=5, cpu_threads=1, variant=
             "us_per_step": step_ms * 1e3, "repeats": reps,
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": gbs / HBM_PEAK_GBS,
-                         "basis": f"{bps} B algorithmic per state-iteration x {states} states"},
+                         "kernel": "egm_chain_kernel" if kern_ms else "whole step (fused kernel)",
+                         "kernel_avg_ms": kern_ms, "launches": nl,
+                         "frac_per_step": gbs_step / HBM_PEAK_GBS,
+                         "basis": f"{bps} B algorithmic per state-iteration x {states} states / "
+                                  + ("the chained launch's dispatch-recorded duration (one "
+                                     "launch per step)" if kern_ms else "the step time")},
             "cpu_baseline": {"unit": "state-iterations/s", "kind": "port", **cpu_out,
                              "sample": f"{reps_cpu} EGM step(s) at Na={Na} (oracle/aiy_oracle.c)"}}
 
@@ -442,7 +455,8 @@ def dist_leg(pkg, dev, Na=20000, pushes=320, cpu_pushes=600, cpu_threads=1):
                         f"lambda, device tier (aiy_dist_stationary_dev, tol=0)",
             "value": pushes / (wall_ms * 1e-3), "unit": "pushes/s",
             "states_per_s": pushes * states / (wall_ms * 1e-3),
-            "us_per_push": wall_ms * 1e3 / pushes, "kernel_us": kern_ms * 1e3,
+            "us_per_push": wall_ms * 1e3 / pushes,
+            "kernel_us": kern_ms * 1e3,  # events recorded by the push's own dispatch (no gaps)
             "to_tol": {"tol": 1e-13, "pushes": it_tol, "dist": d_tol, "wall_ms": tol_ms,
                        "K": float(K[0])},
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -246,32 +246,23 @@ int aiy_ws_invalidate(aiy_ws* ws);
 int aiy_ws_set_search(aiy_ws* ws, int coarse_stride, int k_chunk);
 /* VFI solves (A2, all tiers) enqueue up to max_batch sweeps between reads of max|v_new-v_old|
  * (default 16; 0 or 1 = one synchronisation per sweep).  Sweeps past the stopping sweep are
- * discarded, so iteration count, v_new, v_old and policies do not depend on it; memory:
- * max_batch + 1 value buffers and max_batch policy sets per workspace. */
+ * discarded, so iteration count, v_new, v_old and policies do not depend on it; memory: two
+ * batches in flight — 2·max_batch + 1 value buffers and 2·max_batch policy sets per workspace. */
 int aiy_ws_set_speculation(aiy_ws* ws, int max_batch);
-/* A2 on small grids (Na <= 4096, A1 tree screen, integer sigma, default geometry): with
- * persistent = 1 a solve runs sweep 1 with ordinary launches and every later sweep inside ONE
- * cooperative launch that tests the stop rule on the device (no kernel boundary and no host
- * read per sweep).  Results are identical either way.  Default 0 (the speculative loop): at
- * Na = 400 the in-kernel grid barriers cost more than the launches they replace (31 vs 15 us
- * per sweep). */
-int aiy_ws_set_persistent(aiy_ws* ws, int persistent);
-/* screen-kernel shape (tuning only; results are identical).  bit 3 clear (default): the bound
- * tree screen, bit 0 = 2 states per lane (else 1), bits 1-2 = 1, 2, 4 or 8 cooperating waves
- * per tile, bit 4 = XCD-aware tile order.  bit 3 set: the chunked screen + merge, with
- * bit 0 = 4 states per lane (else 2), bit 1 = registers capped for 8 waves per SIMD, bit 2 =
- * fp64-only screen (else the packed fp32 pre-screen with directed-rounding bounds first).
- * Tree screen extras: bit 5 = no hill-climb from the hint, bits 7-8 = hint window half-width
- * 1, 2, 4 or 8, bit 9 = no extrapolated (hint + last shift) start, bit 6 = 4 lanes per state,
- * bit 10 = the plain exhaustive scan, bit 12 = cooperating waves deal the first superblock's
- * passing 8-blocks round-robin (else by 64-block).  EGM steps on this workspace: bit 11 = two
- * launches per step even when Na <= 1024 (default there: one fused launch); bit 12 = the one-pass
- * scatter step when Na > 1024 (default there: two launches, one chained launch per step in the
- * solve loops); bit 13 = no chaining in the solve loops; bit 14 = no interp1 segment hints.  Bit 13 = tiles in
- * descending asset order (one wave per tile); bit 17 = each XCD's range of tiles dealt in
- * reverse dispatch order (with bit 4).  Results are identical for every value in [-1, 262143].
- * -1 (default): chosen by size — Na <= 4096: 2 cooperating waves per tile (A1), 4 with bit 12
- * (labour); else 16. */
+/* kernel shapes and A/B knobs (tuning only; results are identical for every value in
+ * [-1, 2^21)).  VFI, bit 3 clear (default): the bound tree screen, bit 0 = 2 states per lane
+ * (else 1), bits 1-2 = 1, 2, 4 or 8 cooperating waves per tile, bit 4 = XCD-aware tile order;
+ * bit 3 set: the chunked screen + merge, with bit 0 = 4 states per lane (else 2), bit 1 =
+ * registers capped for 8 waves per SIMD, bit 2 = fp64-only screen (else the packed fp32
+ * pre-screen with directed-rounding bounds first).  Tree screen extras: bit 5 = no hill-climb
+ * from the hint, bits 7-8 = hint window half-width 1, 2, 4 or 8, bit 9 = no extrapolated
+ * (hint + last shift) start, bit 10 = the plain exhaustive scan, bit 12 = cooperating waves
+ * deal the first superblock's passing 8-blocks round-robin (else by 64-block), bits 14 / 15 =
+ * force the VALU / MFMA expectation.  EGM steps on this workspace (their own bits, so a VFI
+ * variant never changes the EGM path): bit 18 = two launches per step even when Na <= 1024
+ * (default there: one fused launch); bit 19 = no chaining in the solve loops (two launches per
+ * step); bit 20 = no interp1 segment windows.  -1 (default): chosen by size — Na <= 4096:
+ * 2 cooperating waves per tile (A1), 4 with bit 12 (labour); else 16. */
 int aiy_ws_set_variant(aiy_ws* ws, int variant);
 
 /* A1 on device.  hint (nullable, [N][Na] int32 0-based) = previous sweep's argmax; the result
@@ -287,18 +278,11 @@ int aiy_vfi_sweep_dev(aiy_ws* ws, const double* v_old, const double* a_grid, con
  * wrote (ping-pong), so after the call v_new is in v_b when nsweeps is odd, else in v_a.  hint
  * (nullable) is sweep 1's hint, every later sweep's hint is idx (the previous argmax).  idx,
  * policy_k, policy_c hold the last sweep's policies; diff (nullable, device double[2]) its
- * {max|v_new-v_old|, any}.  Results equal nsweeps aiy_vfi_sweep_dev calls bit for bit.  With
- * chaining on (aiy_ws_set_chain) and the tree screen at one state per lane (N <= 16, integer
- * sigma, VALU expectation) each sweep after the first is ONE launch: the tree kernel of sweep g
- * also builds sweep g+1's table. */
+ * {max|v_new-v_old|, any}.  Results equal nsweeps aiy_vfi_sweep_dev calls bit for bit. */
 int aiy_vfi_sweeps_dev(aiy_ws* ws, double* v_a, double* v_b, const double* a_grid,
                        const double* s, const double* P, double r, double w, double beta,
                        double sigma, const int32_t* hint, int64_t nsweeps, int mode, int32_t* idx,
                        double* policy_k, double* policy_c, double* diff, void* stream);
-/* chained sweeps in aiy_vfi_sweeps_dev and the VFI solves (1) or a table launch per sweep (0,
- * default: at Na = 20,000 the chain's in-kernel hand-off costs more than the launch it removes,
- * DESIGN.md §5); results are identical either way. */
-int aiy_ws_set_chain(aiy_ws* ws, int on);
 /* A2 on device: v_a (in: v_old) and v_b are ping-pong buffers; on return *out_new points
  * (0 = v_a, 1 = v_b) to the buffer holding v_new, the other holds v_old (break semantics).
  * idx doubles as the hint between sweeps. */

@@ -104,10 +104,9 @@ def test_egm_solve_nonmonotone_grid_is_reported(pkg, gpu):
 @pytest.mark.parametrize("labor", [False, True])
 def test_egm_fused_small_grid_equals_two_launches(pkg, gpu, Na, N, labor):
     """The default step — egm_fused_kernel (one launch, a workgroup per productivity state) for
-    Na <= 1024, the two-launch step above — against variant bits 11 | 12 (the two-launch step
-    on small grids, the one-pass egm_scatter_kernel on large ones: segments → query ranges of
-    the fixed a_grid).  Both, and the C restatement, agree bit for bit over several steps
-    (policy_c, policy_k, policy_l and the step's dist), N = 1 … 16."""
+    Na <= 1024, the two-launch step above — against the EGM knobs 18 | 20 (the two-launch step
+    on small grids, interp1 without segment windows).  Both, and the C restatement, agree bit
+    for bit over several steps (policy_c, policy_k, policy_l and the step's dist), N = 1 … 16."""
     import torch
     dev = torch.device("cuda", 0)
     cal = no.calib_aiyagari(Na=Na, shocks="rouwenhorst", N=N) if N != 7 else \
@@ -120,7 +119,7 @@ def test_egm_fused_small_grid_equals_two_launches(pkg, gpu, Na, N, labor):
     a_t, s_t, P_t = t(a), t(s), t(P)
     pc = np.tile(((1 + r) * a + w * np.mean(s))[None, :], (N, 1))
     runs = []
-    for var in (-1, 2048 | 4096):
+    for var in (-1, (1 << 18) | (1 << 20)):
         ws = pkg.Workspace(N, Na)
         if var >= 0:
             ws.set_variant(var)
@@ -150,7 +149,7 @@ def test_egm_fused_small_grid_equals_two_launches(pkg, gpu, Na, N, labor):
 
 def test_egm_nonmonotone_grid_is_reported_large_grid(pkg, gpu):
     """Na > 1024: the two-launch step (flag word) reports a folding â like the small-grid
-    step; so does the one-pass scatter step (flag in the slots), variant bit 12."""
+    step, with and without the segment windows (EGM knob bit 20)."""
     import torch
     a = np.linspace(0, 10, 5000)
     pc0 = np.tile(np.linspace(50, 0.01, 5000)[:, None], (1, 2))
@@ -162,7 +161,7 @@ def test_egm_nonmonotone_grid_is_reported_large_grid(pkg, gpu):
                       0.0, 1e-6, 50)
     dev = torch.device("cuda", 0)
     t = lambda x: torch.as_tensor(np.ascontiguousarray(x), device=dev)
-    for var in (-1, 4096):
+    for var in (-1, 1 << 20):
         ws = pkg.Workspace(2, 5000)
         ws.set_variant(var)
         c = t(pc0.T)
@@ -193,8 +192,9 @@ def test_egm_n1_large_grid_solve(pkg, gpu, Na):
 def test_egm_chained_solve_dev(pkg, gpu, Na, N, labor):
     """aiy_egm_solve_dev: for Na > 1,024 each step of the speculative solve is ONE launch
     (egm_chain_kernel: interp1 of step t + the Euler RHS of step t+1 on the same tiles) — equal
-    bit for bit to the two-launch steps (variant bit 13) and to the C loop: iteration count,
-    dist, policy_c, policy_k (and policy_l)."""
+    bit for bit to the two-launch steps (EGM knob bit 19) and to the C loop: iteration count,
+    dist, policy_c, policy_k (and policy_l).  A VFI geometry variant on the same workspace
+    (bits 12 | 13 | 14, formerly shared with EGM knobs) leaves the EGM path unchanged."""
     import torch
     dev = torch.device("cuda", 0)
     cal = no.calib_aiyagari(Na=Na, shocks="rouwenhorst", N=N) if N not in (7, 1) else \
@@ -208,7 +208,7 @@ def test_egm_chained_solve_dev(pkg, gpu, Na, N, labor):
     t = lambda x: torch.as_tensor(np.ascontiguousarray(x), device=dev)
     pc0 = np.tile(((1 + r) * a + w * np.mean(s))[None, :], (N, 1))
     outs = []
-    for var in (-1, 8192):
+    for var in (-1, 1 << 19, 4096 | 8192 | 16384):
         ws = pkg.Workspace(N, Na)
         if var >= 0:
             ws.set_variant(var)
@@ -219,11 +219,13 @@ def test_egm_chained_solve_dev(pkg, gpu, Na, N, labor):
                                      400, pk, labor=labor, phi=1.0, theta=1.0, policy_l=pl)
         outs.append((it, dist, c.cpu().numpy(), pk.cpu().numpy(),
                      pl.cpu().numpy() if labor else None))
-    (i0, d0, c0_, k0, l0), (i1, d1, c1, k1, l1) = outs
-    assert i0 == i1 and d0 == d1
-    assert np.array_equal(c0_, c1) and np.array_equal(k0, k1)
+    (i0, d0, c0_, k0, l0) = outs[0]
+    for (i1, d1, c1, k1, l1) in outs[1:]:
+        assert i0 == i1 and d0 == d1
+        assert np.array_equal(c0_, c1) and np.array_equal(k0, k1)
+        if labor:
+            assert np.array_equal(l0, l1)
     if labor:
-        assert np.array_equal(l0, l1)
         Ro = corc.labor_egm_solve(pc0, a, s, P, r, w, 0.96, 5.0, 1.0, 1.0, cal["amin"], 1e-6, 400)
     else:
         Ro = corc.egm_solve(pc0, a, s, P, r, w, 0.96, 5.0, cal["amin"], 1e-6, 400)

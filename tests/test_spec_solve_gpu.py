@@ -14,12 +14,11 @@ from oracle import np_oracle as no
 pytestmark = pytest.mark.gpu
 
 
-def _solve(pkg, torch, spec, v0, cal, r, sigma, tol, max_iter, mode=0, v_b=None, persist=False):
+def _solve(pkg, torch, spec, v0, cal, r, sigma, tol, max_iter, mode=0, v_b=None):
     dev = torch.device("cuda:0")
     N, Na = v0.shape
     ws = pkg.Workspace(N, Na)
     ws.set_speculation(spec)
-    ws.set_persistent(persist)
     t = lambda x: torch.as_tensor(np.ascontiguousarray(x), device=dev)
     va, at, st, Pt = t(v0), t(cal["a_grid"]), t(cal["s"]), t(cal["P"])
     vb = torch.zeros_like(va) if v_b is None else t(v_b)
@@ -50,8 +49,6 @@ def test_speculative_equals_synchronous(pkg, gpu, max_iter):
     ref = _solve(pkg, torch, 0, v0, cal, 0.04, 5.0, 1e-5, max_iter)
     for spec in (2, 3, 16, 64):  # the speculative host loop (default)
         _same(_solve(pkg, torch, spec, v0, cal, 0.04, 5.0, 1e-5, max_iter), ref)
-    for spec in (2, 16):  # the persistent small-grid solve (aiy_ws_set_persistent)
-        _same(_solve(pkg, torch, spec, v0, cal, 0.04, 5.0, 1e-5, max_iter, persist=True), ref)
     if max_iter == 1000:  # and both equal the C oracle's solve
         R = corc.vfi_solve(v0, cal["a_grid"], cal["s"], cal["P"], 0.04, no.wage(0.04, 0.36, 0.08),
                            0.96, 5.0, 1e-5, 1000)
@@ -70,9 +67,7 @@ def test_speculative_warm_start_and_first_sweep_stop(pkg, gpu):
     for tol in (1e-5, 1e-12):
         ref = _solve(pkg, torch, 0, V, cal, 0.03, 5.0, tol, 1000, v_b=V + 1.0)
         for spec in (2, 16):
-            for persist in (True, False):
-                _same(_solve(pkg, torch, spec, V, cal, 0.03, 5.0, tol, 1000, v_b=V + 1.0,
-                             persist=persist), ref)
+            _same(_solve(pkg, torch, spec, V, cal, 0.03, 5.0, tol, 1000, v_b=V + 1.0), ref)
 
 
 @pytest.mark.parametrize("sigma,mode", [(2.5, 0), (5.0, 2)])
@@ -97,15 +92,15 @@ def test_set_speculation_validates(pkg, gpu):
 
 @pytest.mark.parametrize("Na,sigma,max_iter", [(4096, 5.0, 60), (1000, 3.0, 400), (64, 2.0, 1000),
                                                (2500, 9.0, 37)])
-def test_persistent_solve_sizes(pkg, gpu, Na, sigma, max_iter):
-    """The persistent cooperative solve across grid sizes (one to 448 tree items, one to eight
+def test_speculative_solve_sizes(pkg, gpu, Na, sigma, max_iter):
+    """The speculative solve across grid sizes (one to 448 tree items, one to eight
     512-candidate table chunks per row) and CRRA powers: equal to the synchronous loop, and —
     run to tol — to the C oracle's solve."""
     import torch
     cal = no.calib_aiyagari(Na=Na, shocks="rouwenhorst", sigma=sigma)
     v0 = np.zeros((7, Na))
     ref = _solve(pkg, torch, 0, v0, cal, 0.03, sigma, 1e-5, max_iter)
-    got = _solve(pkg, torch, 16, v0, cal, 0.03, sigma, 1e-5, max_iter, persist=True)
+    got = _solve(pkg, torch, 16, v0, cal, 0.03, sigma, 1e-5, max_iter)
     _same(got, ref)
     R = corc.vfi_solve(v0, cal["a_grid"], cal["s"], cal["P"], 0.03, no.wage(0.03, 0.36, 0.08),
                        0.96, sigma, 1e-5, max_iter)

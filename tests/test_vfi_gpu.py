@@ -76,7 +76,7 @@ def test_screened_equals_plain_and_oracle(pkg, gpu, Na, shocks, variant, k_chunk
     assert np.array_equal(pks, pko) and np.array_equal(pcs, pco)
 
 
-@pytest.mark.parametrize("variant", [0, 64, 4098, 4100])
+@pytest.mark.parametrize("variant", [0, 16, 4098, 4100])
 def test_hint_does_not_change_result(pkg, gpu, variant):
     import torch
     cal = no.calib_aiyagari(Na=900)
@@ -146,7 +146,7 @@ def test_full_size_bitwise_vs_oracle(pkg, gpu):
     assert (pcs > 0).all()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 6, 8, 12, 64, 96, 4098, 4100, 4102, 8192, 8194])
+@pytest.mark.parametrize("variant", [0, 1, 2, 6, 8, 12, 16, 32, 96, 512, 4098, 4100, 4102])
 def test_screen_stress_noisy_value(pkg, gpu, variant):
     """Rough value functions put many candidates within rounding distance of the running best
     (near-ties everywhere, multi-modal objectives): the fp32 pre-screen, the fp64 screen and

@@ -2,8 +2,7 @@
 512 candidates, more than the 64 the tree kernel's level-0 bounds hold per load — the
 superblock walk refills them (`load512(g)`, g = 64), a path Na <= 32,768 never takes.  The
 last of a chain of hinted sweeps from v = 0 is compared bit for bit with the C oracle's
-exhaustive sweep of the device's own v_old, for the default geometry and for chained sweeps
-(level-0 bounds from the 64-block maxima there)."""
+exhaustive sweep of the device's own v_old, for the default geometry."""
 import numpy as np
 import pytest
 
@@ -15,8 +14,7 @@ pytestmark = pytest.mark.gpu
 NA = 40000
 
 
-@pytest.mark.parametrize("chain", [False, True])
-def test_vfi_na40000_refilled_level0_bounds(pkg, gpu, chain):
+def test_vfi_na40000_refilled_level0_bounds(pkg, gpu):
     import torch
     cal = no.calib_aiyagari(Na=NA, shocks="rouwenhorst")
     N = cal["N"]
@@ -27,7 +25,6 @@ def test_vfi_na40000_refilled_level0_bounds(pkg, gpu, chain):
     w = pkg.calibration.wage(r, cal["alpha"], cal["delta"])
     assert (NA + 511) // 512 > 64
     ws = pkg.Workspace(N, NA)
-    ws.set_chain(chain)
     va = torch.zeros((N, NA), dtype=torch.float64, device=dev)
     vb = torch.zeros_like(va)
     idx = torch.zeros((N, NA), dtype=torch.int32, device=dev)
