@@ -1495,7 +1495,10 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
             long long* tr = A.trace + 16 * (size_t)item;
             tr[0] = t_start;
             tr[1] = (long long)wall_clock64();
-            tr[2] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));  // HW_REG_XCC_ID
+            // HW_REG_XCC_ID (bits 0-31) | HW_REG_HW_ID << 32 (wave, SIMD, CU, SH, SE of this wave)
+            tr[2] = (long long)(unsigned)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) |
+                    ((long long)(unsigned)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11))
+                     << 32);
             for (int c = 0; c < 4; ++c) {
                 long long sum = 0;
                 for (int v = 0; v < W; ++v) sum += s_cnt[v][c];

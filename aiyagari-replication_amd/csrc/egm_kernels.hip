@@ -272,12 +272,21 @@ __device__ __forceinline__ void egm_trace(const EgmArgs& A, int rec, long long t
 }
 
 // interp1 needs an increasing â_j: a non-increasing adjacent pair of the wave's 64 nodes sets
-// the flag word (the reference's interp1 would sort or fail, Aiyagari_EGM.m:95).  Issued at the
-// end of the kernels, off the interpolation's dependent rounds.
-__device__ __forceinline__ void egm_flag_order(const EgmArgs& A, int j, int tile) {
+// the flag word (the reference's interp1 would sort or fail, Aiyagari_EGM.m:95).  The pair is
+// loaded after the interpolation's dependent rounds (issued with the interpolation in the
+// register budget, they had pushed the chained kernel into scratch) and tested at the end.
+struct EgmOrderPair {
+    double xm, xc;
+    bool ok;
+};
+__device__ __forceinline__ EgmOrderPair egm_order_load(const EgmArgs& A, int j, int tile) {
     const int a_i = tile * 64 + (threadIdx.x & 63);
     const double* __restrict__ x = A.ahat + (size_t)j * A.Na;
-    if (a_i > 0 && a_i < A.Na && !(x[a_i - 1] < x[a_i])) atomicOr(A.flags, 1u);
+    const bool ok = a_i > 0 && a_i < A.Na;
+    return {ok ? x[a_i - 1] : 0.0, ok ? x[a_i] : 1.0, ok};
+}
+__device__ __forceinline__ void egm_order_check(const EgmArgs& A, const EgmOrderPair& p) {
+    if (p.ok && !(p.xm < p.xc)) atomicOr(A.flags, 1u);
 }
 
 __global__ __launch_bounds__(256) void egm_interp_kernel(EgmArgs A, int ntile) {
@@ -294,7 +303,7 @@ __global__ __launch_bounds__(256) void egm_interp_kernel(EgmArgs A, int ntile) {
         double cn;
         ok = egm_interp_wave(A, j, tile, s_x[wave], s_y[wave], d, cn, A.trace ? cy : nullptr) &&
              d == d;
-        egm_flag_order(A, j, tile);
+        egm_order_check(A, egm_order_load(A, j, tile));
     }
     block_max_to_slots(ok, d, A.diff);
     if (A.trace && wv < A.N * ntile) egm_trace(A, wv, t_in, cy, 4);
@@ -331,6 +340,7 @@ __global__ __launch_bounds__(1024) void egm_chain_kernel(EgmArgs A) {
     const long long t_in = TR ? (long long)wall_clock64() : 0;
     const bool okl = egm_interp_wave(A, j, blockIdx.x, s_x[m], s_y[m], d, cn, TR ? cy : nullptr);
     const bool ok = okl && d == d;
+    const EgmOrderPair ord = egm_order_load(A, j, blockIdx.x);  // (latency under the RHS below)
     // step t+1's Euler RHS on this tile: u'(policy_c_next) of every row through LDS
     const int a_i = blockIdx.x * 64 + lane;
     s_up[m][lane] = okl ? uprime_dev(cn, A.sigma, A.ns) : 0.0;
@@ -353,8 +363,8 @@ __global__ __launch_bounds__(1024) void egm_chain_kernel(EgmArgs A) {
         A.ahat_next[(size_t)j * Na + a_i] = ah;
         if (A.labor) A.cnext_next[(size_t)j * Na + a_i] = c2;  // (A4 interpolates a_grid, not c̃)
     }
+    egm_order_check(A, ord);
     block_max_to_slots(ok, d, A.diff);
-    egm_flag_order(A, j, blockIdx.x);
     if constexpr (TR) egm_trace(A, blockIdx.x * N + j, t_in, cy, 4);
 }
 

@@ -153,3 +153,37 @@ def test_lifecycle_lock_balanced_and_release_registered(cal):
     lib = load_pkg().lib()
     lib.aiy_host_cache_bytes.restype = C.c_int64
     assert lib.aiy_host_cache_bytes() == 0
+
+
+def test_step_gateways_validate(cal):
+    """The step-level gateways (one EGM pass, one labour sweep): usage, shapes, and
+    the library status without a device."""
+    import torch
+    pc = np.ones((20, 7))  # Na x N
+    with pytest.raises(mexstub.MexError) as e:
+        mexstub.call("aiy_egm_step_mex", 3, pc, cal["a_grid"])
+    assert e.value.id == "aiy:usage"
+    with pytest.raises(mexstub.MexError) as e:  # s length != N
+        mexstub.call("aiy_egm_step_mex", 3, pc, cal["a_grid"], cal["s"][:-1], cal["P"], 0.04, 1.0,
+                     0.96, 5.0, 0.0)
+    assert e.value.id == "aiy:shape"
+    with pytest.raises(mexstub.MexError) as e:  # P not N x N
+        mexstub.call("aiy_labor_egm_step_mex", 4, pc, cal["a_grid"], cal["s"], np.eye(5), 0.04,
+                     1.0, 0.96, 5.0, 1.0, 1.0, 0.0)
+    assert e.value.id == "aiy:shape"
+    L = np.linspace(0.01, 1.5, 10)
+    with pytest.raises(mexstub.MexError) as e:  # trailing v_new of the wrong shape
+        mexstub.call("aiy_labor_vfi_sweep_mex", 4, np.zeros((7, 20)), cal["a_grid"], cal["s"],
+                     cal["P"], L, 0.04, 1.0, 0.96, 5.0, 1.0, 2.0, np.zeros((7, 19)))
+    assert e.value.id == "aiy:shape"
+    if not torch.cuda.is_available():
+        for name, n, args in (
+                ("aiy_egm_step_mex", 3, (pc, cal["a_grid"], cal["s"], cal["P"], 0.04, 1.0, 0.96,
+                                         5.0, 0.0)),
+                ("aiy_labor_egm_step_mex", 4, (pc, cal["a_grid"], cal["s"], cal["P"], 0.04, 1.0,
+                                               0.96, 5.0, 1.0, 1.0, 0.0)),
+                ("aiy_labor_vfi_sweep_mex", 5, (np.zeros((7, 20)), cal["a_grid"], cal["s"],
+                                                cal["P"], L, 0.04, 1.0, 0.96, 5.0, 1.0, 2.0))):
+            with pytest.raises(mexstub.MexError) as e:
+                mexstub.call(name, n, *args)
+            assert e.value.id == "aiy:NO_DEVICE"

@@ -154,3 +154,39 @@ def test_ge_batch_gateway(pkg, gpu):
                                             [U[:, c] for c in range(3)])
     assert np.array_equal(ks[:, 0], Ks) and np.array_equal(kd[:, 0], Kd)
     assert np.array_equal(it[:, 0].astype(np.int64), It)
+
+
+def test_step_gateways(pkg, gpu, golden):
+    """SURVEY B2's step-level entry points through the MATLAB-facing boundary: one EGM pass
+    (Aiyagari_EGM.m:77-107) iterated by the caller reproduces the solve gateway's loop; one
+    labour EGM pass and one labour VFI sweep (…Labor_VFI.m:69-112) equal the C oracle's."""
+    g = golden("a4_egm_defaults")
+    args = (g["a_grid"], g["s"], g["P"], float(g["r"]), float(g["w"]), 0.96, 5.0)
+    c = g["policy_c0"]
+    it, dist = 0, 1.0
+    while dist > 1e-5 and it < 1000:  # the script's own loop (:74) around the step gateway
+        c_next, k, d = mexstub.call("aiy_egm_step_mex", 3, c, *args, float(g["amin"]))
+        dist = float(d[0, 0])
+        c = c_next
+        it += 1
+    pc, pk, dist2, it2 = mexstub.call("aiy_egm_solve_mex", 4, g["policy_c0"], *args,
+                                      float(g["amin"]), 1e-5, 1000.0)
+    assert it == int(it2[0, 0]) and dist == float(dist2[0, 0])
+    assert np.array_equal(c, pc) and np.array_equal(k, pk)
+    cl, kl, ll, dl = mexstub.call("aiy_labor_egm_step_mex", 4, g["policy_c0"], *args, 1.0, 1.0,
+                                  float(g["amin"]))
+    co, ko, lo, do = corc.labor_egm_step(g["policy_c0"].T, g["a_grid"], g["s"], g["P"],
+                                         float(g["r"]), float(g["w"]), 0.96, 5.0, 1.0, 1.0,
+                                         float(g["amin"]))
+    assert np.array_equal(cl, co.T) and np.array_equal(kl, ko.T) and np.array_equal(ll, lo.T)
+    assert float(dl[0, 0]) == do
+    h = golden("a3_labor_vfi_na100")
+    V = h["v_new"] + 0.25
+    v1, k1, l1, c1, lin = mexstub.call("aiy_labor_vfi_sweep_mex", 5, V, h["a_grid"], h["s"],
+                                       h["P"], h["L"], float(h["r"]), float(h["w"]), 0.96, 5.0,
+                                       1.0, 2.0)
+    vo, (pko, plo, pco, lino) = corc.labor_vfi_sweep(V, h["a_grid"], h["s"], h["P"], h["L"],
+                                                     float(h["r"]), float(h["w"]), 0.96, 5.0,
+                                                     1.0, 2.0)
+    assert np.array_equal(v1, vo) and np.array_equal(lin - 1, lino)
+    assert np.array_equal(k1, pko) and np.array_equal(l1, plo) and np.array_equal(c1, pco)

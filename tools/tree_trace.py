@@ -38,6 +38,8 @@ def main():
                 ms, _, _ = ws.timing()
                 ws.set_timing(False)
                 T = ws.trace()
+                hw = (T[:, 2] >> 32) & 0xffffffff  # HW_REG_HW_ID of the item's wave
+                T[:, 2] &= 0xffffffff             # XCC id
                 dur = (T[:, 1] - T[:, 0]) / 100.0  # µs (100 MHz)
                 t0 = T[:, 0].min()
                 st = (T[:, 0] - t0) / 100.0
@@ -74,6 +76,27 @@ def main():
                               f"last end {en[m].max():.1f}")
                 rows = np.arange(len(T)) // ntile
                 print("  per-row mean dur:", [round(dur[rows == i].mean(), 1) for i in range(N)])
+                # co-residency: items whose wave ran on the same SIMD (XCC, SE, SH, CU, SIMD)
+                # during the item's own lifetime (entry to exit)
+                simd = (T[:, 2] << 16) | (((hw >> 13) & 7) << 8) | (((hw >> 12) & 1) << 7) | \
+                    (((hw >> 8) & 15) << 2) | ((hw >> 4) & 3)
+                ent = (T[:, 12] - t0) / 100.0
+                co = np.zeros(len(T), int)
+                for k in range(len(T)):
+                    m = (simd == simd[k]) & (ent < en[k]) & (en > ent[k])
+                    co[k] = int(m.sum())  # including itself
+                print("  SIMDs used %d; items per SIMD max %d" % (len(np.unique(simd)),
+                      np.bincount(np.unique(simd, return_inverse=True)[1]).max()))
+                for c in sorted(set(co)):
+                    m = co == c
+                    print(f"    co-resident {c}: items {m.sum()} dur mean {dur[m].mean():.1f} "
+                          f"p90 {np.percentile(dur[m], 90):.1f} max {dur[m].max():.1f} "
+                          f"end max {en[m].max():.1f}")
+                late = np.argsort(en)[-10:]
+                print("  last to finish (row, tile, entry, dur, end, co, sup, blk, cand):")
+                for k in late:
+                    print("   ", k // ntile, k % ntile, round(ent[k], 1), round(dur[k], 1),
+                          round(en[k], 1), co[k], *T[k, 3:6])
 
 
 if __name__ == "__main__":
