@@ -25,6 +25,11 @@ struct KsArgs {
     // several s blocks in one launch (sharded path): blockIdx.y = q handles nodes
     // node0 + q·sstride + [0, n_local); ns = 1 (sstride unused) otherwise
     int ns, sstride;
+    // direct (peer-read) schedule: the value / slope column c = s'·nK + K' that a forecast reads
+    // lives at colV[c] / coldV[c] (the owning shard's buffer, on this or a peer device); null:
+    // the launch's own V / dV arrays
+    const double* const* colV;
+    const double* const* coldV;
 };
 struct KsParams {  // the 13-double parameter block, in order
     double beta, alpha, delta, k_min, k_max, ug, ub, l_bar, mu, z1, z2, e1, e2;

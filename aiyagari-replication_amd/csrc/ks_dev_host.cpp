@@ -30,6 +30,11 @@ struct ks_dev {
     int* seg = nullptr;    // [node] segment hints: improve writes them, Howard checks and uses them
     ks_dev* seg_owner = nullptr;  // set: seg is that handle's array (ks_dev_share_hints)
     int sharers = 0;              // handles using this handle's seg array
+    int* own_cols = nullptr;      // the shard's own columns (direct schedule: its slopes)
+    int n_own = 0;
+    // direct schedule (ks_dev_set_columns): device table of 4·nK value then 4·nK slope column
+    // pointers into the owners' buffers; null = the caller's full arrays
+    const double* const* colV = nullptr;
 };
 
 namespace aiy {
@@ -49,6 +54,8 @@ static KsArgs shard_args(const ks_dev* h) {
     A.k_min = h->k_min;
     A.k_max = h->k_max;
     A.seg_hint = h->seg;
+    A.colV = h->colV;
+    A.coldV = h->colV ? h->colV + 4 * h->nK : nullptr;
     return A;
 }
 }  // namespace aiy
@@ -63,7 +70,8 @@ int ks_dev_destroy(ks_dev* h) {
         return fail(AIY_BAD_ARG, "ks_dev_destroy: %d handle(s) still share this handle's hints; "
                     "destroy them first", h->sharers);
     if (h->seg_owner) h->seg_owner->sharers--;
-    void* ps[] = {h->kg, h->P, h->sl, h->dV, h->cols, h->slots, h->seg_owner ? nullptr : h->seg};
+    void* ps[] = {h->kg, h->P, h->sl, h->dV, h->cols, h->own_cols, h->slots,
+                  h->seg_owner ? nullptr : h->seg};
     for (void* q : ps)
         if (q) (void)hipFree(q);
     delete h;
@@ -98,9 +106,11 @@ int ks_dev_create_slice(const double* k_grid, const double* K_grid, const double
             const int kp = sl[s * nK + K].kp_idx;
             for (int sn = 0; sn < 4; ++sn) need[sn * nK + kp] = 1;
         }
-    std::vector<int> cols;
+    std::vector<int> cols, own;
     for (int c = 0; c < 4 * nK; ++c)
         if (need[c]) cols.push_back(c);
+    for (int64_t s = s0; s < s1; ++s)
+        for (int64_t K = K0; K < K1; ++K) own.push_back((int)(s * nK + K));
     double Pr[16];
     for (int i = 0; i < 4; ++i)
         for (int m = 0; m < 4; ++m) Pr[i * 4 + m] = P[i + m * 4];
@@ -110,6 +120,7 @@ int ks_dev_create_slice(const double* k_grid, const double* K_grid, const double
     h->s0 = (int)s0; h->s1 = (int)s1;
     h->beta = p.beta; h->k_min = p.k_min; h->k_max = p.k_max;
     h->ncols = (int)cols.size();
+    h->n_own = (int)own.size();
     const size_t n = (size_t)nk * nK * 4;
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = hipMalloc((void**)&h->kg, nk * sizeof(double));
@@ -117,6 +128,7 @@ int ks_dev_create_slice(const double* k_grid, const double* K_grid, const double
     if (e == hipSuccess) e = hipMalloc((void**)&h->sl, sl.size() * sizeof(KsSlice));
     if (e == hipSuccess) e = hipMalloc((void**)&h->dV, n * sizeof(double));
     if (e == hipSuccess) e = hipMalloc((void**)&h->cols, cols.size() * sizeof(int));
+    if (e == hipSuccess) e = hipMalloc((void**)&h->own_cols, own.size() * sizeof(int));
     if (e == hipSuccess) e = hipMalloc((void**)&h->slots, 2 * kDiffSlots * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMalloc((void**)&h->seg, n * sizeof(int));
     if (e == hipSuccess) e = hipMemset(h->seg, 0, n * sizeof(int));
@@ -124,6 +136,7 @@ int ks_dev_create_slice(const double* k_grid, const double* K_grid, const double
     if (e == hipSuccess) e = hipMemcpy(h->P, Pr, sizeof Pr, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->sl, sl.data(), sl.size() * sizeof(KsSlice), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->cols, cols.data(), cols.size() * sizeof(int), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(h->own_cols, own.data(), own.size() * sizeof(int), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         ks_dev_destroy(h);
         return fail(AIY_HIP_ERROR, "ks_dev_create: %s", hipGetErrorString(e));
@@ -167,6 +180,32 @@ int ks_dev_howard_fused(ks_dev* h, const double* V, const double* dV, const doub
     if (V == Vout || dV == dVout)
         return fail(AIY_BAD_ARG, "Howard sweeps are Jacobi: V/Vout and dV/dVout must differ");
     return launch_ks_howard_slopes(shard_args(h), V, dV, kopt, Vout, dVout, (hipStream_t)stream);
+}
+
+// Direct (peer-read) schedule: every shard keeps the value and slopes of its OWN columns current
+// in its own buffers; a sweep or improvement reads a forecast column wherever its owner keeps
+// it (table: 4·nK value column pointers, then 4·nK slope column pointers, on this device or a
+// peer's), so no column is ever copied.  table = NULL returns to the caller's full arrays.
+int ks_dev_set_columns(ks_dev* h, const void* const* table) {
+    if (!h) return fail(AIY_BAD_ARG, "NULL handle");
+    h->colV = reinterpret_cast<const double* const*>(table);
+    return AIY_OK;
+}
+
+// the slopes of the shard's own columns of V into dV (the start of a direct schedule)
+int ks_dev_slopes_own(ks_dev* h, const double* V, double* dV, void* stream) {
+    if (!h || !V || !dV) return fail(AIY_BAD_ARG, "NULL argument");
+    return launch_ks_slopes_cols(shard_args(h), h->own_cols, h->n_own, V, dV,
+                                 (hipStream_t)stream);
+}
+
+// the improvement of the direct schedule: fminbnd on the shard's nodes, every forecast column
+// (value and slopes) read through the table — the owners' slopes are current, so no slope launch
+int ks_dev_improve_direct(ks_dev* h, double* kopt, void* stream) {
+    if (!h || !kopt) return fail(AIY_BAD_ARG, "NULL argument");
+    if (!h->colV) return fail(AIY_BAD_ARG, "ks_dev_improve_direct: no column table (ks_dev_set_columns)");
+    const KsArgs A = shard_args(h);
+    return launch_ks_improve(A, nullptr, nullptr, kopt, nullptr, (hipStream_t)stream);
 }
 
 // max over the shard's nodes of |V - Vold| / (|Vold| + 1e-10), NaN ignored (:195).

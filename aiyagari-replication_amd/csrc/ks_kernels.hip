@@ -54,8 +54,11 @@ __device__ __forceinline__ double ks_bellman_dev(const KsArgs& A, const KsView& 
     double expec = 0;
 #pragma unroll
     for (int sn = 0; sn < 4; ++sn) {
-        size_t col = ((size_t)sn * A.nK + sl.kp_idx) * nk;
-        expec = expec + A.P[si * 4 + sn] * pchip_at(W.kg, W.V + col, W.dV + col, seg, kq);
+        const int c = sn * A.nK + sl.kp_idx;  // (slice-uniform: scalar loads of the table)
+        const size_t col = (size_t)c * nk;
+        const double* Vc = A.colV ? A.colV[c] : W.V + col;
+        const double* dVc = A.colV ? A.coldV[c] : W.dV + col;
+        expec = expec + A.P[si * 4 + sn] * pchip_at(W.kg, Vc, dVc, seg, kq);
     }
     double c = (sl.a1 * k + sl.a2) - kp;
     c = fmax(c, 1e-10);
@@ -406,6 +409,7 @@ int launch_ks_fused(const KsArgs& A, double* V, double* kopt, int* nfev, KsOut* 
                     hipStream_t st) {
     KsArgs F = A;
     F.seg_hint = nullptr;  // k_opt lives in registers here; the search runs in LDS anyway
+    F.colV = F.coldV = nullptr;  // (everything in LDS)
     ks_fused_vfi_kernel<<<1, kFusedThreads, ks_fused_lds_bytes(A.nk, A.nK), st>>>(F, V, kopt,
                                                                                   nfev, out);
     AIY_HIP(hipGetLastError());

@@ -105,6 +105,227 @@ std::vector<Run> foreign_runs(const Rect& r, int nK, const std::vector<int>& own
 
 }  // namespace
 
+// The direct (peer-read) schedule, depth = 0.  Every shard keeps only its OWN columns of value
+// and slopes current, in its own double-buffered arrays; the fused Howard+slopes sweep and the
+// improvement read each forecast column (Krusell_Smith_VFI.m:343-349) where its owner keeps it,
+// through a per-shard table of column pointers into the owners' buffers (peer pointers over
+// xGMI, peer access enabled) — no column is copied and no ghost column is swept.  Sweep t reads
+// parity cur and writes cur ^ 1; before it a shard waits (stream waits on events, never the
+// host) for the sweep t − 1 of every neighbour — the owners of what it reads (their values are
+// complete) and the shards that read its columns (they are done with the buffer it is about to
+// overwrite).  Same kernels on the same values: bit for bit the single-device solve.
+int ks_vfi_solve_direct_impl(double* value, double* k_opt, const double* k_grid,
+                             const double* K_grid, const double* B, const double* P,
+                             const double* params, int64_t nk, int64_t nK, int64_t howard_steps,
+                             double tol, int64_t max_vfi, int n_shards, int64_t* iters,
+                             double* rel_diff) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1)
+        return fail(AIY_NO_DEVICE, "no HIP device visible");
+    AIY_TRY(check_grid(k_grid, nk));
+    const int W = (int)std::max<int64_t>(1, std::min<int64_t>(n_shards, 2 * nK));
+    KsParams p;
+    memcpy(&p, params, sizeof p);
+    std::vector<KsSlice> sl;
+    ks_slices(p, B, K_grid, (int)nK, sl);
+    const int C = (int)(4 * nK);
+    const size_t n = (size_t)nk * C, nb = n * sizeof(double), colb = nk * sizeof(double);
+    std::vector<int> owner(C, -1);
+    struct DShard {
+        int dev = 0;
+        hipStream_t st = nullptr;
+        hipEvent_t done[2] = {nullptr, nullptr};  // sweep writing parity b complete
+        Rect own{};
+        ks_dev* h = nullptr;
+        double *V[2] = {nullptr, nullptr}, *dV[2] = {nullptr, nullptr};
+        double *kopt = nullptr, *Vold = nullptr;
+        const double** tab[2] = {nullptr, nullptr};  // device: column pointers per parity
+        unsigned long long* red = nullptr;
+        std::vector<int> nbr;  // shards this one waits for before each sweep
+    };
+    std::vector<DShard> S(W);
+    for (int q = 0; q < W; ++q) {
+        S[q].own = shard_slice((int)nK, q, W);
+        for (int s = S[q].own.s0; s < S[q].own.s1; ++s)
+            for (int K = S[q].own.K0; K < S[q].own.K1; ++K) owner[s * nK + K] = q;
+    }
+    // neighbours: owners of the forecast columns a shard reads, and the shards reading its own
+    std::vector<std::vector<char>> nb_m(W, std::vector<char>(W, 0));
+    for (int q = 0; q < W; ++q) {
+        const Rect& r = S[q].own;
+        for (int s = r.s0; s < r.s1; ++s)
+            for (int K = r.K0; K < r.K1; ++K)
+                for (int sn = 0; sn < 4; ++sn) {
+                    const int o = owner[sn * nK + sl[s * nK + K].kp_idx];
+                    if (o != q) nb_m[q][o] = nb_m[o][q] = 1;
+                }
+    }
+    for (int q = 0; q < W; ++q)
+        for (int o = 0; o < W; ++o)
+            if (nb_m[q][o]) S[q].nbr.push_back(o);
+    int rc = AIY_OK;
+    auto cleanup = [&]() {
+        for (auto& sh : S) {
+            (void)hipSetDevice(sh.dev);
+            if (sh.st) (void)hipStreamSynchronize(sh.st);
+        }
+        for (auto& sh : S) {
+            (void)hipSetDevice(sh.dev);
+            if (sh.h) ks_dev_destroy(sh.h);
+            void* ps[] = {sh.V[0], sh.V[1], sh.dV[0], sh.dV[1], sh.kopt, sh.Vold, sh.red,
+                          (void*)sh.tab[0], (void*)sh.tab[1]};
+            for (void* q : ps)
+                if (q) (void)hipFree(q);
+            for (auto& e : sh.done)
+                if (e) (void)hipEventDestroy(e);
+            if (sh.st) (void)hipStreamDestroy(sh.st);
+        }
+    };
+#define KD_CHECK(call)                                                                   \
+    do {                                                                                 \
+        hipError_t e_ = (call);                                                          \
+        if (e_ != hipSuccess) {                                                          \
+            rc = fail(AIY_HIP_ERROR, "%s: %s", #call, hipGetErrorString(e_));            \
+            cleanup();                                                                   \
+            return rc;                                                                   \
+        }                                                                                \
+    } while (0)
+#define KD_TRY(expr)          \
+    do {                      \
+        rc = (expr);          \
+        if (rc != AIY_OK) {   \
+            cleanup();        \
+            return rc;        \
+        }                     \
+    } while (0)
+    const int nd = std::min(ndev, W);
+    for (int a = 0; a < nd; ++a)
+        for (int b = 0; b < nd; ++b) {
+            if (a == b) continue;
+            int can = 0;
+            KD_CHECK(hipDeviceCanAccessPeer(&can, a, b));
+            if (!can) {
+                rc = fail(AIY_HIP_ERROR, "device %d cannot access device %d: the direct schedule "
+                          "reads peer memory (use depth >= 1)", a, b);
+                cleanup();
+                return rc;
+            }
+            KD_CHECK(hipSetDevice(a));
+            const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) KD_CHECK(e);
+            (void)hipGetLastError();
+        }
+    for (int q = 0; q < W; ++q) {
+        DShard& sh = S[q];
+        sh.dev = q % ndev;
+        KD_CHECK(hipSetDevice(sh.dev));
+        KD_CHECK(hipStreamCreateWithFlags(&sh.st, hipStreamNonBlocking));
+        for (auto& e : sh.done) KD_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        for (int b = 0; b < 2; ++b) {
+            KD_CHECK(hipMalloc((void**)&sh.V[b], nb));
+            KD_CHECK(hipMalloc((void**)&sh.dV[b], nb));
+            KD_CHECK(hipMalloc((void**)&sh.tab[b], 2 * (size_t)C * sizeof(double*)));
+        }
+        KD_CHECK(hipMalloc((void**)&sh.kopt, nb));
+        KD_CHECK(hipMalloc((void**)&sh.Vold, nb));
+        KD_CHECK(hipMalloc((void**)&sh.red, 2 * sizeof(unsigned long long)));
+        KD_TRY(ks_dev_create_slice(k_grid, K_grid, B, P, params, nk, nK, sh.own.K0, sh.own.K1,
+                                   sh.own.s0, sh.own.s1, &sh.h));
+        KD_CHECK(hipMemcpyAsync(sh.V[0], value, nb, hipMemcpyHostToDevice, sh.st));
+        KD_CHECK(hipMemcpyAsync(sh.kopt, k_opt, nb, hipMemcpyHostToDevice, sh.st));
+    }
+    for (int q = 0; q < W; ++q) {  // column tables: column c of parity b lives at its owner
+        DShard& sh = S[q];
+        KD_CHECK(hipSetDevice(sh.dev));
+        for (int b = 0; b < 2; ++b) {
+            std::vector<const double*> t(2 * (size_t)C);
+            for (int c = 0; c < C; ++c) {
+                const DShard& o = S[owner[c]];
+                t[c] = o.V[b] + (size_t)c * nk;
+                t[C + c] = o.dV[b] + (size_t)c * nk;
+            }
+            KD_CHECK(hipMemcpy(sh.tab[b], t.data(), t.size() * sizeof(double*), hipMemcpyHostToDevice));
+        }
+        // the slopes of the own columns of the incoming value (what sweep 1 and the first
+        // improvement read), then "sweep 0 writing parity 0" is done
+        KD_TRY(ks_dev_slopes_own(sh.h, sh.V[0], sh.dV[0], sh.st));
+        KD_CHECK(hipEventRecord(sh.done[0], sh.st));
+    }
+    int cur = 0;
+    auto wait_nbrs = [&](DShard& sh) -> int {  // the neighbours' sweep that wrote parity cur
+        for (int o : sh.nbr) AIY_HIP(hipStreamWaitEvent(sh.st, S[o].done[cur], 0));
+        return AIY_OK;
+    };
+    double rel = NAN;
+    int64_t it;
+    std::vector<unsigned long long> hred(2 * W);
+    for (it = 1; it <= max_vfi; ++it) {
+        for (auto& sh : S) {  // value_old = value (:145), own columns
+            KD_CHECK(hipSetDevice(sh.dev));
+            for (int s = sh.own.s0; s < sh.own.s1; ++s) {
+                const size_t off = (size_t)(s * nK + sh.own.K0) * nk;
+                KD_CHECK(hipMemcpyAsync(sh.Vold + off, sh.V[cur] + off,
+                                        (size_t)(sh.own.K1 - sh.own.K0) * colb,
+                                        hipMemcpyDeviceToDevice, sh.st));
+            }
+        }
+        if ((it - 1) % 5 == 0) {  // policy improvement (:148-168), forecast columns in place
+            for (auto& sh : S) {
+                KD_CHECK(hipSetDevice(sh.dev));
+                KD_TRY(wait_nbrs(sh));
+                KD_TRY(ks_dev_set_columns(sh.h, (const void* const*)sh.tab[cur]));
+                KD_TRY(ks_dev_improve_direct(sh.h, sh.kopt, sh.st));
+            }
+        }
+        for (int64_t hs = 0; hs < howard_steps; ++hs) {  // Jacobi Howard sweeps (:172-192)
+            for (auto& sh : S) {
+                KD_CHECK(hipSetDevice(sh.dev));
+                KD_TRY(wait_nbrs(sh));
+                KD_TRY(ks_dev_set_columns(sh.h, (const void* const*)sh.tab[cur]));
+                KD_TRY(ks_dev_howard_fused(sh.h, sh.V[cur], sh.dV[cur], sh.kopt, sh.V[cur ^ 1],
+                                           sh.dV[cur ^ 1], sh.st));
+                KD_CHECK(hipEventRecord(sh.done[cur ^ 1], sh.st));
+            }
+            cur ^= 1;
+        }
+        for (int q = 0; q < W; ++q) {  // :195, NaN ignored, max over shards
+            DShard& sh = S[q];
+            KD_CHECK(hipSetDevice(sh.dev));
+            KD_TRY(ks_dev_reldiff(sh.h, sh.V[cur], sh.Vold, sh.red, sh.st));
+            KD_CHECK(hipMemcpyAsync(&hred[2 * q], sh.red, 2 * sizeof(unsigned long long),
+                                    hipMemcpyDeviceToHost, sh.st));
+        }
+        double mx = NAN;
+        for (int q = 0; q < W; ++q) {
+            KD_CHECK(hipSetDevice(S[q].dev));
+            KD_CHECK(hipStreamSynchronize(S[q].st));
+            if (hred[2 * q + 1]) {
+                const double d = aiy_bitsd(hred[2 * q]);
+                if (d == d && !(mx >= d)) mx = d;
+            }
+        }
+        rel = mx;
+        if (rel < tol) break;
+    }
+    if (it > max_vfi) it = max_vfi;
+    for (auto& sh : S) {  // every shard's own columns of value and k_opt
+        KD_CHECK(hipSetDevice(sh.dev));
+        for (int s = sh.own.s0; s < sh.own.s1; ++s) {
+            const size_t off = (size_t)(s * nK + sh.own.K0) * nk;
+            const size_t bytes = (size_t)(sh.own.K1 - sh.own.K0) * colb;
+            KD_CHECK(hipMemcpyAsync(value + off, sh.V[cur] + off, bytes, hipMemcpyDeviceToHost, sh.st));
+            KD_CHECK(hipMemcpyAsync(k_opt + off, sh.kopt + off, bytes, hipMemcpyDeviceToHost, sh.st));
+        }
+        KD_CHECK(hipStreamSynchronize(sh.st));
+    }
+    cleanup();
+    *iters = it;
+    *rel_diff = rel;
+    return AIY_OK;
+#undef KD_CHECK
+#undef KD_TRY
+}
+
 int ks_vfi_solve_sharded_impl(double* value, double* k_opt, const double* k_grid,
                               const double* K_grid, const double* B, const double* P,
                               const double* params, int64_t nk, int64_t nK,
@@ -336,13 +557,17 @@ extern "C" int ks_vfi_solve_sharded(double* value, double* k_opt, const double* 
         return fail(AIY_BAD_ARG, "NULL argument");
     if (max_vfi < 1 || howard_steps < 0) return fail(AIY_BAD_ARG, "max_vfi >= 1, howard_steps >= 0");
     if (nk < 3 || nK < 1) return fail(AIY_BAD_SHAPE, "need k_size >= 3 and K_size >= 1");
-    if (n_shards < 1 || depth < 1) return fail(AIY_BAD_ARG, "n_shards >= 1 and depth >= 1");
+    if (n_shards < 1 || depth < 0) return fail(AIY_BAD_ARG, "n_shards >= 1 and depth >= 0");
     std::lock_guard<std::mutex> lk(host_mutex());
     int cur = 0;
     (void)hipGetDevice(&cur);
-    const int rc = ks_vfi_solve_sharded_impl(value, k_opt, k_grid, K_grid, B, P, params, nk, nK,
-                                             howard_steps, tol, max_vfi, n_shards, depth, iters,
-                                             rel_diff);
+    const int rc =
+        depth == 0 ? ks_vfi_solve_direct_impl(value, k_opt, k_grid, K_grid, B, P, params, nk, nK,
+                                              howard_steps, tol, max_vfi, n_shards, iters,
+                                              rel_diff)
+                   : ks_vfi_solve_sharded_impl(value, k_opt, k_grid, K_grid, B, P, params, nk,
+                                               nK, howard_steps, tol, max_vfi, n_shards, depth,
+                                               iters, rel_diff);
     (void)hipSetDevice(cur);
     return rc;
 }

@@ -276,12 +276,36 @@ class HipShard:
         check(lib().ks_dev_howard_fused(self._h, ptr(V), ptr(dV), ptr(kopt), ptr(Vout),
                                         ptr(dVout), stream_handle(None)))
 
+    # the direct schedule (ks_vfi_solve_sharded depth = 0): forecast columns read in place
+    def set_columns(self, table):
+        """table: device int64 tensor of 4·nK value-column then 4·nK slope-column addresses
+        (None: back to the caller's arrays)."""
+        check(lib().ks_dev_set_columns(self._h, ptr(table)))
+
+    def slopes_own(self, V, dV):
+        check(lib().ks_dev_slopes_own(self._h, ptr(V), ptr(dV), stream_handle(None)))
+
+    def improve_direct(self, kopt):
+        check(lib().ks_dev_improve_direct(self._h, ptr(kopt), stream_handle(None)))
+
     def reldiff(self, V, Vold):
         import torch
         out = torch.zeros(2, dtype=torch.int64, device=V.device)
         check(lib().ks_dev_reldiff(self._h, ptr(V), ptr(Vold), ptr(out), stream_handle(None)))
         o = out.cpu()
         return float(o[0:1].view(torch.float64)[0]) if int(o[1]) != 0 else math.nan
+
+
+def column_table(owners_V, owners_dV, owner, nk):
+    """The direct schedule's column table of one shard: column c of value / slopes lives in the
+    buffers of shard owner[c] (owners_V[q] / owners_dV[q]: that shard's (4, K, k) tensors).
+    Returns a device int64 tensor of 4·nK + 4·nK addresses."""
+    import torch
+    C = len(owner)
+    dev = owners_V[0].device
+    addr = [owners_V[owner[c]].data_ptr() + 8 * c * nk for c in range(C)] + \
+           [owners_dV[owner[c]].data_ptr() + 8 * c * nk for c in range(C)]
+    return torch.tensor(addr, dtype=torch.int64, device=dev)
 
 
 def _exchange(V, rank, world, nK, bounds=None):

@@ -305,8 +305,9 @@ def main():
     if not args.no_ks:   # BASELINE configs[4]: KS VFI sharded over the same ranks (strong)
         import bench_ks
         legs["ks_sharded"] = bench_ks.ks_leg(pkg, world, rank, dev, depth=args.ks_depth)
-        if world == 1 and not args.no_extra:  # compute side of the N = 8 schedule, on this GPU
-            legs["ks_sharded"]["ghost_model"] = bench_ks.ghost_model(pkg, dev)
+        if world == 1 and not args.no_extra:  # compute side of the N = 8 schedules, on this GPU
+            legs["ks_sharded"]["direct_model"] = bench_ks.direct_model(pkg, dev)
+            legs["ks_sharded"]["ghost_model"] = bench_ks.ghost_model(pkg, dev, depths=(4,))
         progress("ks_sharded done")
     if not args.no_ge:   # BASELINE configs[3]: multisection GE over the same ranks
         legs["ge_batch"] = BL.ge_batch_leg(pkg, world, rank, dev)

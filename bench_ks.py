@@ -200,6 +200,76 @@ def ghost_model(pkg, dev, world=8, nk=32768, nK=64, depths=(1, 2, 3, 4, 6, 8), s
                     "HIP events on the stream (tools/ks_ghost_probe.py gives the per-kernel split)"}
 
 
+def direct_model(pkg, dev, world=8, nk=32768, nK=64, sweeps=24, howard=50):
+    """Compute side of the direct (peer-read) schedule — ks_vfi_solve_sharded(depth = 0) — on ONE
+    GPU: `world` emulated shards ((K, Z) slices, even K ranges), each with its own double-buffered
+    value / slope arrays; each shard's improvement and fused Howard sweeps read the forecast
+    columns in the OTHER shards' buffers through its column table (ks_dev_set_columns), as on
+    `world` devices with peer pointers.  Each shard is timed alone (HIP events on the stream):
+    its GPU time per sweep and per improvement is what its device does at N = world between the
+    stream-event waits on its neighbours.  Returns the slowest shard's figures and the projected
+    VFI iteration (improvement + `howard` sweeps, waits not included)."""
+    import numpy as np
+    import torch
+    kd = pkg.ks_dist
+    kg, Kg, P, V0 = pkg.calibration.krusell_smith(k_size=nk, K_size=nK)
+    B = np.array([0.1, 0.97, 0.08, 0.975])
+    V = torch.as_tensor(np.ascontiguousarray(V0.transpose(2, 1, 0)), device=dev)
+    owner = [0] * (4 * nK)
+    slices = [kd.shard_slices(nK, q, world) for q in range(world)]
+    for q, (K0, K1, s0, s1) in enumerate(slices):
+        for sidx in range(s0, s1):
+            for K in range(K0, K1):
+                owner[sidx * nK + K] = q
+    sh = [kd.HipShard(kg, Kg, B, P, pkg.ks_params(), *slices[q]) for q in range(world)]
+    Vb = [[V.clone(), V.clone()] for _ in range(world)]
+    dVb = [[torch.empty_like(V), torch.empty_like(V)] for _ in range(world)]
+    for q in range(world):
+        sh[q].slopes_own(Vb[q][0], dVb[q][0])
+        dVb[q][1].copy_(dVb[q][0])
+    ko = torch.ones_like(V)
+    tabs = [[kd.column_table([Vb[p][b] for p in range(world)], [dVb[p][b] for p in range(world)],
+                             owner, nk) for b in range(2)] for _ in range(world)]
+    torch.cuda.synchronize()
+    ev = lambda: torch.cuda.Event(enable_timing=True)
+    imp, swp = [], []
+    for q in range(world):
+        sh[q].set_columns(tabs[q][0])
+        sh[q].improve_direct(ko)  # warm-up
+        e0, e1 = ev(), ev()
+        e0.record()
+        sh[q].improve_direct(ko)
+        e1.record()
+        torch.cuda.synchronize()
+        imp.append(e0.elapsed_time(e1))
+        cur = 0
+
+        def run(n):
+            nonlocal cur
+            for _ in range(n):
+                sh[q].set_columns(tabs[q][cur])
+                sh[q].howard_fused(Vb[q][cur], dVb[q][cur], ko, Vb[q][cur ^ 1], dVb[q][cur ^ 1])
+                cur ^= 1
+        run(2)
+        e0, e1 = ev(), ev()
+        e0.record()
+        run(sweeps)
+        e1.record()
+        torch.cuda.synchronize()
+        swp.append(e0.elapsed_time(e1) / sweeps)
+    for x in sh:
+        x.close()
+    it_ms = max(imp) + howard * max(swp)
+    return {"world": world, "sweeps": sweeps, "improve_ms_by_shard": imp,
+            "gpu_ms_per_sweep_by_shard": swp, "gpu_ms_per_sweep_slowest": max(swp),
+            "improve_ms_slowest": max(imp), "projected_vfi_iteration_ms": it_ms,
+            "note": f"direct schedule (ks_vfi_solve_sharded depth 0) emulated on one GPU: each of "
+                    f"{world} shards timed alone, reading the other shards' buffers through its "
+                    f"column table; projected iteration = slowest improvement + {howard} x "
+                    f"slowest sweep (the per-sweep stream-event waits between devices are not in "
+                    f"it; no columns are copied)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nk", type=int, default=32768)
@@ -209,6 +279,8 @@ def main():
     ap.add_argument("--depth", type=int, default=None, help="Howard sweeps per exchange")
     ap.add_argument("--ghost-model", action="store_true",
                     help="one GPU: compute time per sweep vs depth for emulated 8-rank shards")
+    ap.add_argument("--direct-model", action="store_true",
+                    help="one GPU: per-shard time of the direct (peer-read) schedule, 8 shards")
     ap.add_argument("--gpus", type=int, default=1, help="ranks (started here when no launcher)")
     args = ap.parse_args()
     import bench_launch
@@ -223,6 +295,8 @@ def main():
     dev = torch.device("cuda", local)
     if args.ghost_model:
         out = ghost_model(bench.load_pkg(), dev, nk=args.nk, nK=args.nK)
+    elif args.direct_model:
+        out = direct_model(bench.load_pkg(), dev, nk=args.nk, nK=args.nK)
     else:
         out = ks_leg(bench.load_pkg(), world, rank, dev, args.nk, args.nK, args.howard,
                      args.exchange, depth=args.depth)

@@ -164,8 +164,11 @@ int ks_vfi_solve(double* value, double* k_opt, const double* k_grid, const doubl
  * enabled between the devices in use.  Howard sweeps run in blocks of `depth`: before a block
  * each shard receives the value columns of its ghost rectangle (every column its next `depth`
  * sweeps read, peer copies over xGMI) and sweeps the shrinking rectangles with the fused
- * Howard+slopes kernel — one exchange per block, event-synchronised on the streams.  Results
- * equal the single-device solve bit for bit for every n_shards and depth. */
+ * Howard+slopes kernel — one exchange per block, event-synchronised on the streams.  depth = 0:
+ * the direct schedule — no copies and no ghost sweeps: every sweep reads each forecast column
+ * where its owner keeps it (peer pointers; needs peer access between the devices in use) and
+ * waits only for its neighbours' previous sweep (stream-event waits).  Results equal the
+ * single-device solve bit for bit for every n_shards and depth. */
 int ks_vfi_solve_sharded(double* value, double* k_opt, const double* k_grid,
                          const double* K_grid, const double* B, const double* P,
                          const double* params, int64_t nk, int64_t nK, int64_t howard_steps,
@@ -378,6 +381,15 @@ int ks_dev_slopes(ks_dev* h, const double* V, double* dV, void* stream);
 int ks_dev_howard_fused(ks_dev* h, const double* V, const double* dV, const double* kopt,
                         double* Vout, double* dVout, void* stream);
 int ks_dev_reldiff(ks_dev* h, const double* V, const double* Vold, void* out, void* stream);
+/* The direct (peer-read) schedule of ks_vfi_solve_sharded(depth = 0): each shard keeps only its
+ * own columns current and reads every forecast column where its owner keeps it — table = a
+ * device array of 4·K_size value-column pointers then 4·K_size slope-column pointers (into the
+ * owners' buffers on this device or a peer; NULL restores the caller's full arrays), used by
+ * ks_dev_howard_fused (its V / dV arguments are then not read) and ks_dev_improve_direct.
+ * ks_dev_slopes_own writes the slopes of the shard's own columns (the schedule's start). */
+int ks_dev_set_columns(ks_dev* h, const void* const* table);
+int ks_dev_slopes_own(ks_dev* h, const double* V, double* dV, void* stream);
+int ks_dev_improve_direct(ks_dev* h, double* kopt, void* stream);
 /* Ghost shards (ks_dist.py exchanges halos every m Howard sweeps and sweeps a widening
  * rectangle of other ranks' columns redundantly in between — same kernels, so still bit-exact):
  * h uses owner's segment-hint array (same grid and device; destroying owner while a handle

@@ -153,3 +153,39 @@ def test_fused_howard_equals_two_launch_sweep(pkg, gpu):
         assert torch.equal(torch.isnan(x), torch.isnan(y)), nk
         assert torch.equal(torch.nan_to_num(x, nan=0.0), torch.nan_to_num(y, nan=0.0)), nk
         sh.close()
+
+
+@pytest.mark.parametrize("shards", [8, 6, 5, 3, 2, 1])
+def test_direct_peer_reads_reference_size(pkg, gpu, golden, shards):
+    """The direct schedule (ks_vfi_solve_sharded depth = 0): no column copies, no ghost sweeps —
+    every Howard sweep and improvement reads each forecast column (Krusell_Smith_VFI.m:343-349)
+    where its owning shard keeps it (pointer tables into the owners' double buffers) after
+    stream-event waits on the neighbours' previous sweep.  Up to 8 (K, Z) slices on this card
+    at the reference grid: bit for bit the single-device solve."""
+    g, prm = _setup(golden)
+    B = np.array([0.1, 0.97, 0.08, 0.975])
+    args = (g["V0"], g["V0"] * 0 + 1.0, g["k_grid"], g["K_grid"], B, g["P"], prm)
+    R1 = pkg.ks_vfi_solve(*args, howard_steps=10, tol=1e-6, max_vfi=12)
+    Rs = pkg.ks_vfi_solve(*args, howard_steps=10, tol=1e-6, max_vfi=12, n_devices=shards,
+                          depth=0)
+    assert Rs["iters"] == R1["iters"] and Rs["rel_diff"] == R1["rel_diff"]
+    assert np.array_equal(Rs["value"], R1["value"])
+    assert np.array_equal(Rs["k_opt"], R1["k_opt"])
+
+
+@pytest.mark.parametrize("nk,nK,howard,vfi", [(4096, 16, 7, 6), (32768, 64, 3, 1)])
+def test_direct_peer_reads_large(pkg, gpu, nk, nK, howard, vfi):
+    """The direct schedule on 8 shards at k = 4,096, K = 16 (multi-block columns, 2 policy
+    improvements) and at the scaling size k = 32,768, K = 64 (8.4 M nodes, one VFI iteration):
+    bit for bit the single-device solve."""
+    kg, Kg, P, V0 = pkg.calibration.krusell_smith(k_size=nk, K_size=nK)
+    prm = pkg.ks_params()
+    B = np.array([0.1, 0.97, 0.08, 0.975])
+    k0 = np.ones_like(V0)
+    R1 = pkg.ks_vfi_solve(V0, k0, kg, Kg, B, P, prm, howard_steps=howard, tol=0.0, max_vfi=vfi)
+    R8 = pkg.ks_vfi_solve(V0, k0, kg, Kg, B, P, prm, howard_steps=howard, tol=0.0, max_vfi=vfi,
+                          n_devices=8, depth=0)
+    assert R1["iters"] == R8["iters"] == vfi and R1["rel_diff"] == R8["rel_diff"]
+    assert np.array_equal(R1["value"], R8["value"])
+    assert np.array_equal(R1["k_opt"], R8["k_opt"])
+    assert np.isfinite(R1["value"]).all()
