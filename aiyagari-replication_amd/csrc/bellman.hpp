@@ -24,6 +24,9 @@ struct BellArgs {
     const double* dis;  // psi*L^(1+eta)/(1+eta) per level (A3) or nullptr
     const int* hint;    // nullable: last sweep's linear index (l + Nl*k)
     int* mom;           // nullable [N][Na]: the argmax's shift in k over the last hinted sweep
+    const int* perm;    // nullable [N·ntile]: tree dispatch order (block b → item perm[b]); see
+                        // ws_tree_perm — work order only
+    int tw;             // tree tile width (states per one-wave tile, R = 1); 0 = 64
                         // (tree kernel: read for an extrapolated start, rewritten; heuristic
                         // only — any start is a valid screening bar)
     // scratch
@@ -73,6 +76,8 @@ inline bool bell_ev_mfma(int N, int variant) {
     if (variant >= 0 && (variant & 32768)) return true;
     return N >= kEvMfmaMinN;
 }
+// states per tree tile (R states per lane): 64·R, or A.tw for the one-state-per-lane geometry
+inline int bell_tile_width(const BellArgs& A, int R) { return (R == 1 && A.tw > 0) ? A.tw : 64 * R; }
 int launch_bell_ev_mfma(const BellArgs& A, hipStream_t st);
 int launch_bell_table(const BellArgs& A, hipStream_t st);
 int launch_bell_kf(const BellArgs& A, hipStream_t st);

@@ -870,7 +870,8 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
                  "s"(A0.variant), "s"(A0.C), "s"(A0.nb512), "s"(A0.sigma), "s"(A0.trace));
     const long long t_boot = (INS && A0.trace) ? (long long)wall_clock64() : 0;  // (instrumentation)
     const long long c_boot = (INS && A0.trace) ? (long long)__builtin_amdgcn_s_memtime() : 0;
-    int item = (A0.variant & 16) ? xcd_remap(block_id, nblocks) : block_id;
+    int item = A0.perm ? A0.perm[block_id]
+                       : ((A0.variant & 16) ? xcd_remap(block_id, nblocks) : block_id);
     BellArgs A = A0;
     if (A0.C > 1) {  // batched candidates: blocks [c·N·ntile, (c+1)·N·ntile) are candidate c's
         const int c = item / (A0.N * ntile);
@@ -886,7 +887,9 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
     const double* __restrict__ Drow = A.Dt + (size_t)i * Na;
     const double* __restrict__ ev = A.EV + (size_t)i * Na;
     const double y = A.w * A.s[i];
-    const int jbase = tile * (64 * R);
+    // states per tile: 64·R, or A.tw (< 64, R = 1: lanes tw..63 idle) — see bell_tile_width
+    const int TW = (R == 1 && A0.tw > 0) ? A0.tw : 64 * R;
+    const int jbase = tile * TW;
     __shared__ double2 s_cand[W][512];  // each wave's current superblock: (a_k, D_k)
     __shared__ unsigned long long s_pass[W];  // (first superblock, bit 12) per-wave pass masks
     // W >= 2 (cooperating waves): registers were budgeted for 5 waves per SIMD, so the staging
@@ -906,7 +909,7 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int j = jbase + r * 64 + lane;
-        vo_pre[r] = (j < Na && wave == 0) ? A.v_old[(size_t)i * Na + j] : 0.0;
+        vo_pre[r] = (j < Na && r * 64 + lane < TW && wave == 0) ? A.v_old[(size_t)i * Na + j] : 0.0;
     }
 
     double x[R], best[R];
@@ -920,7 +923,7 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int j = jbase + r * 64 + lane;
-        okr[r] = j < Na;
+        okr[r] = j < Na && r * 64 + lane < TW;
         const size_t t = (size_t)i * Na + (okr[r] ? j : 0);
         x[r] = okr[r] ? (1 + A.r) * a[j] : 0.0;
         best[r] = __builtin_nan("");
@@ -1076,7 +1079,7 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
         if (A.r > -1.0) {
             // coh is increasing in j when 1 + r > 0, so every feasible prefix kf is
             // non-decreasing along the tile: the maximum sits in the last valid lane
-            const int jl = min(Na - 1, jbase + 64 * R - 1);  // the tile's last state
+            const int jl = min(Na - 1, jbase + TW - 1);  // the tile's last state
             kg = readlane_i(kg, (jl - jbase) & 63);
         } else {
             for (int off = 32; off > 0; off >>= 1) kg = max(kg, __shfl_xor(kg, off));
@@ -1751,7 +1754,7 @@ static void run_screen(const BellArgs& A, hipStream_t st) {
 template <int NP, bool LAB, int R, int W>
 static void tree_geo(const BellArgs& A, hipStream_t st) {
     constexpr int LB = LAB ? 5 : 1;
-    const int ntile = cdiv(A.Na, 64 * R);
+    const int ntile = cdiv(A.Na, bell_tile_width(A, R));
     const int grid = std::max(A.C, 1) * A.N * ntile;
     if (A.trace || A.hitcount)
         launch_dispatch_timed(bell_tree_kernel<NP, LAB, R, LB, W, true>, dim3(grid), dim3(64 * W),

@@ -123,6 +123,8 @@ int ws_timing_drain(aiy_ws* ws) {
 }
 
 // ---------------------------------------------------------------------------- Bellman sweep
+bool tree_perm_eligible(const BellArgs& A);
+int ws_tree_perm(aiy_ws* ws, const BellArgs& A, hipStream_t st);
 // validation, the kernel arguments of one sweep, and the cached feasible prefixes
 static int bell_args(aiy_ws* ws, const BellCall& c, BellArgs& A, hipStream_t st) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
@@ -155,6 +157,15 @@ static int bell_args(aiy_ws* ws, const BellCall& c, BellArgs& A, hipStream_t st)
                                      : (ws->Na <= 4096 ? (c.labor ? 4 | 4096 : 2) : 16);
     A.variant = var;
     A.ev_mfma = bell_ev_mfma(A.N, ws->variant);
+    // (variant bit 13) one-wave tiles of tw < 64 states, tw = ceil(N·Na / (3 waves × 1,024
+    // SIMDs)): every SIMD holds three tiles instead of two or three (the 3-wave SIMDs end the
+    // launch, tools/tree_trace.py); lanes tw..63 idle.  Work split only.
+    A.tw = 0;
+    if ((var & 8192) && !c.labor && (var & (1 | 2 | 4 | 8)) == 0) {
+        const int64_t tw = (ws->N * ws->Na + 3 * 1024 - 1) / (3 * 1024);
+        A.tw = (int)std::max<int64_t>(16, std::min<int64_t>(64, tw));
+        if (A.tw == 64) A.tw = 0;
+    }
     A.r = c.r;
     A.w = c.w;
     A.beta = c.beta;
@@ -222,7 +233,76 @@ static int bell_args(aiy_ws* ws, const BellCall& c, BellArgs& A, hipStream_t st)
         ws->kf_ok = true;
         ws->kf_r = c.r; ws->kf_w = c.w; ws->kf_a = c.a; ws->kf_s = c.s; ws->kf_L = A.L;
         ws->kf_Nl = A.Nl; ws->kf_lab = A.labor;
+        ws->perm_ok = false;
     }
+    A.perm = nullptr;
+    if (tree_perm_eligible(A)) {
+        const int key = A.tw * 4096 + (A.variant & (64 | 2048));
+        if (!ws->perm_ok || ws->perm_key != key) {
+            AIY_TRY(ws_tree_perm(ws, A, st));
+            ws->perm_key = key;
+        }
+        A.perm = ws->tree_perm;
+    }
+    return AIY_OK;
+}
+
+// Dispatch order of the one-wave-per-tile A1 tree launch (variant bit 6).  A launch of N·ntile
+// one-wave items on 1,024 SIMDs puts three waves on some SIMDs — the last-dispatched items of
+// each XCD — and those items end the launch (tools/tree_trace.py: every last-to-finish item sits
+// on a 3-wave SIMD).  The order keeps each XCD's item range (xcd_remap: the same L2 sets) and
+// deals it heaviest first, by the feasible prefix of the tile's last state (the bound tree's
+// superblock count), so the third waves are the cheapest tiles.  Work order only.
+bool tree_perm_eligible(const BellArgs& A) {
+    return (A.variant & (64 | 2048)) && A.tree && !A.labor && A.C <= 1 && A.np >= 1 && A.np <= 8 &&
+           (A.variant & (1 | 2 | 4 | 8)) == 0;
+}
+constexpr int kSimdsPerXcd = 128;  // MI355X: 32 CUs x 4 SIMDs per XCD
+int ws_tree_perm(aiy_ws* ws, const BellArgs& A, hipStream_t st) {
+    const int N = A.N, Na = A.Na, TW = bell_tile_width(A, 1), ntile = (Na + TW - 1) / TW;
+    const int G = N * ntile;
+    std::vector<int> kf((size_t)N * Na);
+    AIY_HIP(hipMemcpyAsync(kf.data(), A.kf, kf.size() * sizeof(int), hipMemcpyDeviceToHost, st));
+    AIY_HIP(hipStreamSynchronize(st));
+    std::vector<int> perm(G);
+    const int q = G / 8, r = G % 8;
+    for (int x = 0; x < 8; ++x) {
+        const int start = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+        const int size = x < r ? q + 1 : q;
+        std::vector<int> items(size);
+        for (int u = 0; u < size; ++u) items[u] = start + u;
+        auto cost = [&](int it) {
+            const int i = it / ntile, t = it % ntile;
+            const int jl = std::min(Na - 1, t * TW + TW - 1);
+            return kf[(size_t)i * Na + jl];
+        };
+        if (A.variant & 64) {  // the whole range heaviest first
+            std::stable_sort(items.begin(), items.end(),
+                             [&](int a, int b) { return cost(a) > cost(b); });
+        } else {  // (bit 11) row-major, but the range's cheapest tiles dispatched last
+            const int tail = std::max(0, std::min(size, size - 2 * kSimdsPerXcd));
+            std::vector<int> by(items);
+            std::stable_sort(by.begin(), by.end(), [&](int a, int b) { return cost(a) < cost(b); });
+            std::vector<char> last(G, 0);
+            for (int u = 0; u < tail; ++u) last[by[u]] = 1;
+            std::vector<int> out;
+            for (int it : items)
+                if (!last[it]) out.push_back(it);
+            for (int u = tail - 1; u >= 0; --u) out.push_back(by[u]);
+            items.swap(out);
+        }
+        for (int u = 0; u < size; ++u) perm[(size_t)u * 8 + x] = items[u];  // block b = 8u + x
+    }
+    if (!ws->tree_perm || ws->perm_cap < G) {
+        if (ws->tree_perm) (void)hipFree(ws->tree_perm);
+        ws->tree_perm = nullptr;
+        AIY_HIP(hipMalloc((void**)&ws->tree_perm, (size_t)G * sizeof(int)));
+        ws->perm_cap = G;
+    }
+    AIY_HIP(hipMemcpyAsync(ws->tree_perm, perm.data(), (size_t)G * sizeof(int),
+                           hipMemcpyHostToDevice, st));
+    AIY_HIP(hipStreamSynchronize(st));
+    ws->perm_ok = true;
     return AIY_OK;
 }
 

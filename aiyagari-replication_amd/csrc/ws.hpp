@@ -37,6 +37,9 @@ struct aiy_ws {
     const void* kf_L = nullptr;
     int64_t kf_Nl = 0;
     bool kf_lab = false;
+    int* tree_perm = nullptr;  // tree dispatch order for the cached kf (ws_tree_perm)
+    int perm_cap = 0, perm_key = 0;
+    bool perm_ok = false;
     int* partial = nullptr;
     size_t partial_cap = 0;
     unsigned long long* diff = nullptr;      // device [2*kDiffSlots] {max bits, any}
@@ -157,7 +160,7 @@ struct aiy_ws {
     }
     void free_all() {
         void* ps[] = {EV, T, T32, Dm, Dm8, Dt, Dm512, touched, best0, idx0, mom, dis, kf, partial, diff, hitcount, trace, g0, g1, g2, gi,
-                      d_key, d_off, d_wr, d_mass, d_part, egm_x2, egm_y2, egm_seg};
+                      d_key, d_off, d_wr, d_mass, d_part, egm_x2, egm_y2, egm_seg, tree_perm};
         for (void* p : ps)
             if (p) (void)hipFree(p);
         free_spec();
@@ -171,6 +174,7 @@ struct aiy_ws {
         g0 = g1 = g2 = nullptr; gi = nullptr;
         egm_x2 = egm_y2 = nullptr;
         egm_seg = nullptr;
+        tree_perm = nullptr; perm_cap = 0; perm_ok = false;
         d_key = d_off = nullptr; d_wr = d_mass = d_part = nullptr;
         partial_cap = 0;
     }

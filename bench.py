@@ -420,9 +420,6 @@ def main():
             out["batch_config4_share"]["roofline"].update(
                 pmc=pm("batch"), traffic=tr("batch"),
                 pmc_source="profiles/r03_pmc_batch.json, r03_traffic_batch.json")
-            out["dist"]["roofline"].update(
-                pmc=pm("dist_push"), traffic=tr("dist_push"),
-                pmc_source="profiles/r03_pmc_dist_push.json, r03_traffic_dist_push.json")
             out["labor_vfi"] = {"Na400": BL.labor_leg(pkg, dev, 400, cpu_threads=threads,
                                                       cpu=not args.no_cpu_baseline),
                                 "Na20000": BL.labor_leg(pkg, dev, 20000, steps=5, reps=3, cpu=False)}
@@ -433,10 +430,16 @@ def main():
                                                       cpu_threads=threads)}
             out["labor_vfi"]["Na400"]["roofline"]["pmc"] = pm("labor_na400")
             out["labor_vfi"]["Na20000"]["roofline"]["pmc"] = pm("labor_na20000")
-            out["egm"]["Na20000"]["roofline"].update(
-                pmc={"egm_rhs_kernel": pm("egm_rhs"), "egm_interp_kernel": pm("egm_interp")},
-                traffic=(tr("egm_rhs") or 0) + (tr("egm_interp") or 0) or None,
-                pmc_source="profiles/r03_pmc_egm_{rhs,interp}.json, r03_traffic_egm_*.json")
+            pm4 = lambda n: ((_json_profile(f"r04_pmc_{n}.json") or {}).get("derived"))
+            tr4 = lambda n: ((_json_profile(f"r04_traffic_{n}.json") or {}).get("bytes_per_launch"))
+            for leg, nm in (("egm", "egm_chain"), ("labor_egm", "labor_egm_chain")):
+                out[leg]["Na20000"]["roofline"].update(
+                    pmc={"egm_chain_kernel": pm4(nm)}, traffic=tr4(nm),
+                    pmc_source=f"profiles/r04_pmc_{nm}.json, r04_traffic_{nm}.json (the timed "
+                               f"kernel, egm_chain_kernel, 200 launches of the solve loop)")
+            out["dist"]["roofline"].update(
+                pmc=pm4("dist_push"), traffic=tr4("dist_push"),
+                pmc_source="profiles/r04_pmc_dist_push.json, r04_traffic_dist_push.json")
         if not args.no_panel and world == 1:   # F3/F2: KS shock panel + agent simulation
             import bench_panel
             out["ks_panel"] = bench_panel.panel_leg(pkg, dev, cpu_threads=threads)

@@ -95,6 +95,8 @@ def ks_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, exchange="halo", r
                                   f"out) x {nodes // world} nodes per GPU / sweep time; the "
                                   f"working set (V, dV, k_opt: 200 MB) is HBM-resident"},
             "pmc": _ks_pmc(),
+            "pmc_source": "profiles/r04_pmc_ks_howard_slopes.json, "
+                          "profiles/r04_traffic_ks_howard_slopes.json (the timed kernel)",
             "scaling": "strong", "vfi_iteration_ms": (ti + th) * 1e3,
             "howard_ms_per_sweep": th / howard * 1e3, "improve_ms": ti * 1e3,
             "workload": f"Krusell_Smith_VFI k={nk} K={nK} S=4 ({nodes} nodes, BASELINE "
@@ -110,12 +112,12 @@ def ks_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, exchange="halo", r
 
 
 def _ks_pmc():
-    """Counter summaries of the two Howard-sweep kernels at this size (rocprofv3 --pmc passes
-    over `bench_ks.py --howard 10`, tools/exp/exp_r02b_s10.sh), if committed under profiles/."""
+    """Counter summary of the kernel this leg times — ks_howard_slopes_kernel, one launch per
+    Howard sweep at k = 32,768, K = 64 (rocprofv3 --pmc passes over tools/pmc_workloads_r04.py,
+    tools/exp/r04_g2.sh) — if committed under profiles/."""
     out = {}
-    for name, f, t in (("ks_howard_kernel", "r02b_pmc_ks_howard.json", "r02b_traffic_ks_howard.json"),
-                       ("ks_slopes_cols_kernel", "r02b_pmc_ks_slopes.json",
-                        "r02b_traffic_ks_slopes.json")):
+    for name, f, t in (("ks_howard_slopes_kernel", "r04_pmc_ks_howard_slopes.json",
+                        "r04_traffic_ks_howard_slopes.json"),):
         p, q = ROOT / "profiles" / f, ROOT / "profiles" / t
         if p.exists():
             d = json.loads(p.read_text())["derived"]

@@ -146,7 +146,8 @@ def test_full_size_bitwise_vs_oracle(pkg, gpu):
     assert (pcs > 0).all()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 6, 8, 12, 16, 32, 96, 512, 4098, 4100, 4102])
+@pytest.mark.parametrize("variant", [0, 1, 2, 6, 8, 12, 16, 32, 96, 512, 4098, 4100, 4102, 80, 2064,
+                                     8192, 8208, 8272, 10256])
 def test_screen_stress_noisy_value(pkg, gpu, variant):
     """Rough value functions put many candidates within rounding distance of the running best
     (near-ties everywhere, multi-modal objectives): the fp32 pre-screen, the fp64 screen and
@@ -166,3 +167,25 @@ def test_screen_stress_noisy_value(pkg, gpu, variant):
                                               mode=1, hint=hint, variant=variant, k_chunk=320)
             assert np.array_equal(vs, vo) and np.array_equal(is_, io), (Na, scale)
             assert np.array_equal(pks, pko) and np.array_equal(pcs, pco)
+
+
+@pytest.mark.parametrize("variant", [16, 80, 2064, 8208, 8272, 10256])
+def test_full_size_dispatch_orders_and_tile_widths(pkg, gpu, variant):
+    """Na = 20,000 (configs[1]): the tree's dispatch orders (bit 6: each XCD's range heaviest
+    first; bit 11: its cheapest tiles last) and the narrow one-wave tiles (bit 13: 46 states per
+    tile, three tiles per SIMD) change only the work split — a hinted warm sweep is bit-exact
+    against the C oracle for each."""
+    import torch
+    cal = no.calib_aiyagari(Na=20000, shocks="rouwenhorst")
+    a, s, P = cal["a_grid"], cal["s"], cal["P"]
+    w = no.wage(0.04, 0.36, 0.08)
+    c4 = no.calib_aiyagari(Na=400, shocks="rouwenhorst")
+    V4 = corc.vfi_solve(np.zeros((7, 400)), c4["a_grid"], c4["s"], c4["P"], 0.04, w, 0.96,
+                        5.0)["v_new"]
+    V = np.stack([np.interp(a, c4["a_grid"], V4[i]) for i in range(7)])
+    vo, io, pko, pco = corc.vfi_sweep(V, a, s, P, 0.04, w, 0.96, 5.0)
+    hint = np.clip(io + 3, 0, 19999)
+    vs, is_, pks, pcs = _device_sweep(pkg, torch, V, a, s, P, 0.04, w, 0.96, 5.0, mode=1,
+                                      hint=hint, variant=variant)
+    assert np.array_equal(vs, vo) and np.array_equal(is_, io)
+    assert np.array_equal(pks, pko) and np.array_equal(pcs, pco)

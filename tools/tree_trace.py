@@ -38,6 +38,8 @@ def main():
                 ms, _, _ = ws.timing()
                 ws.set_timing(False)
                 T = ws.trace()
+                if len(sys.argv) > 1 and "AIY_TRACE_DUMP" in __import__("os").environ:
+                    np.save(f"{__import__('os').environ['AIY_TRACE_DUMP']}_v{var}_s{q}.npy", T)
                 hw = (T[:, 2] >> 32) & 0xffffffff  # HW_REG_HW_ID of the item's wave
                 T[:, 2] &= 0xffffffff             # XCC id
                 dur = (T[:, 1] - T[:, 0]) / 100.0  # µs (100 MHz)
