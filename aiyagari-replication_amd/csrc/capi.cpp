@@ -152,9 +152,14 @@ static int bell_args(aiy_ws* ws, const BellCall& c, BellArgs& A, hipStream_t st)
     // 81.5 -> 70.3 (profiles/r02c_s6_*); A1 is neutral to it (16.4 us either way)
     // (Na > 4096: bit 13, tiles in descending j, is faster in a solve's early sweeps — sweep 25:
     // 34.9 vs 35.8 us — and slower once the policy has settled — sweep 100: 33.6 vs 32.8 us,
-    // whole solve to tol 9.37 vs 8.99 ms — so the default stays row-major, XCD-contiguous (16))
-    const int var = ws->variant >= 0 ? ws->variant
-                                     : (ws->Na <= 4096 ? (c.labor ? 4 | 4096 : 2) : 16);
+    // whole solve to tol 9.37 vs 8.99 ms — so the order stays row-major, XCD-contiguous (16)).
+    // Round 4, A1 at Na > 4096: bit 11 (each XCD's cheapest 2 x 128 tiles dispatched last, the
+    // rest row-major) over 16 alone, three alternating runs on one box: step 39.3 -> 36.3 us,
+    // solve to tol 8.74 -> 8.63 ms; heaviest-first (bit 6) 37.6 us / 8.75 ms; narrower tiles
+    // (bit 13) slower, 40.6 / 39.3 us (profiles/r04_g7_order_ab.txt)
+    const int var = ws->variant >= 0
+                        ? ws->variant
+                        : (ws->Na <= 4096 ? (c.labor ? 4 | 4096 : 2) : (c.labor ? 16 : 16 | 2048));
     A.variant = var;
     A.ev_mfma = bell_ev_mfma(A.N, ws->variant);
     // (variant bit 13) one-wave tiles of tw < 64 states, tw = ceil(N·Na / (3 waves × 1,024
