@@ -78,6 +78,14 @@ inline bool bell_ev_mfma(int N, int variant) {
 }
 // states per tree tile (R states per lane): 64·R, or A.tw for the one-state-per-lane geometry
 inline int bell_tile_width(const BellArgs& A, int R) { return (R == 1 && A.tw > 0) ? A.tw : 64 * R; }
+// one-wave tiles per workgroup (variant bits 16-17: 1, 2, 4, 8), used with a dispatch
+// permutation (A.perm, which then holds -1 in the last workgroup's unused slots); instantiated
+// for A1 at sigma = 5 (np = 4), one state per lane, one wave per tile
+inline int bell_tree_pack(const BellArgs& A) {
+    return (A.np == 4 && !A.labor && A.tree && (A.variant & (1 | 2 | 4 | 8)) == 0)
+               ? 1 << ((A.variant >> 16) & 3)
+               : 1;
+}
 int launch_bell_ev_mfma(const BellArgs& A, hipStream_t st);
 int launch_bell_table(const BellArgs& A, hipStream_t st);
 int launch_bell_kf(const BellArgs& A, hipStream_t st);

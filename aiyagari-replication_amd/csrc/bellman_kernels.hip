@@ -858,11 +858,15 @@ __global__ __launch_bounds__(256, MINW) void bell_screen_kernel(BellArgs A, int 
 // INS: the instrumented build (per-state work counters, per-item trace); the production
 // instantiation compiles every counter and time stamp out
 // The body of one work item (tile of row i); block_id / nblocks are the launch coordinates.
-template <int NP, bool LAB, int R, int LB, int W, bool INS>
+// PK > 1 (W = 1, variant bits 16-17): PK independent one-wave tiles share a workgroup (fewer
+// dispatches); each wave is its own item, `lw` its LDS slice, and no workgroup barrier runs.
+template <int NP, bool LAB, int R, int LB, int W, bool INS, int PK>
 __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, int block_id,
                                                int nblocks) {
+    static_assert(PK == 1 || W == 1, "packed workgroups hold one-wave tiles");
     const int lane = threadIdx.x & 63;
-    const int wave = readfirst(threadIdx.x >> 6);
+    const int lw = readfirst(threadIdx.x >> 6);  // this wave's LDS slice
+    const int wave = PK > 1 ? 0 : lw;            // its rank among the tile's cooperating waves
     // every kernel argument the start-up reads, in one batch of scalar loads (otherwise the
     // compiler fetches them in dependent rounds as the control flow reaches each use)
     asm volatile("" ::"s"(A0.a), "s"(A0.Dt), "s"(A0.EV), "s"(A0.kf), "s"(A0.hint), "s"(A0.v_old),
@@ -872,6 +876,7 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
     const long long c_boot = (INS && A0.trace) ? (long long)__builtin_amdgcn_s_memtime() : 0;
     int item = A0.perm ? A0.perm[block_id]
                        : ((A0.variant & 16) ? xcd_remap(block_id, nblocks) : block_id);
+    if (PK > 1 && item < 0) return;  // (the last workgroup's unused slots)
     BellArgs A = A0;
     if (A0.C > 1) {  // batched candidates: blocks [c·N·ntile, (c+1)·N·ntile) are candidate c's
         const int c = item / (A0.N * ntile);
@@ -890,7 +895,7 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
     // states per tile: 64·R, or A.tw (< 64, R = 1: lanes tw..63 idle) — see bell_tile_width
     const int TW = (R == 1 && A0.tw > 0) ? A0.tw : 64 * R;
     const int jbase = tile * TW;
-    __shared__ double2 s_cand[W][512];  // each wave's current superblock: (a_k, D_k)
+    __shared__ double2 s_cand[W * PK][512];  // each wave's current superblock: (a_k, D_k)
     __shared__ unsigned long long s_pass[W];  // (first superblock, bit 12) per-wave pass masks
     // W >= 2 (cooperating waves): registers were budgeted for 5 waves per SIMD, so the staging
     // and fine-screen software pipelines (two register sets each) are off and the screen
@@ -1049,7 +1054,7 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
         if constexpr (W > 1) {
 #pragma unroll
             for (int r = 0; r < R; ++r)  // (index exact as a double)
-                s_cand[wave][r * 64 + lane] = make_double2(best[r], (double)idx[r]);
+                s_cand[lw][r * 64 + lane] = make_double2(best[r], (double)idx[r]);
             __syncthreads();
             for (int v = 0; v < W; ++v)
 #pragma unroll
@@ -1150,7 +1155,7 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
         // the whole 64-block is staged, candidates past the feasible range are masked by fine()
         auto load_tk = [&](int bit, double2 (&tk)[8]) __attribute__((always_inline)) {
 #pragma unroll
-            for (int kk = 0; kk < 8; ++kk) tk[kk] = s_cand[wave][(bit << 3) + kk];
+            for (int kk = 0; kk < 8; ++kk) tk[kk] = s_cand[lw][(bit << 3) + kk];
         };
         auto fine = [&](int sbase, int k0, int k1, const double2 (&tk)[8])
                         __attribute__((always_inline)) {
@@ -1200,7 +1205,7 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
                 const int kk = __builtin_ctz(vote);
                 vote &= vote - 1;
                 const int k = k0 + kk;
-                const double2 tkk = s_cand[wave][k - sbase];
+                const double2 tkk = s_cand[lw][k - sbase];
 #pragma unroll
                 for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -1302,8 +1307,8 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
                         const int k1 = min(sbase + (b1 << 6) + lane, Na - 1);
                         v1 = make_double2(a[k1], Drow[k1]);
                     }
-                    s_cand[wave][(b0 << 6) + lane] = v0;
-                    if (b1 >= 0) s_cand[wave][(b1 << 6) + lane] = v1;
+                    s_cand[lw][(b0 << 6) + lane] = v0;
+                    if (b1 >= 0) s_cand[lw][(b1 << 6) + lane] = v1;
                 }
             } else {
 #pragma unroll
@@ -1322,7 +1327,7 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
             if constexpr (!LEAN)
 #pragma unroll
                 for (int b = 0; b < 8; ++b)
-                    if ((pass >> (8 * b)) & 0xffull) s_cand[wave][(b << 6) + lane] = st[b];
+                    if ((pass >> (8 * b)) & 0xffull) s_cand[lw][(b << 6) + lane] = st[b];
             __builtin_amdgcn_wave_barrier();  // a wave reads only its own slice
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             stamp(1);
@@ -1487,14 +1492,25 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
     if (INS && A.trace) {  // instrumentation (aiy_ws_set_timing bit 2): per-wave sums into wave 0
         __shared__ unsigned s_cnt[W][4];
         __shared__ unsigned s_pairs;
-        if (threadIdx.x == 0) s_pairs = 0;
-        __syncthreads();
-        atomicAdd(&s_pairs, lane_pairs);
-        if (lane == 0) {
-            s_cnt[wave][0] = nsup; s_cnt[wave][1] = nblk; s_cnt[wave][2] = nfine; s_cnt[wave][3] = nhits;
+        unsigned pairs = lane_pairs, sums[4] = {nsup, nblk, nfine, nhits};
+        if constexpr (W == 1) {  // one wave: a shuffle sum, no barrier (packed workgroups)
+            for (int o = 32; o > 0; o >>= 1) pairs += __shfl_xor(pairs, o);
+        } else {
+            if (threadIdx.x == 0) s_pairs = 0;
+            __syncthreads();
+            atomicAdd(&s_pairs, lane_pairs);
+            if (lane == 0) {
+                s_cnt[wave][0] = nsup; s_cnt[wave][1] = nblk; s_cnt[wave][2] = nfine; s_cnt[wave][3] = nhits;
+            }
+            __syncthreads();
+            pairs = s_pairs;
+            for (int c = 0; c < 4; ++c) {
+                unsigned sum = 0;
+                for (int v = 0; v < W; ++v) sum += s_cnt[v][c];
+                sums[c] = sum;
+            }
         }
-        __syncthreads();
-        if (threadIdx.x == 0) {
+        if (W == 1 ? lane == 0 : threadIdx.x == 0) {
             long long* tr = A.trace + 16 * (size_t)item;
             tr[0] = t_start;
             tr[1] = (long long)wall_clock64();
@@ -1502,17 +1518,13 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
             tr[2] = (long long)(unsigned)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) |
                     ((long long)(unsigned)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11))
                      << 32);
-            for (int c = 0; c < 4; ++c) {
-                long long sum = 0;
-                for (int v = 0; v < W; ++v) sum += s_cnt[v][c];
-                tr[3 + c] = sum;
-            }
+            for (int c = 0; c < 4; ++c) tr[3 + c] = sums[c];
             tr[7] = block_id;
             for (int c = 0; c < 4; ++c) tr[8 + c] = cyc[c];
             tr[12] = t_boot;                                   // kernel entry (wall clock)
             tr[13] = c_mark0 - c_boot;                         // start-up cycles (hint, climb)
             tr[14] = (long long)__builtin_amdgcn_s_memtime() - c_end;  // output cycles
-            tr[15] = s_pairs;  // (state, sub-block) pairs passing the 8-block bound
+            tr[15] = pairs;  // (state, sub-block) pairs passing the 8-block bound
         }
     }
     if (INS && A.hitcount) {  // instrumentation (aiy_ws_set_timing bit 1)
@@ -1527,12 +1539,14 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
     }
 }
 
-template <int NP, bool LAB, int R, int LB, int W, bool INS>
+template <int NP, bool LAB, int R, int LB, int W, bool INS, int PK>
 // min waves per SIMD 3 (168 VGPRs): every item of Na = 20,000 is resident at W = 1; the
 // cooperative tiles (W >= 2) serve small grids and labour, where a few hundred waves run and
 // latency, not occupancy, bounds them — a budget of 5 (and of 4) made those builds spill
-__global__ __launch_bounds__(64 * W, 3) void bell_tree_kernel(BellArgs A0, int ntile) {
-    bell_tree_item<NP, LAB, R, LB, W, INS>(A0, ntile, (int)blockIdx.x, (int)gridDim.x);
+__global__ __launch_bounds__(64 * W * PK, 3) void bell_tree_kernel(BellArgs A0, int ntile) {
+    const int lw = PK > 1 ? readfirst(threadIdx.x >> 6) : 0;
+    bell_tree_item<NP, LAB, R, LB, W, INS, PK>(A0, ntile, (int)blockIdx.x * PK + lw,
+                                               (int)gridDim.x * PK);
 }
 
 // ------------------------------------------------------------------------------ 4. merge
@@ -1751,26 +1765,37 @@ static void run_screen(const BellArgs& A, hipStream_t st) {
         }
     }
 }
-template <int NP, bool LAB, int R, int W>
+template <int NP, bool LAB, int R, int W, int PK = 1>
 static void tree_geo(const BellArgs& A, hipStream_t st) {
     constexpr int LB = LAB ? 5 : 1;
     const int ntile = cdiv(A.Na, bell_tile_width(A, R));
-    const int grid = std::max(A.C, 1) * A.N * ntile;
+    const int grid = cdiv(std::max(A.C, 1) * A.N * ntile, PK);
     if (A.trace || A.hitcount)
-        launch_dispatch_timed(bell_tree_kernel<NP, LAB, R, LB, W, true>, dim3(grid), dim3(64 * W),
-                              0, st, A, ntile);
+        launch_dispatch_timed(bell_tree_kernel<NP, LAB, R, LB, W, true, PK>, dim3(grid),
+                              dim3(64 * W * PK), 0, st, A, ntile);
     else
-        launch_dispatch_timed(bell_tree_kernel<NP, LAB, R, LB, W, false>, dim3(grid),
-                              dim3(64 * W), 0, st, A, ntile);
+        launch_dispatch_timed(bell_tree_kernel<NP, LAB, R, LB, W, false, PK>, dim3(grid),
+                              dim3(64 * W * PK), 0, st, A, ntile);
 }
-// variant bit 0: 2 states per lane (A1 only); bits 1-2: waves per tile 1 (default), 2, 4, 8
+// variant bit 0: 2 states per lane (A1 only); bits 1-2: waves per tile 1 (default), 2, 4, 8;
+// one-wave tiles with a dispatch permutation: bell_tree_pack waves per workgroup
 template <int NP, bool LAB, int R>
 static void tree_w(const BellArgs& A, hipStream_t st) {
     switch ((A.variant >> 1) & 3) {
         case 1: tree_geo<NP, LAB, R, 2>(A, st); break;
         case 2: tree_geo<NP, LAB, R, 4>(A, st); break;
         case 3: tree_geo<NP, LAB, R, 8>(A, st); break;
-        default: tree_geo<NP, LAB, R, 1>(A, st); break;
+        default:
+            if constexpr (!LAB && R == 1) {
+                switch (A.perm ? bell_tree_pack(A) : 1) {
+                    case 2: tree_geo<NP, LAB, R, 1, 2>(A, st); return;
+                    case 4: tree_geo<NP, LAB, R, 1, 4>(A, st); return;
+                    case 8: tree_geo<NP, LAB, R, 1, 8>(A, st); return;
+                    default: break;
+                }
+            }
+            tree_geo<NP, LAB, R, 1>(A, st);
+            break;
     }
 }
 template <int NP, bool LAB>

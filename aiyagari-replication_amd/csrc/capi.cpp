@@ -156,10 +156,12 @@ static int bell_args(aiy_ws* ws, const BellCall& c, BellArgs& A, hipStream_t st)
     // Round 4, A1 at Na > 4096: bit 11 (each XCD's cheapest 2 x 128 tiles dispatched last, the
     // rest row-major) over 16 alone, three alternating runs on one box: step 39.3 -> 36.3 us,
     // solve to tol 8.74 -> 8.63 ms; heaviest-first (bit 6) 37.6 us / 8.75 ms; narrower tiles
-    // (bit 13) slower, 40.6 / 39.3 us (profiles/r04_g7_order_ab.txt)
-    const int var = ws->variant >= 0
-                        ? ws->variant
-                        : (ws->Na <= 4096 ? (c.labor ? 4 | 4096 : 2) : (c.labor ? 16 : 16 | 2048));
+    // (bit 13) slower, 40.6 / 39.3 us (profiles/r04_g7_order_ab.txt).  Two one-wave tiles per
+    // workgroup (bits 16-17 = 1) on top: 36.5 -> 36.0 us, solve 8.68 -> 8.59 ms; four: 36.3 us,
+    // eight: 47 us (profiles/r04_g9_pack_ab.txt)
+    const int var = ws->variant >= 0 ? ws->variant
+                    : ws->Na <= 4096 ? (c.labor ? 4 | 4096 : 2)
+                    : (c.labor ? 16 : 16 | 2048 | 1 << 16);
     A.variant = var;
     A.ev_mfma = bell_ev_mfma(A.N, ws->variant);
     // (variant bit 13) one-wave tiles of tw < 64 states, tw = ceil(N·Na / (3 waves × 1,024
@@ -242,7 +244,7 @@ static int bell_args(aiy_ws* ws, const BellCall& c, BellArgs& A, hipStream_t st)
     }
     A.perm = nullptr;
     if (tree_perm_eligible(A)) {
-        const int key = A.tw * 4096 + (A.variant & (64 | 2048));
+        const int key = A.tw * (1 << 18) + (A.variant & (64 | 2048 | (3 << 16)));
         if (!ws->perm_ok || ws->perm_key != key) {
             AIY_TRY(ws_tree_perm(ws, A, st));
             ws->perm_key = key;
@@ -266,14 +268,17 @@ constexpr int kSimdsPerXcd = 128;  // MI355X: 32 CUs x 4 SIMDs per XCD
 int ws_tree_perm(aiy_ws* ws, const BellArgs& A, hipStream_t st) {
     const int N = A.N, Na = A.Na, TW = bell_tile_width(A, 1), ntile = (Na + TW - 1) / TW;
     const int G = N * ntile;
+    // PK one-wave tiles per workgroup (bell_tree_pack); workgroup b runs on XCD b mod 8, its
+    // waves take slots b·PK .. b·PK + PK - 1; the last workgroup's unused slots hold -1
+    const int PK = bell_tree_pack(A), nwg = (G + PK - 1) / PK, slots = nwg * PK;
     std::vector<int> kf((size_t)N * Na);
     AIY_HIP(hipMemcpyAsync(kf.data(), A.kf, kf.size() * sizeof(int), hipMemcpyDeviceToHost, st));
     AIY_HIP(hipStreamSynchronize(st));
-    std::vector<int> perm(G);
-    const int q = G / 8, r = G % 8;
+    std::vector<int> perm(slots, -1);
+    int start = 0;
     for (int x = 0; x < 8; ++x) {
-        const int start = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
-        const int size = x < r ? q + 1 : q;
+        int size = (nwg / 8 + (x < nwg % 8 ? 1 : 0)) * PK;
+        if (x == (nwg - 1) % 8) size -= slots - G;
         std::vector<int> items(size);
         for (int u = 0; u < size; ++u) items[u] = start + u;
         auto cost = [&](int it) {
@@ -296,15 +301,17 @@ int ws_tree_perm(aiy_ws* ws, const BellArgs& A, hipStream_t st) {
             for (int u = tail - 1; u >= 0; --u) out.push_back(by[u]);
             items.swap(out);
         }
-        for (int u = 0; u < size; ++u) perm[(size_t)u * 8 + x] = items[u];  // block b = 8u + x
+        for (int u = 0; u < size; ++u)  // the XCD's (u / PK)-th workgroup b = 8(u / PK) + x
+            perm[(size_t)(8 * (u / PK) + x) * PK + u % PK] = items[u];
+        start += size;
     }
-    if (!ws->tree_perm || ws->perm_cap < G) {
+    if (!ws->tree_perm || ws->perm_cap < slots) {
         if (ws->tree_perm) (void)hipFree(ws->tree_perm);
         ws->tree_perm = nullptr;
-        AIY_HIP(hipMalloc((void**)&ws->tree_perm, (size_t)G * sizeof(int)));
-        ws->perm_cap = G;
+        AIY_HIP(hipMalloc((void**)&ws->tree_perm, (size_t)slots * sizeof(int)));
+        ws->perm_cap = slots;
     }
-    AIY_HIP(hipMemcpyAsync(ws->tree_perm, perm.data(), (size_t)G * sizeof(int),
+    AIY_HIP(hipMemcpyAsync(ws->tree_perm, perm.data(), (size_t)slots * sizeof(int),
                            hipMemcpyHostToDevice, st));
     AIY_HIP(hipStreamSynchronize(st));
     ws->perm_ok = true;

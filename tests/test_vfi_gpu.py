@@ -147,7 +147,8 @@ def test_full_size_bitwise_vs_oracle(pkg, gpu):
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 6, 8, 12, 16, 32, 96, 512, 4098, 4100, 4102, 80, 2064,
-                                     8192, 8208, 8272, 10256])
+                                     8192, 8208, 8272, 10256, 2064 | 2 << 16,
+                                     10240 | 1 << 16, 64 | 3 << 16])
 def test_screen_stress_noisy_value(pkg, gpu, variant):
     """Rough value functions put many candidates within rounding distance of the running best
     (near-ties everywhere, multi-modal objectives): the fp32 pre-screen, the fp64 screen and
@@ -169,12 +170,15 @@ def test_screen_stress_noisy_value(pkg, gpu, variant):
             assert np.array_equal(pks, pko) and np.array_equal(pcs, pco)
 
 
-@pytest.mark.parametrize("variant", [16, 80, 2064, 8208, 8272, 10256])
+@pytest.mark.parametrize("variant", [16, 80, 2064, 8208, 8272, 10256, 2064 | 1 << 16,
+                                     2064 | 2 << 16, 2064 | 3 << 16, 80 | 2 << 16,
+                                     10256 | 2 << 16])
 def test_full_size_dispatch_orders_and_tile_widths(pkg, gpu, variant):
     """Na = 20,000 (configs[1]): the tree's dispatch orders (bit 6: each XCD's range heaviest
-    first; bit 11: its cheapest tiles last) and the narrow one-wave tiles (bit 13: 46 states per
-    tile, three tiles per SIMD) change only the work split — a hinted warm sweep is bit-exact
-    against the C oracle for each."""
+    first; bit 11: its cheapest tiles last), the narrow one-wave tiles (bit 13: 46 states per
+    tile, three tiles per SIMD) and packed workgroups (bits 16-17: 2, 4 or 8 one-wave tiles per
+    workgroup) change only the work split — a hinted warm sweep is bit-exact against the C
+    oracle for each."""
     import torch
     cal = no.calib_aiyagari(Na=20000, shocks="rouwenhorst")
     a, s, P = cal["a_grid"], cal["s"], cal["P"]
@@ -189,3 +193,23 @@ def test_full_size_dispatch_orders_and_tile_widths(pkg, gpu, variant):
                                       hint=hint, variant=variant)
     assert np.array_equal(vs, vo) and np.array_equal(is_, io)
     assert np.array_equal(pks, pko) and np.array_equal(pcs, pco)
+
+
+@pytest.mark.parametrize("Na,variant", [(1100, 2048 | 2 << 16), (1100, 64 | 3 << 16),
+                                        (333, 2048 | 1 << 16), (4100, 8192 | 2048 | 2 << 16)])
+def test_packed_workgroups_ragged(pkg, gpu, Na, variant):
+    """Packed workgroups whose last one is partly empty (7 rows x 18 tiles = 126 one-wave
+    items in 4-wave workgroups: 2 unused slots; 7 x 6 = 42 in 2-wave ones at Na = 333; the
+    narrow-tile count at Na = 4,100): the unused slots exit, every state is written once —
+    a cold sweep and a hinted one, bit-exact against the C oracle."""
+    import torch
+    cal = no.calib_aiyagari(Na=Na, shocks="rouwenhorst")
+    a, s, P = cal["a_grid"], cal["s"], cal["P"]
+    w = no.wage(0.04, 0.36, 0.08)
+    V = corc.vfi_solve(np.zeros((7, Na)), a, s, P, 0.04, w, 0.96, 5.0, 1e-3, 1000)["v_new"]
+    vo, io, pko, pco = corc.vfi_sweep(V, a, s, P, 0.04, w, 0.96, 5.0)
+    for hint in (None, np.clip(io - 2, 0, Na - 1)):
+        vs, is_, pks, pcs = _device_sweep(pkg, torch, V, a, s, P, 0.04, w, 0.96, 5.0, mode=1,
+                                          hint=hint, variant=variant)
+        assert np.array_equal(vs, vo) and np.array_equal(is_, io)
+        assert np.array_equal(pks, pko) and np.array_equal(pcs, pco)
