@@ -190,7 +190,9 @@ __device__ __forceinline__ BellArgs bell_cand(const BellArgs& A, int c) {
 // formed first, as the reference's (beta * P) * v_old associates), B = V[m][k] (lane l: m =
 // l >> 4, column l & 15), C/D in the f64 layout (column l & 15, row (l >> 4) + 4·reg).  Four
 // waves per block cover 64 consecutive k; blockIdx.y = 16-row tile, blockIdx.z = candidate
-// (config 4 batches; stopped candidates are skipped).  Out-of-range rows/columns/m are zero.
+// (config 4 batches; candidates stopped at an earlier sweep are skipped — one that stops at
+// this sweep, decided by the table kernel after this pass, gets one unused pass, and its EV
+// buffer is scratch from then on).  Out-of-range rows/columns/m are zero.
 typedef double aiy_v4d __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void bell_ev_mfma_kernel(int N, int Na,
                                                            const double* __restrict__ P,
