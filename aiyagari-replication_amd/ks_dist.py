@@ -308,6 +308,203 @@ def column_table(owners_V, owners_dV, owner, nk):
     return torch.tensor(addr, dtype=torch.int64, device=dev)
 
 
+class DirectPeers:
+    """The direct schedule (ks_vfi_solve_sharded depth = 0) under one process per
+    GPU.  Every rank keeps its own columns of value and slopes in two parity buffers; the
+    other ranks map them through IPC handles (exchanged once), and the rank's column tables
+    point each forecast column at its owner's buffer, so a Howard sweep or an improvement reads
+    neighbours' columns in place over xGMI — no halo copies, no ghost sweeps.  The hand-off is
+    a counter per rank in a host page every rank maps (`aiy_flag_set` after each sweep,
+    `aiy_flags_wait` on the neighbours' counters before the next one): stream-ordered, the
+    host never blocks.  Neighbours = the owners of the columns this rank reads and the ranks
+    that read its columns (the latter so a buffer is not overwritten while it is read)."""
+
+    # the host page: counter slot q at byte 128·q (q < 64), rank q's timeout word at 8192 + 128·q
+    PAGE = 16384
+
+    def __init__(self, shard, nK, rank, world, V, bounds=None, timeout_s=30.0):
+        import torch
+        import torch.distributed as dist
+        from multiprocessing import shared_memory
+        if world > 32:
+            raise ValueError("DirectPeers: at most 32 ranks")
+        self.shard, self.nK, self.rank, self.world = shard, nK, rank, world
+        self.nk = V.shape[-1]
+        self.timeout_s = float(timeout_s)
+        # NaN outside the own columns: a read of a local copy instead of the owner's would show
+        self.V = [torch.full_like(V, math.nan) for _ in range(2)]
+        self.dV = [torch.full_like(V, math.nan) for _ in range(2)]
+        self.own = owned_columns(nK, rank, world, bounds)
+        plan = halo_plan(shard.kp_idx, nK, world, bounds)
+        self.nbr = sorted({p for p in range(world) if p != rank and (plan[rank][p] or plan[p][rank])})
+        self.mask = sum(1 << p for p in self.nbr)
+        # IPC handles of the four buffers, every rank's
+        mine = []
+        for t in self.V + self.dV:
+            h = (C.c_char * 64)()
+            off = C.c_int64()
+            check(lib().aiy_ipc_get_handle(ptr(t), h, C.byref(off)))
+            mine.append((bytes(h), off.value))
+        allh = [None] * world
+        dist.all_gather_object(allh, mine)
+        self._opened = []
+        addr = []   # addr[q] = (V0, V1, dV0, dV1) device addresses of rank q's buffers
+        for q in range(world):
+            if q == rank:
+                addr.append(tuple(t.data_ptr() for t in self.V + self.dV))
+                continue
+            row = []
+            for hb, off in allh[q]:
+                p_ = vp()
+                check(lib().aiy_ipc_open(C.create_string_buffer(hb, 64), i64(off), C.byref(p_)))
+                self._opened.append((p_.value, off))
+                row.append(p_.value)
+            addr.append(tuple(row))
+        owner = [0] * (4 * nK)
+        for q in range(world):
+            for c in owned_columns(nK, q, world, bounds):
+                owner[c] = q
+        cb = 8 * self.nk
+        self.tab = [torch.tensor([addr[owner[c]][b] + cb * c for c in range(4 * nK)] +
+                                 [addr[owner[c]][2 + b] + cb * c for c in range(4 * nK)],
+                                 dtype=torch.int64, device=V.device) for b in (0, 1)]
+        # the counter page: rank 0 creates it, every rank maps and registers it
+        name = [None]
+        if rank == 0:
+            self._shm = shared_memory.SharedMemory(create=True, size=self.PAGE)
+            self._shm.buf[:self.PAGE] = bytes(self.PAGE)
+            name[0] = self._shm.name
+        dist.broadcast_object_list(name, src=0)
+        if rank != 0:
+            self._shm = shared_memory.SharedMemory(name=name[0])
+            try:  # the creator unlinks it; keep this process's tracker from doing so too
+                from multiprocessing import resource_tracker
+                resource_tracker.unregister(self._shm._name, "shared_memory")
+            except Exception:
+                pass
+        self._host = C.c_char.from_buffer(self._shm.buf)
+        self._hostp = C.addressof(self._host)
+        dp = vp()
+        check(lib().aiy_host_register(C.c_void_p(self._hostp), i64(self.PAGE), C.byref(dp)))
+        self._flags = dp.value
+        self._err = self._flags + 8192 + 128 * rank     # this rank's error word (host-mapped)
+        self._err_host = self._hostp + 8192 + 128 * rank
+        self.n = 0     # sweeps this rank has published (identical schedule on every rank)
+        dist.barrier()
+
+    def error(self):
+        return C.c_uint64.from_address(self._err_host).value
+
+    def publish(self):
+        self.n += 1
+        check(lib().aiy_flag_set(C.c_void_p(self._flags), C.c_int32(self.rank),
+                                 C.c_uint64(self.n), stream_handle(None)))
+
+    def wait(self):
+        check(lib().aiy_flags_wait(C.c_void_p(self._flags), C.c_uint64(self.mask),
+                                   C.c_uint64(self.n), C.c_double(self.timeout_s),
+                                   C.c_void_p(self._err), stream_handle(None)))
+
+    def own_runs(self):
+        return _runs(self.own)
+
+    # the schedule (every rank calls the same sequence)
+    def start(self, V):
+        """Own columns of V into parity 0, their slopes, and publish "sweep 0"."""
+        import torch
+        import torch.distributed as dist
+        torch.cuda.synchronize()
+        dist.barrier()                 # peers finished with every buffer of a past schedule
+        nk = self.nk
+        for a, b in self.own_runs():
+            self.V[0].view(-1, nk)[a:b].copy_(V.view(-1, nk)[a:b])
+        self.cur = 0
+        self.shard.slopes_own(self.V[0], self.dV[0])
+        self.publish()
+
+    def improve(self, kopt):
+        """Policy improvement (:148-168) of the own nodes, forecast columns read in place."""
+        self.wait()
+        self.shard.set_columns(self.tab[self.cur])
+        self.shard.improve_direct(kopt)
+
+    def sweeps(self, kopt, n):
+        """n Jacobi Howard sweeps (:172-192): per sweep the hand-off wait, one fused launch and
+        the publish, all enqueued by one C call (ks_dev_direct_sweeps)."""
+        if n <= 0:
+            return
+        check(lib().ks_dev_direct_sweeps(
+            self.shard._h, ptr(self.tab[0]), ptr(self.tab[1]), ptr(self.V[0]), ptr(self.V[1]),
+            ptr(self.dV[0]), ptr(self.dV[1]), ptr(kopt), C.c_int32(self.cur), i64(n),
+            C.c_void_p(self._flags), C.c_int32(self.rank), C.c_uint64(self.mask),
+            C.c_uint64(self.n), C.c_double(self.timeout_s), C.c_void_p(self._err),
+            stream_handle(None)))
+        self.n += n
+        self.cur ^= n & 1
+
+    def current(self):
+        return self.V[self.cur]
+
+    def check(self):
+        """Raise if a wait timed out (after a host synchronisation)."""
+        e = self.error()
+        if e:
+            raise RuntimeError(f"DirectPeers: rank {self.rank} timed out waiting for rank "
+                               f"{e - 1}'s sweep")
+
+    def close(self):
+        import torch
+        import torch.distributed as dist
+        if getattr(self, "_shm", None) is None:
+            return
+        torch.cuda.synchronize()
+        dist.barrier()     # nobody reads a peer buffer or the page any more
+        for p_, off in self._opened:
+            lib().aiy_ipc_close(C.c_void_p(p_), i64(off))
+        self._opened = []
+        lib().aiy_host_unregister(C.c_void_p(self._hostp))
+        del self._host
+        self._shm.close()
+        dist.barrier()
+        if self.rank == 0:
+            self._shm.unlink()
+        self._shm = None
+
+
+def _solve_direct(V, k_opt, shard, nK, howard_steps, tol, max_vfi, rank, world, bounds,
+                  peers=None):
+    """ks_vfi_solve_dist's loop on the direct schedule (DirectPeers); V, k_opt: full arrays on
+    every rank (in), own columns current on return (the caller all-gathers)."""
+    import torch
+    import torch.distributed as dist
+    dp = peers if peers is not None else DirectPeers(shard, nK, rank, world, V, bounds)
+    try:
+        nk = dp.nk
+        runs = dp.own_runs()
+        flat = lambda t: t.view(-1, nk)
+        Vold = torch.empty_like(V)
+        dp.start(V)
+        rel, it = math.nan, 0
+        for it in range(1, max_vfi + 1):
+            for a, b in runs:                  # value_old = value (:145), own columns
+                flat(Vold)[a:b].copy_(flat(dp.current())[a:b])
+            if (it - 1) % 5 == 0:              # policy improvement (:148-168)
+                dp.improve(k_opt)
+            dp.sweeps(k_opt, howard_steps)     # Jacobi Howard sweeps (:172-192)
+            rel = shard.reldiff(dp.current(), Vold)   # :195 (host sync)
+            dp.check()
+            rel = _allreduce_max(rel, V.device)
+            if rel < tol:
+                break
+        shard.set_columns(None)
+        for a, b in runs:
+            flat(V)[a:b].copy_(flat(dp.current())[a:b])
+        return it, rel
+    finally:
+        if peers is None:
+            dp.close()
+
+
 def _exchange(V, rank, world, nK, bounds=None):
     """All-gather every rank's owned columns of V (rows of the (4·nK, k) view) into every
     rank's V, in place."""
@@ -469,12 +666,15 @@ class HowardSweeps:
 
 
 def ks_vfi_solve_dist(value, k_opt, shard, nK, howard_steps=50, tol=1e-6, max_vfi=10000,
-                      rank=0, world=1, exchange="halo", poison=False, depth=1, bounds=None):
+                      rank=0, world=1, exchange="halo", poison=False, depth=1, bounds=None,
+                      peers=None):
     """Krusell_Smith_VFI.m:141-204 for the current B.  value, k_opt: (4, K, k) tensors on this
     rank's device, full arrays on every rank (in/out).  `shard` owns [K0, K1) of [s0, s1)
     (HipShard, or any object with the same improve / howard / reldiff / ghost / hints methods
     and a kp_idx table).  exchange: "halo" (point-to-point, only the columns read; `depth`
-    sweeps per exchange, HowardSweeps) or "allgather".  bounds: the K partition the shards were
+    sweeps per exchange, HowardSweeps), "allgather", or "direct" (forecast columns read in the
+    owners' buffers through IPC mappings, DirectPeers; `peers`: a DirectPeers kept across
+    solves, else one is made and closed per call).  bounds: the K partition the shards were
     made with (`shard_slices(..., bounds)`; None = even ranges).  poison (tests): NaN every column this
     rank neither owns nor reads, proving the exchanges are sufficient.
     Returns (iters, rel_diff)."""
@@ -484,6 +684,15 @@ def ks_vfi_solve_dist(value, k_opt, shard, nK, howard_steps=50, tol=1e-6, max_vf
     nk = V.shape[-1]
     if world > 1:
         dist.barrier()   # first collective on every rank before any point-to-point
+    if exchange == "direct":
+        if world == 1:
+            exchange = "halo"
+        else:
+            it, rel = _solve_direct(V, k_opt, shard, nK, howard_steps, tol, max_vfi, rank, world,
+                                    bounds, peers)
+            _exchange(k_opt, rank, world, nK, bounds)   # every rank leaves with all of both
+            _exchange(V, rank, world, nK, bounds)
+            return it, rel
     hs = HowardSweeps(shard, nK, rank, world, V, depth=depth, exchange=exchange, bounds=bounds)
     if poison and world > 1 and exchange == "halo":
         keep = hs.read_columns()

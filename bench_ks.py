@@ -111,6 +111,93 @@ def ks_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, exchange="halo", r
                               f"{nk} values)")}
 
 
+def ks_direct_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, reps=3, check_sweeps=6):
+    """The direct schedule under one process per GPU (ks_dist.DirectPeers: forecast columns
+    read in the owners' buffers through IPC mappings, a stream-ordered counter hand-off per
+    sweep, no copies, no ghost sweeps): one VFI iteration (improvement + `howard`
+    sweeps) at the scaling size, max over ranks, median of `reps`.  Before timing, the same
+    short run (improvement + `check_sweeps` sweeps from the same start) through the halo
+    schedule, which the tests pin bit-exact to the single-device solve, must give identical
+    own columns on every rank (`bit_exact_vs_halo`).  Every rank must call it."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    kd = pkg.ks_dist
+    kg, Kg, P, V0 = pkg.calibration.krusell_smith(k_size=nk, K_size=nK)
+    B = np.array([0.1, 0.97, 0.08, 0.975])
+    K0, K1, s0, s1 = kd.shard_slices(nK, rank, world)
+    sh = kd.HipShard(kg, Kg, B, P, pkg.ks_params(), K0, K1, s0, s1)
+    Vs = torch.as_tensor(np.ascontiguousarray(V0.transpose(2, 1, 0)), device=dev)
+
+    def sync():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    # the exactness check: halo schedule (depth 1) vs direct on the same start
+    Vh, Vh2, koh = Vs.clone(), Vs.clone(), torch.ones_like(Vs)
+    hs = kd.HowardSweeps(sh, nK, rank, world, Vh, depth=1)
+    hs.improve(Vh, koh)
+    Vh, Vh2 = hs.run(Vh, Vh2, koh, check_sweeps)
+    hs.close()
+    dp = kd.DirectPeers(sh, nK, rank, world, Vs)
+    kod = torch.ones_like(Vs)
+    dp.start(Vs)
+    dp.improve(kod)
+    dp.sweeps(kod, check_sweeps)
+    sync()
+    dp.check()
+    flat = lambda t: t.view(-1, nk)
+    same = all(torch.equal(flat(dp.current())[a:b], flat(Vh)[a:b]) and
+               torch.equal(flat(kod)[a:b], flat(koh)[a:b]) for a, b in dp.own_runs())
+    ok = torch.tensor([1.0 if same else 0.0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    del Vh, Vh2, koh
+    # timing: improvement + howard sweeps, as ks_leg
+    dp.sweeps(kod, 2)
+    samples = []
+    for _ in range(reps):
+        sync()
+        t0 = time.perf_counter()
+        dp.improve(kod)
+        sync()
+        t1 = time.perf_counter()
+        dp.sweeps(kod, howard)
+        sync()
+        t2 = time.perf_counter()
+        samples.append((t1 - t0, t2 - t1))
+    dp.check()
+    ti = sorted(x[0] for x in samples)[reps // 2]
+    th = sorted(x[1] for x in samples)[reps // 2]
+    if world > 1:
+        t = torch.tensor([ti, th], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ti, th = float(t[0]), float(t[1])
+    nbr = len(dp.nbr)
+    sh.set_columns(None)
+    dp.close()
+    sh.close()
+    nodes = nk * nK * 4
+    bpn = 52
+    gbs = nodes * bpn / (th / howard) / 1e9 / world
+    return {"metric": "Krusell-Smith bellman_value evals/sec (Howard sweeps, fp64)",
+            "value": nodes * howard / th, "unit": "evals/s", "n_gpus": world,
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": 8000.0, "unit": "GB/s",
+                         "frac": gbs / 8000.0,
+                         "basis": f"{bpn} B algorithmic per node per Howard sweep x "
+                                  f"{nodes // world} nodes per GPU / sweep time"},
+            "scaling": "strong", "vfi_iteration_ms": (ti + th) * 1e3,
+            "howard_ms_per_sweep": th / howard * 1e3, "improve_ms": ti * 1e3,
+            "bit_exact_vs_halo": bool(ok[0] > 0.5),
+            "workload": f"Krusell_Smith_VFI k={nk} K={nK} S=4 ({nodes} nodes), one VFI iteration "
+                        f"= improvement + {howard} Howard sweeps, median of {reps}",
+            "parallelism": f"(K, Z) shards over {world} ranks (rank 0: K [{K0}, {K1}), s [{s0}, "
+                           f"{s1})), direct schedule: forecast columns read in the owners' "
+                           f"buffers (IPC), counter hand-off with {nbr} neighbour(s) per sweep"}
+
+
 def _ks_pmc():
     """Counter summary of the kernel this leg times — ks_howard_slopes_kernel, one launch per
     Howard sweep at k = 32,768, K = 64 (rocprofv3 --pmc passes over tools/pmc_workloads_r04.py,

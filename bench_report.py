@@ -83,7 +83,8 @@ def leg_summary(leg):
         s["cpu_cores"] = cores
     for k in ("wall_s_gpu", "wall_s_cpu", "identical_trace", "r", "r_gpu", "iters", "wall_ms",
               "ms_per_sweep", "us_per_step", "us_per_push", "howard_ms_per_sweep",
-              "vfi_iteration_ms", "r_equals_reference_trace", "speedup_vs_sequential_rates"):
+              "vfi_iteration_ms", "r_equals_reference_trace", "speedup_vs_sequential_rates",
+              "bit_exact_vs_halo"):
         if k in leg and (_num(leg[k]) is not None or isinstance(leg[k], bool)):
             s[k] = leg[k]
     return s

@@ -395,6 +395,33 @@ int ks_dev_reldiff(ks_dev* h, const double* V, const double* Vold, void* out, vo
 int ks_dev_set_columns(ks_dev* h, const void* const* table);
 int ks_dev_slopes_own(ks_dev* h, const double* V, double* dV, void* stream);
 int ks_dev_improve_direct(ks_dev* h, double* kopt, void* stream);
+/* The direct schedule under one process per GPU (ks_dist.DirectPeers; no reference
+ * counterpart — the reference is one MATLAB process): the column buffers are shared through
+ * IPC handles and the sweep hand-off through counters in a host page every rank maps.
+ * aiy_ipc_get_handle: the IPC handle (AIY_IPC_HANDLE_BYTES) of the allocation holding dptr and
+ * dptr's offset in it; aiy_ipc_open maps it in this process (peer access enabled on demand;
+ * *dptr = base + offset) and aiy_ipc_close unmaps.  aiy_host_register pins and maps a host
+ * range for the device (*dptr: its device address).  Counter slot q is the uint64 at
+ * flags + 128·q (q < 64).  aiy_flags_wait enqueues one wave that holds the stream until every
+ * slot q in `mask` is >= value; after timeout_s seconds without that it stores 1 + q in *err
+ * (host-mapped) and lets the stream go (the caller checks err; results are then invalid).
+ * aiy_flag_set enqueues a system-scope release store value -> slot. */
+#define AIY_IPC_HANDLE_BYTES 64
+int aiy_ipc_get_handle(const void* dptr, void* handle, int64_t* offset);
+int aiy_ipc_open(const void* handle, int64_t offset, void** dptr);
+int aiy_ipc_close(void* dptr, int64_t offset);
+int aiy_host_register(void* p, int64_t bytes, void** dptr);
+int aiy_host_unregister(void* p);
+int aiy_flags_wait(const void* flags, uint64_t mask, uint64_t value, double timeout_s, void* err,
+                   void* stream);
+int aiy_flag_set(void* flags, int32_t slot, uint64_t value, void* stream);
+/* nsweeps fused Howard sweeps of the direct schedule in one call: sweep i reads parity
+ * p = parity ^ (i & 1) (V/dV p, column table tab_p) and writes parity p ^ 1, once the slots in
+ * `mask` hold >= n0 + i; then slot `slot` := n0 + i + 1. */
+int ks_dev_direct_sweeps(ks_dev* h, const void* const* tab0, const void* const* tab1,
+                         double* V0, double* V1, double* dV0, double* dV1, double* kopt,
+                         int32_t parity, int64_t nsweeps, void* flags, int32_t slot, uint64_t mask,
+                         uint64_t n0, double timeout_s, void* err, void* stream);
 /* Ghost shards (ks_dist.py exchanges halos every m Howard sweeps and sweeps a widening
  * rectangle of other ranks' columns redundantly in between — same kernels, so still bit-exact):
  * h uses owner's segment-hint array (same grid and device; destroying owner while a handle

@@ -69,6 +69,18 @@ def _worker(rank, world, port, outdir, nK, exchange="halo", depth=1, B_alm=B_ALM
                       HSA_ENABLE_IPC_MODE_LEGACY="0")
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    if exchange == "timeout":
+        _timeout_probe(rank, world, outdir, nK)
+        dist.destroy_process_group()
+        return
+    if exchange == "bench":
+        sys.path.insert(0, str(ROOT))
+        import bench_ks
+        leg = bench_ks.ks_direct_leg(_pkg(), world, rank, "cuda:0", nk=300, nK=nK, howard=7,
+                                     reps=1, check_sweeps=5)
+        Path(outdir, f"leg{rank}.json").write_text(json.dumps(leg))
+        dist.destroy_process_group()
+        return
     V, ko, it, rel = _run(rank, world, nK, exchange=exchange, depth=depth, B_alm=B_alm)
     np.save(Path(outdir, f"V{rank}.npy"), V)
     np.save(Path(outdir, f"k{rank}.npy"), ko)
@@ -134,3 +146,65 @@ def test_shared_hints_lifetime(pkg, gpu):
     g.close()
     assert lib.ks_dev_destroy(sh._h) == 0
     sh._h = None
+
+
+@pytest.mark.parametrize("world,nK,B", [(2, 4, "alm"), (2, 6, "mixed"), (3, 12, "mixed"),
+                                        (8, 4, "alm")])
+def test_direct_ipc_ranks_on_one_card(pkg, gpu, tmp_path, world, nK, B):
+    """The direct schedule under one process per rank (ks_dist.DirectPeers): each rank maps
+    the others' parity buffers through IPC handles and reads its forecast columns there, the
+    sweep hand-off runs through counters in a shared host page (aiy_flag_set /
+    aiy_flags_wait, stream-ordered).  Ranks share the card (gloo for the host collectives);
+    every non-own column of a rank's buffers is NaN, so a local read would show.  Equal to the
+    single-device solve bit for bit — 2 and 3 K-range ranks, and the reference K = 4 grid on 8
+    (K, Z) slices."""
+    import torch.multiprocessing as mp
+    Balm = B_ALM if B == "alm" else B_MIXED
+    port = 31100 + (os.getpid() % 1000) + 7 * world + nK
+    mp.spawn(_worker, args=(world, port, str(tmp_path), nK, "direct", 1, Balm), nprocs=world,
+             join=True)
+    Vr, kr, itr, relr = _reference(nK, B_alm=Balm)
+    for rank in range(world):
+        assert np.array_equal(np.load(Path(tmp_path, f"V{rank}.npy")), Vr)
+        assert np.array_equal(np.load(Path(tmp_path, f"k{rank}.npy")), kr)
+        assert json.loads(Path(tmp_path, f"m{rank}.json").read_text())["it"] == itr
+
+
+def _timeout_probe(rank, world, outdir, nK):
+    import torch
+    pkg = _pkg()
+    kg, Kg, P, V0 = _setup(nK)
+    K0, K1, s0, s1 = pkg.ks_dist.shard_slices(nK, rank, world)
+    sh = pkg.ks_dist.HipShard(kg, Kg, B_MIXED, P, pkg.ks_params(), K0, K1, s0, s1)
+    V = torch.as_tensor(np.ascontiguousarray(V0.transpose(2, 1, 0)), device="cuda:0")
+    dp = pkg.ks_dist.DirectPeers(sh, nK, rank, world, V, timeout_s=1.0)
+    err = 0
+    if rank == 0:            # waits for a sweep rank 1 never publishes
+        dp.n = 3
+        dp.wait()
+        torch.cuda.synchronize()
+        err = dp.error()
+    dp.close()
+    sh.close()
+    Path(outdir, f"err{rank}.json").write_text(json.dumps(err))
+
+
+def test_direct_ipc_wait_times_out(pkg, gpu, tmp_path):
+    """A neighbour that never publishes: the waiting wave gives up after timeout_s, stores
+    1 + the neighbour's rank in the rank's timeout word and releases the stream (no hang)."""
+    import torch.multiprocessing as mp
+    port = 31300 + (os.getpid() % 1000)
+    mp.spawn(_worker, args=(2, port, str(tmp_path), 6, "timeout"), nprocs=2, join=True)
+    assert json.loads(Path(tmp_path, "err0.json").read_text()) == 2
+    assert json.loads(Path(tmp_path, "err1.json").read_text()) == 0
+
+
+def test_bench_direct_leg_two_ranks(pkg, gpu, tmp_path):
+    """bench_ks.ks_direct_leg (the N > 1 bench's `ks_direct` leg) on two ranks sharing the
+    card: its built-in check (direct vs halo schedule, own columns bit for bit) holds."""
+    import torch.multiprocessing as mp
+    port = 31500 + (os.getpid() % 1000)
+    mp.spawn(_worker, args=(2, port, str(tmp_path), 8, "bench"), nprocs=2, join=True)
+    for rank in range(2):
+        leg = json.loads(Path(tmp_path, f"leg{rank}.json").read_text())
+        assert leg["bit_exact_vs_halo"] is True and leg["value"] > 0
