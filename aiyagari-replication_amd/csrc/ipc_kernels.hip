@@ -19,6 +19,8 @@ __global__ __launch_bounds__(64) void flags_wait_kernel(const unsigned long long
                                                         long long timeout_ticks,
                                                         unsigned long long* err) {
     const int q = threadIdx.x;
+    // an earlier wait of this rank already timed out: the schedule is void, do not wait again
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0ull) return;
     const bool mine = (mask >> q) & 1ull;
     const long long t0 = (long long)wall_clock64();
     bool ok = !mine;

@@ -338,28 +338,39 @@ class DirectPeers:
         plan = halo_plan(shard.kp_idx, nK, world, bounds)
         self.nbr = sorted({p for p in range(world) if p != rank and (plan[rank][p] or plan[p][rank])})
         self.mask = sum(1 << p for p in self.nbr)
-        # IPC handles of the four buffers, every rank's
-        mine = []
-        for t in self.V + self.dV:
-            h = (C.c_char * 64)()
-            off = C.c_int64()
-            check(lib().aiy_ipc_get_handle(ptr(t), h, C.byref(off)))
-            mine.append((bytes(h), off.value))
+        # IPC handles of the four buffers, every rank's (a failure on any rank is raised on
+        # every rank, after the same collectives, so no rank is left inside one)
+        mine, fail_msg = [], None
+        try:
+            for t in self.V + self.dV:
+                h = (C.c_char * 64)()
+                off = C.c_int64()
+                check(lib().aiy_ipc_get_handle(ptr(t), h, C.byref(off)))
+                mine.append((bytes(h), off.value))
+        except Exception as e:  # noqa: BLE001 (re-raised collectively below)
+            fail_msg = repr(e)
         allh = [None] * world
-        dist.all_gather_object(allh, mine)
+        dist.all_gather_object(allh, (mine, fail_msg))
         self._opened = []
+        self._shm = None
         addr = []   # addr[q] = (V0, V1, dV0, dV1) device addresses of rank q's buffers
-        for q in range(world):
-            if q == rank:
-                addr.append(tuple(t.data_ptr() for t in self.V + self.dV))
-                continue
-            row = []
-            for hb, off in allh[q]:
-                p_ = vp()
-                check(lib().aiy_ipc_open(C.create_string_buffer(hb, 64), i64(off), C.byref(p_)))
-                self._opened.append((p_.value, off))
-                row.append(p_.value)
-            addr.append(tuple(row))
+        if not any(m for _, m in allh):
+            try:
+                for q in range(world):
+                    if q == rank:
+                        addr.append(tuple(t.data_ptr() for t in self.V + self.dV))
+                        continue
+                    row = []
+                    for hb, off in allh[q][0]:
+                        p_ = vp()
+                        check(lib().aiy_ipc_open(C.create_string_buffer(hb, 64), i64(off),
+                                                 C.byref(p_)))
+                        self._opened.append((p_.value, off))
+                        row.append(p_.value)
+                    addr.append(tuple(row))
+            except Exception as e:  # noqa: BLE001
+                fail_msg = repr(e)
+        _agree_or_raise(fail_msg, V.device, "DirectPeers: IPC mapping", self._unmap)
         owner = [0] * (4 * nK)
         for q in range(world):
             for c in owned_columns(nK, q, world, bounds):
@@ -385,7 +396,13 @@ class DirectPeers:
         self._host = C.c_char.from_buffer(self._shm.buf)
         self._hostp = C.addressof(self._host)
         dp = vp()
-        check(lib().aiy_host_register(C.c_void_p(self._hostp), i64(self.PAGE), C.byref(dp)))
+        fail_msg = None
+        try:
+            check(lib().aiy_host_register(C.c_void_p(self._hostp), i64(self.PAGE), C.byref(dp)))
+        except Exception as e:  # noqa: BLE001
+            fail_msg = repr(e)
+            self._hostp_reg = False
+        _agree_or_raise(fail_msg, V.device, "DirectPeers: host page", self.close)
         self._flags = dp.value
         self._err = self._flags + 8192 + 128 * rank     # this rank's error word (host-mapped)
         self._err_host = self._hostp + 8192 + 128 * rank
@@ -446,11 +463,16 @@ class DirectPeers:
         return self.V[self.cur]
 
     def check(self):
-        """Raise if a wait timed out (after a host synchronisation)."""
+        """Raise on every rank if a wait of any rank timed out (call after a host
+        synchronisation; collective)."""
         e = self.error()
-        if e:
-            raise RuntimeError(f"DirectPeers: rank {self.rank} timed out waiting for rank "
-                               f"{e - 1}'s sweep")
+        msg = f"rank {self.rank} timed out waiting for rank {e - 1}'s sweep" if e else None
+        _agree_or_raise(msg, self.V[0].device, "DirectPeers")
+
+    def _unmap(self):
+        for p_, off in self._opened:
+            lib().aiy_ipc_close(C.c_void_p(p_), i64(off))
+        self._opened = []
 
     def close(self):
         import torch
@@ -459,16 +481,28 @@ class DirectPeers:
             return
         torch.cuda.synchronize()
         dist.barrier()     # nobody reads a peer buffer or the page any more
-        for p_, off in self._opened:
-            lib().aiy_ipc_close(C.c_void_p(p_), i64(off))
-        self._opened = []
-        lib().aiy_host_unregister(C.c_void_p(self._hostp))
+        self._unmap()
+        if getattr(self, "_hostp_reg", True):
+            lib().aiy_host_unregister(C.c_void_p(self._hostp))
         del self._host
         self._shm.close()
         dist.barrier()
         if self.rank == 0:
             self._shm.unlink()
         self._shm = None
+
+
+def _agree_or_raise(msg, device, what, cleanup=None):
+    """Collective: if `msg` is set on any rank, every rank (after `cleanup`) raises."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([1.0 if msg else 0.0], dtype=torch.float64,
+                     device=device if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if float(t[0]) > 0:
+        if cleanup is not None:
+            cleanup()
+        raise RuntimeError(f"{what}: {msg or 'failed on another rank'}")
 
 
 def _solve_direct(V, k_opt, shard, nK, howard_steps, tol, max_vfi, rank, world, bounds,

@@ -306,7 +306,10 @@ def main():
         import bench_ks
         legs["ks_sharded"] = bench_ks.ks_leg(pkg, world, rank, dev, depth=args.ks_depth)
         if world > 1:  # the direct schedule across processes (IPC peer reads), same size
-            legs["ks_direct"] = bench_ks.ks_direct_leg(pkg, world, rank, dev)
+            try:  # (its failures are raised on every rank together: DirectPeers)
+                legs["ks_direct"] = bench_ks.ks_direct_leg(pkg, world, rank, dev)
+            except RuntimeError as e:
+                legs["ks_direct"] = {"error": str(e)[:300]}
         if world == 1 and not args.no_extra:  # compute side of the N = 8 schedules, on this GPU
             legs["ks_sharded"]["direct_model"] = bench_ks.direct_model(pkg, dev)
             legs["ks_sharded"]["ghost_model"] = bench_ks.ghost_model(pkg, dev, depths=(4,))

@@ -346,12 +346,51 @@ def direct_model(pkg, dev, world=8, nk=32768, nK=64, sweeps=24, howard=50):
         e1.record()
         torch.cuda.synchronize()
         swp.append(e0.elapsed_time(e1) / sweeps)
+    # the cross-process hand-off's own cost (ks_dist.DirectPeers): the slowest shard's sweeps
+    # through ks_dev_direct_sweeps, waiting on (and publishing to) a counter slot in a mapped
+    # host page — here its own slot, always satisfied, so the difference to the plain sweeps is
+    # the two extra one-wave launches and the host-memory poll per sweep
+    import ctypes as C
+    import mmap
+    check, lib = pkg._capi.check, pkg._capi.lib
+    q = max(range(world), key=lambda x: swp[x])
+    page = mmap.mmap(-1, 16384)
+    host = C.c_char.from_buffer(page)
+    hp = C.addressof(host)
+    dptr = C.c_void_p()
+    check(lib().aiy_host_register(C.c_void_p(hp), C.c_int64(16384), C.byref(dptr)))
+    C.c_uint64.from_address(hp).value = 1
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    P_ = lambda t: C.c_void_p(t.data_ptr())
+
+    def run_direct(n, n0):
+        check(lib().ks_dev_direct_sweeps(
+            sh[q]._h, P_(tabs[q][0]), P_(tabs[q][1]), P_(Vb[q][0]), P_(Vb[q][1]), P_(dVb[q][0]),
+            P_(dVb[q][1]), P_(ko), C.c_int32(0), C.c_int64(n), dptr, C.c_int32(0),
+            C.c_uint64(1), C.c_uint64(n0), C.c_double(30.0), C.c_void_p(dptr.value + 8192), st))
+    run_direct(2, 1)
+    e0, e1 = ev(), ev()
+    e0.record()
+    run_direct(sweeps, 3)
+    e1.record()
+    torch.cuda.synchronize()
+    hand = e0.elapsed_time(e1) / sweeps
+    err = C.c_uint64.from_address(hp + 8192).value
+    check(lib().aiy_host_unregister(C.c_void_p(hp)))
+    del host
+    page.close()
     for x in sh:
         x.close()
     it_ms = max(imp) + howard * max(swp)
     return {"world": world, "sweeps": sweeps, "improve_ms_by_shard": imp,
             "gpu_ms_per_sweep_by_shard": swp, "gpu_ms_per_sweep_slowest": max(swp),
             "improve_ms_slowest": max(imp), "projected_vfi_iteration_ms": it_ms,
+            "handoff": {"shard": q, "gpu_ms_per_sweep_with_handoff": hand,
+                        "handoff_us_per_sweep": (hand - swp[q]) * 1e3, "timeouts": err,
+                        "projected_vfi_iteration_ms": max(imp) + howard * (max(swp) + hand - swp[q]),
+                        "note": "ks_dev_direct_sweeps on the slowest shard with a self-satisfied "
+                                "counter wait + publish per sweep (the multi-process schedule's "
+                                "launches; the neighbours' skew is not in it)"},
             "note": f"direct schedule (ks_vfi_solve_sharded depth 0) emulated on one GPU: each of "
                     f"{world} shards timed alone, reading the other shards' buffers through its "
                     f"column table; projected iteration = slowest improvement + {howard} x "

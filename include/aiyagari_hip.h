@@ -404,7 +404,8 @@ int ks_dev_improve_direct(ks_dev* h, double* kopt, void* stream);
  * range for the device (*dptr: its device address).  Counter slot q is the uint64 at
  * flags + 128·q (q < 64).  aiy_flags_wait enqueues one wave that holds the stream until every
  * slot q in `mask` is >= value; after timeout_s seconds without that it stores 1 + q in *err
- * (host-mapped) and lets the stream go (the caller checks err; results are then invalid).
+ * (host-mapped) and lets the stream go (the caller checks err; results are then invalid; once
+ * err is set, later waits return at once).
  * aiy_flag_set enqueues a system-scope release store value -> slot. */
 #define AIY_IPC_HANDLE_BYTES 64
 int aiy_ipc_get_handle(const void* dptr, void* handle, int64_t* offset);
