@@ -261,7 +261,7 @@ static int bell_args(aiy_ws* ws, const BellCall& c, BellArgs& A, hipStream_t st)
 // deals it heaviest first, by the feasible prefix of the tile's last state (the bound tree's
 // superblock count), so the third waves are the cheapest tiles.  Work order only.
 bool tree_perm_eligible(const BellArgs& A) {
-    return (A.variant & (64 | 2048)) && A.tree && !A.labor && A.C <= 1 && A.np >= 1 && A.np <= 8 &&
+    return (A.variant & (64 | 2048)) && A.tree && A.C <= 1 && A.np >= 1 && A.np <= 8 &&
            (A.variant & (1 | 2 | 4 | 8)) == 0;
 }
 constexpr int kSimdsPerXcd = 128;  // MI355X: 32 CUs x 4 SIMDs per XCD
@@ -271,7 +271,8 @@ int ws_tree_perm(aiy_ws* ws, const BellArgs& A, hipStream_t st) {
     // PK one-wave tiles per workgroup (bell_tree_pack); workgroup b runs on XCD b mod 8, its
     // waves take slots b·PK .. b·PK + PK - 1; the last workgroup's unused slots hold -1
     const int PK = bell_tree_pack(A), nwg = (G + PK - 1) / PK, slots = nwg * PK;
-    std::vector<int> kf((size_t)N * Na);
+    const size_t nall = (size_t)N * Na;
+    std::vector<int> kf((size_t)A.Nl * nall);  // [labour level][row][state]
     AIY_HIP(hipMemcpyAsync(kf.data(), A.kf, kf.size() * sizeof(int), hipMemcpyDeviceToHost, st));
     AIY_HIP(hipStreamSynchronize(st));
     std::vector<int> perm(slots, -1);
@@ -281,10 +282,12 @@ int ws_tree_perm(aiy_ws* ws, const BellArgs& A, hipStream_t st) {
         if (x == (nwg - 1) % 8) size -= slots - G;
         std::vector<int> items(size);
         for (int u = 0; u < size; ++u) items[u] = start + u;
-        auto cost = [&](int it) {
+        auto cost = [&](int it) {  // the feasible prefixes of the tile's last state
             const int i = it / ntile, t = it % ntile;
             const int jl = std::min(Na - 1, t * TW + TW - 1);
-            return kf[(size_t)i * Na + jl];
+            long long c = 0;
+            for (int l = 0; l < A.Nl; ++l) c += kf[l * nall + (size_t)i * Na + jl];
+            return c;
         };
         if (A.variant & 64) {  // the whole range heaviest first
             std::stable_sort(items.begin(), items.end(),
