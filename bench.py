@@ -336,7 +336,7 @@ def main():
         effective = FLOPS_PER_CANDIDATE * evals_per_sweep / (kern_avg_ms * 1e-3) / 1e12
         traffic = None
         # PMC / HBM-traffic passes over the same sweeps 6..25 on the current kernels
-        # (tools/exp/r04_g8.sh: tools/pmc.sh + pmc_summary / pmc_traffic, skip 5 take 20)
+        # (tools/exp/r04_g8.sh / r04_g16.sh: tools/pmc.sh + pmc_summary / pmc_traffic, skip 5 take 20)
         tf_name, pmc_name = "r04_traffic_vfi_tree.json", "r04_pmc_tree.json"
         tf = _json_profile(tf_name)
         if tf:
