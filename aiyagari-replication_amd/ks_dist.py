@@ -380,19 +380,36 @@ class DirectPeers:
                                  [addr[owner[c]][2 + b] + cb * c for c in range(4 * nK)],
                                  dtype=torch.int64, device=V.device) for b in (0, 1)]
         # the counter page: rank 0 creates it, every rank maps and registers it
-        name = [None]
+        name, fail_msg = [None], None
         if rank == 0:
-            self._shm = shared_memory.SharedMemory(create=True, size=self.PAGE)
-            self._shm.buf[:self.PAGE] = bytes(self.PAGE)
-            name[0] = self._shm.name
+            try:
+                self._shm = shared_memory.SharedMemory(create=True, size=self.PAGE)
+                self._shm.buf[:self.PAGE] = bytes(self.PAGE)
+                name[0] = self._shm.name
+            except Exception as e:  # noqa: BLE001 (agreed below)
+                fail_msg = repr(e)
         dist.broadcast_object_list(name, src=0)
-        if rank != 0:
-            self._shm = shared_memory.SharedMemory(name=name[0])
-            try:  # the creator unlinks it; keep this process's tracker from doing so too
-                from multiprocessing import resource_tracker
-                resource_tracker.unregister(self._shm._name, "shared_memory")
-            except Exception:
-                pass
+        if rank != 0 and name[0] is not None:
+            try:
+                self._shm = shared_memory.SharedMemory(name=name[0])
+                try:  # the creator unlinks it; keep this process's tracker from doing so too
+                    from multiprocessing import resource_tracker
+                    resource_tracker.unregister(self._shm._name, "shared_memory")
+                except Exception:  # noqa: BLE001
+                    pass
+            except Exception as e:  # noqa: BLE001
+                fail_msg = repr(e)
+        elif name[0] is None:
+            fail_msg = fail_msg or "rank 0 could not create the counter page"
+
+        def _drop_page():
+            self._unmap()
+            if self._shm is not None:
+                self._shm.close()
+                if rank == 0:
+                    self._shm.unlink()
+                self._shm = None
+        _agree_or_raise(fail_msg, V.device, "DirectPeers: counter page", _drop_page)
         self._host = C.c_char.from_buffer(self._shm.buf)
         self._hostp = C.addressof(self._host)
         dp = vp()
