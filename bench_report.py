@@ -81,6 +81,8 @@ def leg_summary(leg):
     if cv is not None:
         s["cpu"] = cv
         s["cpu_cores"] = cores
+    if isinstance(leg.get("error"), str):   # a leg that failed says so in the line
+        s["error"] = leg["error"][:160]
     for k in ("wall_s_gpu", "wall_s_cpu", "identical_trace", "r", "r_gpu", "iters", "wall_ms",
               "ms_per_sweep", "us_per_step", "us_per_push", "howard_ms_per_sweep",
               "vfi_iteration_ms", "r_equals_reference_trace", "speedup_vs_sequential_rates",
@@ -97,7 +99,7 @@ def legs_of(out):
     for name, v in out.items():
         if name in skip or not isinstance(v, dict):
             continue
-        if "value" in v or "roofline" in v or "wall_s_gpu" in v or "iters" in v:
+        if "value" in v or "roofline" in v or "wall_s_gpu" in v or "iters" in v or "error" in v:
             yield name, v
         else:
             for sub, w in v.items():

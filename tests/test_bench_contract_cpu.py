@@ -108,3 +108,15 @@ def test_side_benches_refuse_world_mismatch(script):
     r = subprocess.run([sys.executable, str(ROOT / script), "--gpus", "4"], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "WORLD_SIZE" in r.stderr
+
+
+def test_failed_leg_is_reported():
+    """A leg that raised (e.g. the N > 1 `ks_direct` leg) appears in the line with its error."""
+    out = {"metric": "m", "value": 1.0, "unit": "u", "n_gpus": 2, "steps": 1, "warmup": 0,
+           "ms_per_step": 1.0, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "f64", "data": "synthetic", "config": {"workload": "w"},
+           "ks_direct": {"error": "DirectPeers: IPC mapping: " + "x" * 500}}
+    line = bench_report.contract_line(out)
+    d = json.loads(line)
+    assert d["legs"]["ks_direct"]["error"].startswith("DirectPeers: IPC mapping")
+    assert len(d["legs"]["ks_direct"]["error"]) <= 160
