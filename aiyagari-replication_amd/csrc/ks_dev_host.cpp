@@ -1,9 +1,11 @@
 // Device tier of the Krusell-Smith VFI (A6/A7) for one process per GPU: a handle owns one
 // shard — the K range [K0, K1) of all four s, or of one z's two s ((K, Z) slices, so the
 // reference's K = 4 grid spreads over 8 ranks) — and runs the improvement, Howard and
-// relative-difference kernels on it, reading full k x K x S arrays already in HBM.  The
-// caller (aiyagari-replication_amd/ks_dist.py) exchanges the owned value slices between
-// ranks with an RCCL all-gather after every Howard sweep.
+// relative-difference kernels on it, reading full k x K x S arrays already in HBM — or, on
+// the direct schedule, the forecast columns through a table of pointers into the owners'
+// buffers (ks_dev_set_columns).  The caller (aiyagari-replication_amd/ks_dist.py, or
+// ks_multi_host.cpp for one process) moves halos / ghost blocks between shards or, on the
+// direct schedule, only orders the sweeps.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

@@ -8,8 +8,12 @@ owned node, the value columns at the forecast K'_idx(s, K) for all s' (Krusell_S
 335-349) and nothing else.  So after every sweep a rank receives exactly the columns its
 nodes forecast into that other ranks own (the halo, `halo_plan`; point-to-point isend/irecv
 pairs, RCCL over xGMI on GPUs) — with the near-identity ALM that is one or two neighbour
-columns, not the whole array.  `exchange="allgather"` keeps the plain all-gather of every
-owned slice for comparison.  The relative-difference stop is an all-reduce MAX of one double;
+columns, not the whole array; with `depth = m` the halo is exchanged once per block of m
+sweeps and a ghost rectangle of neighbouring columns is swept redundantly in between.
+`exchange="direct"` (DirectPeers) drops the copies altogether: each rank maps its neighbours'
+column buffers through IPC handles and reads the forecast columns in place, with a
+stream-ordered counter hand-off per sweep.  `exchange="allgather"` keeps the plain all-gather
+of every owned slice for comparison.  The relative-difference stop is an all-reduce MAX of one double;
 the full value and k_opt arrays are all-gathered once, at the end.  The kernels are the ones
 of the single-device solve (ks_vfi_solve), in the same order, so any number of ranks
 reproduces it bit for bit.
