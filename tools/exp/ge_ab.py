@@ -1,5 +1,7 @@
 """A/B of the overlapped GE driver (round-4 rework vs the HEAD copy in _ge_base.py): wall time
-and identical traces, alternating, 4 rounds."""
+and identical traces, alternating, 4 rounds.  (Record of profiles/r04_g25_ge_driver_ab.txt: the
+rework was reverted, and _ge_base.py was a temporary copy of the package's ge.py at HEAD placed
+next to it for the run.)"""
 import importlib
 import json
 import sys
