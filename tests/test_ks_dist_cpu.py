@@ -274,3 +274,37 @@ def test_calibration_matches_oracle_setup():
         kg2, Kg2, P2, V02 = cal.krusell_smith(k_size=k, K_size=K)
         for a, b in ((kg, kg2), (Kg, Kg2), (P, P2), (V0, V02)):
             assert np.array_equal(a, b)
+
+
+def _agree_worker(rank, world, port, outdir, failing):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    kd = _pkg().ks_dist
+    cleaned = []
+    msg = "boom" if rank in failing else None
+    try:
+        kd._agree_or_raise(msg, "cpu", "probe", lambda: cleaned.append(1))
+        res = "ok"
+    except RuntimeError as e:
+        res = str(e)
+    dist.barrier()   # every rank is out of the collective: nobody was left inside it
+    Path(outdir, f"a{rank}.json").write_text(json.dumps(dict(res=res, cleaned=len(cleaned))))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("failing", [(), (1,), (0, 2)])
+def test_direct_failures_are_agreed(tmp_path, failing):
+    """DirectPeers raises setup failures and wait timeouts on EVERY rank together
+    (ks_dist._agree_or_raise: one all-reduce), after its cleanup, so a failure on one rank never
+    leaves the others inside a collective — gloo, 3 ranks."""
+    import torch.multiprocessing as mp
+    port = 32100 + (os.getpid() % 1000) + 7 * len(failing)
+    mp.spawn(_agree_worker, args=(3, port, str(tmp_path), failing), nprocs=3, join=True)
+    for rank in range(3):
+        d = json.loads(Path(tmp_path, f"a{rank}.json").read_text())
+        if failing:
+            assert d["res"].startswith("probe: ") and d["cleaned"] == 1
+            assert ("boom" in d["res"]) == (rank in failing)
+        else:
+            assert d["res"] == "ok" and d["cleaned"] == 0
