@@ -920,7 +920,7 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
     }
 
     double x[R], best[R];
-    int idx[R], hk0[R];
+    int idx[R], hk0[R], mlast[R];  // mlast: the last sweep's shift (packed into mom's high half)
     bool okr[R], feas[R];
     // momentum (variant bit 9 clear): the argmax's shift over the last hinted sweep, so the
     // start-up also tries hint + shift — in the early sweeps of a solve the optimum drifts by
@@ -936,12 +936,18 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
         best[r] = __builtin_nan("");
         idx[r] = -1;
         hk0[r] = -1;
+        mlast[r] = 0;
         feas[r] = false;
         if (!okr[r]) continue;
         for (int l = 0; l < Nl; ++l) feas[r] = feas[r] || A.kf[l * nall + t] > 0;
         if (A.hint) {
             const int h = A.hint[t];
-            const int mv = (mom && h >= 0) ? max(-Na, min(Na, mom[t])) : 0;
+            // mom packs two shifts: low 16 bits the last sweep's, high 16 the one before; with
+            // variant bit 21 the start extrapolates the drift linearly (2·last − previous)
+            const int mraw = (mom && h >= 0) ? mom[t] : 0;
+            const int ms0 = (int)(short)(mraw & 0xffff), ms1 = (int)(short)(mraw >> 16);
+            mlast[r] = ms0;
+            const int mv = max(-Na, min(Na, (A.variant & (1 << 21)) ? 2 * ms0 - ms1 : ms0));
             if (h >= 0) {
                 const int hl = h % Nl;
                 const int kf = A.kf[hl * nall + t];
@@ -1481,8 +1487,11 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
             if (LAB && A.pl) A.pl[t] = A.L[l];
         }
         A.v_new[t] = b;
-        if (mom && A.hint)  // this sweep's shift of the argmax, for the next sweep's start
-            mom[t] = (hk0[r] >= 0 && idx[r] >= 0) ? idx[r] / Nl - hk0[r] : 0;
+        if (mom && A.hint) {  // this sweep's shift of the argmax, for the next sweep's start
+            const int sh = (hk0[r] >= 0 && idx[r] >= 0) ? idx[r] / Nl - hk0[r] : 0;
+            const int shc = max(-32767, min(32767, sh));
+            mom[t] = (int)(((unsigned)shc & 0xffffu) | ((unsigned)mlast[r] << 16));
+        }
         const double d = fabs(b - vo);
         if (d == d) {
             dmax = okd ? fmax(dmax, d) : d;

@@ -158,10 +158,12 @@ static int bell_args(aiy_ws* ws, const BellCall& c, BellArgs& A, hipStream_t st)
     // solve to tol 8.74 -> 8.63 ms; heaviest-first (bit 6) 37.6 us / 8.75 ms; narrower tiles
     // (bit 13) slower, 40.6 / 39.3 us (profiles/r04_g7_order_ab.txt).  Two one-wave tiles per
     // workgroup (bits 16-17 = 1) on top: 36.5 -> 36.0 us, solve 8.68 -> 8.59 ms; four: 36.3 us,
-    // eight: 47 us (profiles/r04_g9_pack_ab.txt)
+    // eight: 47 us (profiles/r04_g9_pack_ab.txt).  Bit 21 (the start's drift extrapolated from
+    // the last two shifts): A1 36.1 -> 35.6 us, labour 0.285 -> 0.276 ms; neutral at Na = 400
+    // (profiles/r04_g27_*, r04_g28_*)
     const int var = ws->variant >= 0 ? ws->variant
                     : ws->Na <= 4096 ? (c.labor ? 4 | 4096 : 2)
-                    : (c.labor ? 16 : 16 | 2048 | 1 << 16);
+                    : (c.labor ? 16 | 1 << 21 : 16 | 2048 | 1 << 16 | 1 << 21);
     A.variant = var;
     A.ev_mfma = bell_ev_mfma(A.N, ws->variant);
     // (variant bit 13) one-wave tiles of tw < 64 states, tw = ceil(N·Na / (3 waves × 1,024
@@ -604,7 +606,7 @@ int bell_solve_batch_dev(aiy_ws* ws, int64_t C, const double* r, const double* w
     BellArgs A{};
     A.N = (int)ws->N; A.Na = (int)ws->Na; A.Nl = 1; A.labor = false; A.np = np;
     A.coarse = ws->coarse; A.CK = ws->CK;
-    A.variant = ws->variant >= 0 ? ws->variant : (ws->Na <= 4096 ? 0 : 16);
+    A.variant = ws->variant >= 0 ? ws->variant : (ws->Na <= 4096 ? 0 : 16 | 1 << 21);
     A.variant &= ~(1 | 2 | 4 | 8);  // one state per lane, one wave per tile, tree screen
     A.ev_mfma = bell_ev_mfma(A.N, ws->variant);
     A.beta = beta; A.sigma = sigma; A.a = a; A.s = s; A.P = P;
@@ -781,7 +783,7 @@ int aiy_ws_invalidate(aiy_ws* ws) {
 
 int aiy_ws_set_variant(aiy_ws* ws, int variant) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
-    if (variant < -1 || variant >= (1 << 21)) return fail(AIY_BAD_ARG, "variant in [-1, 2^21)");
+    if (variant < -1 || variant >= (1 << 22)) return fail(AIY_BAD_ARG, "variant in [-1, 2^22)");
     ws->variant = variant;
     return AIY_OK;
 }

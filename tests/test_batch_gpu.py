@@ -51,7 +51,7 @@ def _batch_vs_single(pkg, torch, cal, rs, v0, max_iter=1000, sigma=5.0, hint=Non
     return it
 
 
-@pytest.mark.parametrize("Na", [400, 1500])
+@pytest.mark.parametrize("Na", [400, 1500, 5000])
 def test_batch_equals_separate_solves(pkg, gpu, Na):
     import torch
     cal = pkg.calibration.aiyagari(Na=Na)
