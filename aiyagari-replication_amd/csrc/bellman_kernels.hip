@@ -968,12 +968,16 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
                     // the extrapolated start hm = hint + last shift and its two neighbours,
                     // when that window does not touch the hint's own
                     const int hm = min(max(hk + mv, 0), kf - 1);
-                    const bool usem = hm > hk + wn + 1 || hm < hk - wn - 1;
+                    // bit 23: when the extrapolated window is used, the hint's window is the
+                    // hint alone (the drift predictor is usually right: three fewer evaluations)
+                    constexpr int mw = 1;
+                    const bool usem = hm > hk + wn + mw || hm < hk - wn - mw;
+                    const int wnh = (usem && (A.variant & (1 << 23))) ? 0 : wn;
                     constexpr int WM = 8;
                     double wa[2 * WM + 1], we[2 * WM + 1], ma[3], me[3];
 #pragma unroll
                     for (int d = -WM; d <= WM; ++d) {
-                        if (d < -wn || d > wn) continue;  // wave-uniform
+                        if (d < -wnh || d > wnh) continue;  // (per lane when bit 23 is set)
                         const int kc = min(max(hk + d, 0), kf - 1);
                         wa[d + WM] = a[kc];
                         we[d + WM] = ev[kc];
@@ -988,7 +992,7 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
                     }
 #pragma unroll
                     for (int d = -WM; d <= WM; ++d) {
-                        if (d < -wn || d > wn) continue;
+                        if (d < -wnh || d > wnh) continue;
                         const int kc = min(max(hk + d, 0), kf - 1);
                         lexi_take(bell_val<NP, LAB>(coh - wa[d + WM], we[d + WM], A.sigma, dis),
                                   hl + Nl * kc, best[r], idx[r]);
@@ -1009,9 +1013,9 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
                     // the bar one passing candidate at a time.  Any candidate is a valid bar, so
                     // the result does not depend on it (the tree below still proves the maximum).
                     const int kb = idx[r] >= 0 ? idx[r] / Nl : hk;
-                    int dir = kb >= hk + wn ? 1 : (kb <= hk - wn ? -1 : 0);
-                    if (usem && kb >= hm - 1 && kb <= hm + 1)  // best in the extrapolated window
-                        dir = kb == hm + 1 ? 1 : (kb == hm - 1 ? -1 : 0);
+                    int dir = kb >= hk + wnh ? 1 : (kb <= hk - wnh ? -1 : 0);
+                    if (usem && kb >= hm - mw && kb <= hm + mw)  // best in the extrapolated window
+                        dir = kb == hm + mw ? 1 : (kb == hm - mw ? -1 : 0);
                     if (dir != 0 && !(A.variant & 32)) {
                         int k = kb, step = 2;
                         for (;;) {

@@ -127,7 +127,7 @@ def test_labor_solve_infeasible_states_keep_incoming(pkg, gpu, max_iter):
                                         (400, 4098), (400, 4100), (400, 4102), (1100, 4100),
                                         (2000, 4102), (100, 4100), (1100, 2064), (2000, 80),
                                         (5000, 2064), (5000, 80), (5000, 16 | 1 << 21),
-                                        (1100, 4100 | 1 << 21)])
+                                        (1100, 4100 | 1 << 21), (5000, 16 | 1 << 21 | 1 << 23)])
 def test_labor_cooperating_waves_vs_oracle(pkg, gpu, Na, variant):
     """Labour tree kernel with 1, 2, 4 and 8 cooperating waves per tile (variant bits 1-2; the
     Na <= 4096 default is 2 waves), and the exhaustive scan (bit 10): device-tier sweeps with the hint chain of a solve, then one
