@@ -973,11 +973,14 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
                     constexpr int mw = 1;
                     const bool usem = hm > hk + wn + mw || hm < hk - wn - mw;
                     const int wnh = (usem && (A.variant & (1 << 23))) ? 0 : wn;
+                    // bit 24 (with 23): not even the hint itself — the extrapolated window
+                    // and the climb from it carry the start alone
+                    const bool skiph = usem && (A.variant & (1 << 24));
                     constexpr int WM = 8;
                     double wa[2 * WM + 1], we[2 * WM + 1], ma[3], me[3];
 #pragma unroll
                     for (int d = -WM; d <= WM; ++d) {
-                        if (d < -wnh || d > wnh) continue;  // (per lane when bit 23 is set)
+                        if (d < -wnh || d > wnh || skiph) continue;  // (per lane: bits 23-24)
                         const int kc = min(max(hk + d, 0), kf - 1);
                         wa[d + WM] = a[kc];
                         we[d + WM] = ev[kc];
@@ -992,7 +995,7 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
                     }
 #pragma unroll
                     for (int d = -WM; d <= WM; ++d) {
-                        if (d < -wnh || d > wnh) continue;
+                        if (d < -wnh || d > wnh || skiph) continue;
                         const int kc = min(max(hk + d, 0), kf - 1);
                         lexi_take(bell_val<NP, LAB>(coh - wa[d + WM], we[d + WM], A.sigma, dis),
                                   hl + Nl * kc, best[r], idx[r]);

@@ -161,10 +161,12 @@ static int bell_args(aiy_ws* ws, const BellCall& c, BellArgs& A, hipStream_t st)
     // eight: 47 us (profiles/r04_g9_pack_ab.txt).  Bit 21 (the start's drift extrapolated from
     // the last two shifts): A1 36.1 -> 35.6 us, labour 0.285 -> 0.276 ms; neutral at Na = 400
     // (profiles/r04_g27_*, r04_g28_*).  Bit 23 (the hint's window reduced to the hint when the
-    // extrapolated window is used) on top for A1: 36.2 -> 35.75 us (profiles/r04_g33_*)
+    // extrapolated window is used) on top for A1: 36.2 -> 35.75 us (profiles/r04_g33_*); bit 24
+    // (no hint evaluation then at all): kernel 30.9 -> 30.6 us, step 35.7 -> 35.6 (r04_g36_*)
     const int var = ws->variant >= 0 ? ws->variant
                     : ws->Na <= 4096 ? (c.labor ? 4 | 4096 : 2)
-                    : (c.labor ? 16 | 1 << 21 : 16 | 2048 | 1 << 16 | 1 << 21 | 1 << 23);
+                    : (c.labor ? 16 | 1 << 21
+                               : 16 | 2048 | 1 << 16 | 1 << 21 | 1 << 23 | 1 << 24);
     A.variant = var;
     A.ev_mfma = bell_ev_mfma(A.N, ws->variant);
     // (variant bit 13) one-wave tiles of tw < 64 states, tw = ceil(N·Na / (3 waves × 1,024
@@ -784,7 +786,7 @@ int aiy_ws_invalidate(aiy_ws* ws) {
 
 int aiy_ws_set_variant(aiy_ws* ws, int variant) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
-    if (variant < -1 || variant >= (1 << 24)) return fail(AIY_BAD_ARG, "variant in [-1, 2^24)");
+    if (variant < -1 || variant >= (1 << 25)) return fail(AIY_BAD_ARG, "variant in [-1, 2^25)");
     ws->variant = variant;
     return AIY_OK;
 }

@@ -253,14 +253,15 @@ int aiy_ws_set_search(aiy_ws* ws, int coarse_stride, int k_chunk);
  * batches in flight — 2·max_batch + 1 value buffers and 2·max_batch policy sets per workspace. */
 int aiy_ws_set_speculation(aiy_ws* ws, int max_batch);
 /* kernel shapes and A/B knobs (tuning only; results are identical for every value in
- * [-1, 2^24)).  VFI, bit 3 clear (default): the bound tree screen, bit 0 = 2 states per lane
+ * [-1, 2^25)).  VFI, bit 3 clear (default): the bound tree screen, bit 0 = 2 states per lane
  * (else 1), bits 1-2 = 1, 2, 4 or 8 cooperating waves per tile, bit 4 = XCD-aware tile order,
  * bit 6 / bit 11 = one-wave tiles dispatched from a per-workspace permutation that keeps each
  * XCD's tile range and deals it heaviest first / row-major with its cheapest tiles last, bit 13 =
  * one-wave tiles narrowed to ceil(N·Na / 3072) states (>= 16), bits 16-17 = (with bit 6 or
  * 11, A1 at sigma = 5) 1, 2, 4 or 8 one-wave tiles per workgroup, bit 21 = the start-up
  * extrapolates the argmax drift from the last two sweeps' shifts (else the last shift), bit 23 =
- * the hint's own window is the hint alone when the extrapolated window is evaluated;
+ * the hint's own window is the hint alone when the extrapolated window is evaluated, bit 24
+ * (with 23) = not even the hint then;
  * bit 3 set: the chunked screen + merge, with bit 0 = 4 states per lane (else 2), bit 1 =
  * registers capped for 8 waves per SIMD, bit 2 = fp64-only screen (else the packed fp32
  * pre-screen with directed-rounding bounds first).  Tree screen extras: bit 5 = no hill-climb
@@ -272,8 +273,8 @@ int aiy_ws_set_speculation(aiy_ws* ws, int max_batch);
  * (default there: one fused launch); bit 19 = no chaining in the solve loops (two launches per
  * step); bit 20 = no interp1 segment windows.  -1 (default): chosen by size — Na <= 4096:
  * 2 cooperating waves per tile (A1), 4 with bit 12 (labour); else 16 | 2048 | 1 << 16 |
- * 1 << 21 | 1 << 23 (A1), 16 | 1 << 21 (labour) and 16 | 1 << 21 (the batched multi-rate
- * solve). */
+ * 1 << 21 | 1 << 23 | 1 << 24 (A1), 16 | 1 << 21 (labour) and 16 | 1 << 21 (the batched
+ * multi-rate solve). */
 int aiy_ws_set_variant(aiy_ws* ws, int variant);
 
 /* A1 on device.  hint (nullable, [N][Na] int32 0-based) = previous sweep's argmax; the result

@@ -77,7 +77,8 @@ def test_screened_equals_plain_and_oracle(pkg, gpu, Na, shocks, variant, k_chunk
 
 
 @pytest.mark.parametrize("variant", [0, 16, 4098, 4100, 1 << 21, 2064 | 1 << 16 | 1 << 21,
-                                     2064 | 1 << 16 | 1 << 21 | 1 << 23])
+                                     2064 | 1 << 16 | 1 << 21 | 1 << 23,
+                                     2064 | 1 << 16 | 1 << 21 | 3 << 23])
 def test_hint_does_not_change_result(pkg, gpu, variant):
     import torch
     cal = no.calib_aiyagari(Na=900)
@@ -150,7 +151,7 @@ def test_full_size_bitwise_vs_oracle(pkg, gpu):
 @pytest.mark.parametrize("variant", [0, 1, 2, 6, 8, 12, 16, 32, 96, 512, 4098, 4100, 4102, 80, 2064,
                                      8192, 8208, 8272, 10256, 2064 | 2 << 16,
                                      10240 | 1 << 16, 64 | 3 << 16, 1 << 21, 4100 | 1 << 21,
-                                     1 << 21 | 1 << 23, 16 | 1 << 23])
+                                     1 << 21 | 1 << 23, 16 | 1 << 23, 1 << 21 | 3 << 23])
 def test_screen_stress_noisy_value(pkg, gpu, variant):
     """Rough value functions put many candidates within rounding distance of the running best
     (near-ties everywhere, multi-modal objectives): the fp32 pre-screen, the fp64 screen and
@@ -175,7 +176,8 @@ def test_screen_stress_noisy_value(pkg, gpu, variant):
 @pytest.mark.parametrize("variant", [16, 80, 2064, 8208, 8272, 10256, 2064 | 1 << 16,
                                      2064 | 2 << 16, 2064 | 3 << 16, 80 | 2 << 16,
                                      10256 | 2 << 16, 16 | 2048 | 1 << 16 | 1 << 21,
-                                     16 | 2048 | 1 << 16 | 1 << 21 | 1 << 23])
+                                     16 | 2048 | 1 << 16 | 1 << 21 | 1 << 23,
+                                     16 | 2048 | 1 << 16 | 1 << 21 | 3 << 23])
 def test_full_size_dispatch_orders_and_tile_widths(pkg, gpu, variant):
     """Na = 20,000 (configs[1]): the tree's dispatch orders (bit 6: each XCD's range heaviest
     first; bit 11: its cheapest tiles last), the narrow one-wave tiles (bit 13: 46 states per
