@@ -89,6 +89,8 @@ inline int bell_tree_pack(const BellArgs& A) {
 int launch_bell_ev_mfma(const BellArgs& A, hipStream_t st);
 int launch_bell_table(const BellArgs& A, hipStream_t st);
 int launch_bell_kf(const BellArgs& A, hipStream_t st);
+int launch_kf_tile_last(const int* kf, int rows, int Na, int TW, int ntile, int* out,
+                        hipStream_t st);
 int launch_bell_init(const BellArgs& A, hipStream_t st);
 int launch_bell_screen(const BellArgs& A, hipStream_t st);
 int launch_bell_tree(const BellArgs& A, hipStream_t st);

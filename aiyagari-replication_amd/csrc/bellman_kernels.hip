@@ -1747,6 +1747,23 @@ int launch_bell_kf(const BellArgs& A, hipStream_t st) {
     return AIY_OK;
 }
 
+// kf of each tile's last state: out[row][t] = kf[row][min(Na-1, t·TW + TW-1)] for the Nl·N rows
+// (the host-side dispatch order needs only these: ws_tree_perm)
+__global__ void kf_tile_last_kernel(const int* __restrict__ kf, int rows, int Na, int TW,
+                                    int ntile, int* __restrict__ out) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= rows * ntile) return;
+    const int row = g / ntile, t = g - row * ntile;
+    out[g] = kf[(size_t)row * Na + min(Na - 1, t * TW + TW - 1)];
+}
+int launch_kf_tile_last(const int* kf, int rows, int Na, int TW, int ntile, int* out,
+                        hipStream_t st) {
+    kf_tile_last_kernel<<<cdiv((long long)rows * ntile, 256), 256, 0, st>>>(kf, rows, Na, TW,
+                                                                             ntile, out);
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
+}
+
 #ifndef AIY_BELL_R
 #define AIY_BELL_R 2
 #endif

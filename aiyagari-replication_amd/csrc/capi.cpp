@@ -276,9 +276,19 @@ int ws_tree_perm(aiy_ws* ws, const BellArgs& A, hipStream_t st) {
     // PK one-wave tiles per workgroup (bell_tree_pack); workgroup b runs on XCD b mod 8, its
     // waves take slots b·PK .. b·PK + PK - 1; the last workgroup's unused slots hold -1
     const int PK = bell_tree_pack(A), nwg = (G + PK - 1) / PK, slots = nwg * PK;
-    const size_t nall = (size_t)N * Na;
-    std::vector<int> kf((size_t)A.Nl * nall);  // [labour level][row][state]
-    AIY_HIP(hipMemcpyAsync(kf.data(), A.kf, kf.size() * sizeof(int), hipMemcpyDeviceToHost, st));
+    // only each tile's last state's prefixes cross to the host (not all of kf)
+    const int rows = A.Nl * N;
+    if (ws->kf_last_cap < rows * ntile) {
+        if (ws->kf_last) (void)hipFree(ws->kf_last);
+        ws->kf_last = nullptr;
+        ws->kf_last_cap = 0;
+        AIY_HIP(hipMalloc((void**)&ws->kf_last, (size_t)rows * ntile * sizeof(int)));
+        ws->kf_last_cap = rows * ntile;
+    }
+    std::vector<int> kl((size_t)rows * ntile);  // [labour level][row][tile]
+    AIY_TRY(launch_kf_tile_last(A.kf, rows, Na, TW, ntile, ws->kf_last, st));
+    AIY_HIP(hipMemcpyAsync(kl.data(), ws->kf_last, kl.size() * sizeof(int),
+                           hipMemcpyDeviceToHost, st));
     AIY_HIP(hipStreamSynchronize(st));
     std::vector<int> perm(slots, -1);
     int start = 0;
@@ -289,9 +299,8 @@ int ws_tree_perm(aiy_ws* ws, const BellArgs& A, hipStream_t st) {
         for (int u = 0; u < size; ++u) items[u] = start + u;
         auto cost = [&](int it) {  // the feasible prefixes of the tile's last state
             const int i = it / ntile, t = it % ntile;
-            const int jl = std::min(Na - 1, t * TW + TW - 1);
             long long c = 0;
-            for (int l = 0; l < A.Nl; ++l) c += kf[l * nall + (size_t)i * Na + jl];
+            for (int l = 0; l < A.Nl; ++l) c += kl[((size_t)l * N + i) * ntile + t];
             return c;
         };
         if (A.variant & 64) {  // the whole range heaviest first

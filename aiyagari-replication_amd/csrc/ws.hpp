@@ -39,6 +39,8 @@ struct aiy_ws {
     bool kf_lab = false;
     int* tree_perm = nullptr;  // tree dispatch order for the cached kf (ws_tree_perm)
     int perm_cap = 0, perm_key = 0;
+    int* kf_last = nullptr;    // [Nl][N][ntile] kf of each tile's last state (ws_tree_perm)
+    int kf_last_cap = 0;
     bool perm_ok = false;
     int* partial = nullptr;
     size_t partial_cap = 0;
@@ -160,7 +162,8 @@ struct aiy_ws {
     }
     void free_all() {
         void* ps[] = {EV, T, T32, Dm, Dm8, Dt, Dm512, touched, best0, idx0, mom, dis, kf, partial, diff, hitcount, trace, g0, g1, g2, gi,
-                      d_key, d_off, d_wr, d_mass, d_part, egm_x2, egm_y2, egm_seg, tree_perm};
+                      d_key, d_off, d_wr, d_mass, d_part, egm_x2, egm_y2, egm_seg, tree_perm,
+                      kf_last};
         for (void* p : ps)
             if (p) (void)hipFree(p);
         free_spec();
@@ -175,6 +178,7 @@ struct aiy_ws {
         egm_x2 = egm_y2 = nullptr;
         egm_seg = nullptr;
         tree_perm = nullptr; perm_cap = 0; perm_ok = false;
+        kf_last = nullptr; kf_last_cap = 0;
         d_key = d_off = nullptr; d_wr = d_mass = d_part = nullptr;
         partial_cap = 0;
     }

@@ -283,7 +283,9 @@ class HipShard:
     # the direct schedule (ks_vfi_solve_sharded depth = 0): forecast columns read in place
     def set_columns(self, table):
         """table: device int64 tensor of 4·nK value-column then 4·nK slope-column addresses
-        (None: back to the caller's arrays)."""
+        (None: back to the caller's arrays; a no-op on a closed shard)."""
+        if table is None and not getattr(self, "_h", None):
+            return
         check(lib().ks_dev_set_columns(self._h, ptr(table)))
 
     def slopes_own(self, V, dV):
@@ -364,13 +366,20 @@ class DirectPeers:
                     if q == rank:
                         addr.append(tuple(t.data_ptr() for t in self.V + self.dV))
                         continue
+                    # the caching allocator may put several of a rank's buffers in ONE segment
+                    # (one handle): each distinct segment is opened once and closed once, the
+                    # buffers are offsets into it (duplicate opens of one handle are
+                    # runtime-dependent)
+                    base = {}
                     row = []
                     for hb, off in allh[q][0]:
-                        p_ = vp()
-                        check(lib().aiy_ipc_open(C.create_string_buffer(hb, 64), i64(off),
-                                                 C.byref(p_)))
-                        self._opened.append((p_.value, off))
-                        row.append(p_.value)
+                        if hb not in base:
+                            p_ = vp()
+                            check(lib().aiy_ipc_open(C.create_string_buffer(hb, 64), i64(0),
+                                                     C.byref(p_)))
+                            base[hb] = p_.value
+                            self._opened.append((p_.value, 0))
+                        row.append(base[hb] + off)
                     addr.append(tuple(row))
             except Exception as e:  # noqa: BLE001
                 fail_msg = repr(e)
@@ -501,6 +510,7 @@ class DirectPeers:
         if getattr(self, "_shm", None) is None:
             return
         torch.cuda.synchronize()
+        self.shard.set_columns(None)   # its table points into the mappings released below
         dist.barrier()     # nobody reads a peer buffer or the page any more
         self._unmap()
         if getattr(self, "_hostp_reg", True):
@@ -532,6 +542,12 @@ def _solve_direct(V, k_opt, shard, nK, howard_steps, tol, max_vfi, rank, world, 
     every rank (in), own columns current on return (the caller all-gathers)."""
     import torch
     import torch.distributed as dist
+    if peers is not None and peers.shard is not shard:
+        # the peers' neighbour mask and column tables were built from ITS shard's forecast
+        # index (kp_idx, fixed by B at HipShard construction): with another shard (a new ALM B)
+        # the solve would sweep the old B and skip waits it needs (ADVICE r4)
+        raise ValueError("DirectPeers was built for another shard (a different ALM B): build "
+                         "one DirectPeers per shard")
     dp = peers if peers is not None else DirectPeers(shard, nK, rank, world, V, bounds)
     try:
         nk = dp.nk
@@ -551,11 +567,13 @@ def _solve_direct(V, k_opt, shard, nK, howard_steps, tol, max_vfi, rank, world, 
             rel = _allreduce_max(rel, V.device)
             if rel < tol:
                 break
-        shard.set_columns(None)
         for a, b in runs:
             flat(V)[a:b].copy_(flat(dp.current())[a:b])
         return it, rel
     finally:
+        # the shard must not keep the peers' column table past this solve, also on the error
+        # path: a later halo/improve call would read it after DirectPeers.close()
+        shard.set_columns(None)
         if peers is None:
             dp.close()
 

@@ -124,7 +124,8 @@ def solve_wall(pkg, ws, cal, r, w, a_t, s_t, P_t, dev):
     vb = torch.zeros_like(va)
     idx = torch.zeros((N, Na), dtype=torch.int32, device=dev)
     pk, pc = torch.empty_like(va), torch.empty_like(va)
-    torch.cuda.synchronize()
+    ws.invalidate()  # the solve at a new (r, w) rebuilds its feasible prefixes and dispatch
+    torch.cuda.synchronize()  # order (host round trip): that cost is inside the timed solve
     t0 = time.perf_counter()
     iters, _ = ws.vfi_solve(va, vb, a_t, s_t, P_t, r, w, cal["beta"], cal["sigma"], 1e-5, 1000,
                             idx, pk, pc, mode=1)

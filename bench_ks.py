@@ -182,15 +182,20 @@ def ks_direct_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, reps=3, che
     nodes = nk * nK * 4
     bpn = 52
     gbs = nodes * bpn / (th / howard) / 1e9 / world
-    return {"metric": "Krusell-Smith bellman_value evals/sec (Howard sweeps, fp64)",
-            "value": nodes * howard / th, "unit": "evals/s", "n_gpus": world,
+    exact = bool(ok[0] > 0.5)
+    out = {} if exact else {
+        "error": "direct schedule differs from the halo schedule on the same start: value "
+                 "withheld (multi-GPU parity of the direct schedule is pinned only by this check)"}
+    return {**out, "metric": "Krusell-Smith bellman_value evals/sec (Howard sweeps, fp64)",
+            "value": nodes * howard / th if exact else None, "unit": "evals/s", "n_gpus": world,
+            "value_unchecked": nodes * howard / th,
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": 8000.0, "unit": "GB/s",
                          "frac": gbs / 8000.0,
                          "basis": f"{bpn} B algorithmic per node per Howard sweep x "
                                   f"{nodes // world} nodes per GPU / sweep time"},
             "scaling": "strong", "vfi_iteration_ms": (ti + th) * 1e3,
             "howard_ms_per_sweep": th / howard * 1e3, "improve_ms": ti * 1e3,
-            "bit_exact_vs_halo": bool(ok[0] > 0.5),
+            "bit_exact_vs_halo": exact,
             "workload": f"Krusell_Smith_VFI k={nk} K={nK} S=4 ({nodes} nodes), one VFI iteration "
                         f"= improvement + {howard} Howard sweeps, median of {reps}",
             "parallelism": f"(K, Z) shards over {world} ranks (rank 0: K [{K0}, {K1}), s [{s0}, "

@@ -308,3 +308,21 @@ def test_direct_failures_are_agreed(tmp_path, failing):
             assert ("boom" in d["res"]) == (rank in failing)
         else:
             assert d["res"] == "ok" and d["cleaned"] == 0
+
+
+def test_direct_peers_bound_to_their_shard():
+    """a DirectPeers carries the neighbour mask and column tables of the shard (the
+    forecast index of one ALM B) it was built for; handing it to a solve of another shard
+    raises before any wait or launch."""
+    kd = _pkg().ks_dist
+
+    class _Shard:  # stand-ins: only identity matters to the check
+        pass
+
+    class _Peers:
+        def __init__(self, shard):
+            self.shard = shard
+
+    a, b = _Shard(), _Shard()
+    with pytest.raises(ValueError, match="another shard"):
+        kd._solve_direct(None, None, b, 4, 3, 1e-6, 1, 0, 2, None, peers=_Peers(a))
