@@ -86,6 +86,23 @@ inline int bell_tree_pack(const BellArgs& A) {
                ? 1 << ((A.variant >> 16) & 3)
                : 1;
 }
+// The small-grid sweep (bellman_wide_kernels.hip): ONE launch per sweep, a workgroup of NW
+// waves per (64-state tile, split of the candidate range), S splits per tile.  Every workgroup
+// holds its row's feasible range in LDS: (a_k, D_k) and EV_k, 24 B per candidate.
+constexpr int kWideMaxSplits = 16;
+constexpr size_t kWideMaxLds = 144 * 1024;  // dynamic part (the wave bests take <= 12 KiB more)
+inline size_t bell_wide_lds(int Na, int S, int NW) {
+    (void)S;
+    (void)NW;
+    return (size_t)Na * 24 + ((size_t)Na + 7) / 8 * 8;
+}
+// flags (A/B only, results identical): kWideBatch = a block with >= 4 voted candidates
+// evaluates all eight as independent chains; kWideClimb = the bar climbs from the hint's window
+// (measured slower than the window alone, tools/wide_tune.py)
+constexpr int kWideBatch = 1, kWideClimb = 2;
+constexpr int kWideMaxNl = 16;  // labour levels the small-grid sweep holds in registers
+int launch_bell_wide(const BellArgs& A, int S, int NW, int SB, unsigned long long* old_slots,
+                     unsigned* cnt, unsigned long long* part, int flags, hipStream_t st);
 int launch_bell_ev_mfma(const BellArgs& A, hipStream_t st);
 int launch_bell_table(const BellArgs& A, hipStream_t st);
 int launch_bell_kf(const BellArgs& A, hipStream_t st);

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -78,7 +79,10 @@ int ws_ensure_bell(aiy_ws* ws, size_t partial_slots) {
         ws->partial_cap = partial_slots;
     }
     AIY_TRY(dalloc(&ws->diff, 2 * kDiffSlots));
-    AIY_TRY(dalloc(&ws->hitcount, 4 * kDiffSlots));
+    if (!ws->hitcount) {  // zero from the start: counting may be switched on before a sweep
+        AIY_TRY(dalloc(&ws->hitcount, 4 * kDiffSlots));
+        AIY_HIP(hipMemset(ws->hitcount, 0, 4 * kDiffSlots * sizeof(unsigned long long)));
+    }
     AIY_TRY(dalloc(&ws->dis, (size_t)std::max<int64_t>(ws->Nl, 1)));
     if (!ws->hdiff)
         AIY_HIP(hipHostMalloc((void**)&ws->hdiff, (2 * kDiffSlots + 4) * sizeof(unsigned long long)));
@@ -225,7 +229,14 @@ static int bell_args(aiy_ws* ws, const BellCall& c, BellArgs& A, hipStream_t st)
     A.pc = c.pc;
     A.diff = ws->diff;
     A.fold = (unsigned long long*)c.prev_diff_out;
-    if (c.labor) AIY_TRY(launch_disutility(c.L, (int)c.Nl, c.psi, c.eta, ws->dis, st));
+    // disutility per level: cached while (L, Nl, psi, eta) are unchanged (a launch per sweep
+    // otherwise — a dependent launch in the small-grid sweep's one-launch chain)
+    if (c.labor && !(ws->dis_ok && ws->dis_L == c.L && ws->dis_Nl == c.Nl &&
+                     ws->dis_psi == c.psi && ws->dis_eta == c.eta)) {
+        AIY_TRY(launch_disutility(c.L, (int)c.Nl, c.psi, c.eta, ws->dis, st));
+        ws->dis_ok = true;
+        ws->dis_L = c.L; ws->dis_Nl = c.Nl; ws->dis_psi = c.psi; ws->dis_eta = c.eta;
+    }
     // feasible prefixes: cached while (r, w, a, s, L) are unchanged (aiy_ws_invalidate resets)
     size_t kf_need = (size_t)A.Nl * A.N * A.Na;
     if (ws->kf && ws->kf_cap < kf_need) {
@@ -335,6 +346,78 @@ int ws_tree_perm(aiy_ws* ws, const BellArgs& A, hipStream_t st) {
     return AIY_OK;
 }
 
+// The small-grid one-launch sweep (bellman_wide_kernels.hip) and its geometry.  Default: every
+// screened sweep at Na <= 1,536 (A1) / 2,048 (labour) unless a tree geometry was asked for
+// (variant >= 0 without bit 25); aiy_ws_set_wide overrides the bound and the geometry.
+// Measured (tools/wide_tune.py, profiles/r05_wide_tune.jsonl; sweeps 11-60 from v = 0, per
+// sweep, tree = table + tree launch): A1 Na = 400 7.7 vs 13.8 us, 1,000 10.2 vs 16.4, 2,048
+// 16.7 vs 16.5 (a tie: the tree from there); labour Na = 400 17 vs 32 us, 1,000 25 vs 52, 2,000
+// 56 vs 60.  One workgroup per tile (splits = 1): the cross-workgroup hand-off (sc1 partials,
+// an arrival counter) costs more than the extra workgroups save at every size measured.
+static bool wide_pick(const aiy_ws* ws, const BellArgs& A, int* S, int* NW, int* SB) {
+    if (A.np < 1 || A.np > 8 || A.C > 1 || A.ev_mfma || A.Nl > kWideMaxNl) return false;
+    const int vmax = ws->wide_max >= 0 ? ws->wide_max : (A.labor ? 2048 : 1536);
+    if (A.Na > vmax) return false;
+    if (ws->variant >= 0 && !(ws->variant & (1 << 25))) return false;
+    const int sb = ws->wide_SB > 0 ? ws->wide_SB : (A.labor ? 16 : (A.Na <= 1024 ? 32 : 64));
+    const int nw = ws->wide_NW > 0 ? ws->wide_NW : 8;
+    const int s = ws->wide_S > 0 ? ws->wide_S : 1;
+    if (bell_wide_lds(A.Na, s, nw) > kWideMaxLds) return false;
+    *S = s;
+    *NW = nw;
+    *SB = sb;
+    return true;
+}
+
+static int bell_sweep_wide(aiy_ws* ws, BellArgs& A, int S, int NW, int SB, hipStream_t st) {
+    const int ntile = (int)((ws->Na + SB - 1) / SB);
+    const size_t items = (size_t)ws->N * ntile;
+    if (!ws->wdiff) {
+        AIY_TRY(dalloc(&ws->wdiff, 4 * (size_t)kDiffSlots));
+        AIY_HIP(hipMemsetAsync(ws->wdiff, 0, 4 * kDiffSlots * sizeof(unsigned long long), st));
+        ws->wcur = 0;
+    }
+    if (ws->wcnt_cap < items) {
+        dfree(ws->wcnt);
+        AIY_TRY(dalloc(&ws->wcnt, items));
+        AIY_HIP(hipMemsetAsync(ws->wcnt, 0, items * sizeof(unsigned), st));
+        ws->wcnt_cap = items;
+    }
+    const size_t pneed = items * (size_t)S * 64 * 2;
+    if (S > 1 && ws->wpart_cap < pneed) {
+        dfree(ws->wpart);
+        AIY_TRY(dalloc(&ws->wpart, pneed));
+        ws->wpart_cap = pneed;
+    }
+    unsigned long long* cur = ws->wdiff + (size_t)ws->wcur * 2 * kDiffSlots;
+    unsigned long long* nxt = ws->wdiff + (size_t)(ws->wcur ^ 1) * 2 * kDiffSlots;
+    if (A.fold && !ws->last_wide) {  // the previous sweep's slots are the table path's
+        AIY_TRY(launch_reduce_slots(ws->diff, A.fold, st));
+        A.fold = nullptr;
+    }
+    A.diff = nxt;  // zero (the set not current); block 0 folds and clears `cur`
+    A.trace = nullptr;
+    if (ws->tracing) {  // one 64-word record per block (instrumentation)
+        const int64_t blocks = ((int64_t)items + 7) / 8 * 8 * S * 4;  // (in 16-word units)
+        if (ws->trace_cap < blocks) {
+            dfree(ws->trace);
+            AIY_TRY(dalloc(&ws->trace, 16 * (size_t)blocks));
+            ws->trace_cap = blocks;
+        }
+        AIY_HIP(hipMemsetAsync(ws->trace, 0, 16 * (size_t)ws->trace_cap * sizeof(long long), st));
+        A.trace = ws->trace;
+    }
+    const char* fl = getenv("AIY_WIDE_FLAGS");  // (A/B tooling: tools/wide_tune.py)
+    AIY_TRY(ws_dispatch_arm(ws));
+    const int rc = launch_bell_wide(A, S, NW, SB, cur, ws->wcnt, ws->wpart, fl ? atoi(fl) : 0, st);
+    ws_dispatch_commit(ws);
+    AIY_TRY(rc);
+    ws->wcur ^= 1;
+    ws->vdiff = nxt;
+    ws->last_wide = true;
+    return AIY_OK;
+}
+
 int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
     BellArgs A;
     AIY_TRY(bell_args(ws, c, A, st));
@@ -342,6 +425,18 @@ int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
     // by the scan itself); otherwise the bound tree (or the chunked screen, variant bit 3)
     const bool exhaustive = c.mode == 2 || A.np == 0 || (A.variant & 1024);
     const bool screened = !exhaustive;
+    int wS = 0, wNW = 0, wSB = 0;
+    if (screened && wide_pick(ws, A, &wS, &wNW, &wSB)) {  // small grids: one launch per sweep
+        AIY_TRY(bell_sweep_wide(ws, A, wS, wNW, wSB, st));
+        if (c.diff_out) AIY_TRY(launch_reduce_slots(ws->vdiff, c.diff_out, st));
+        return AIY_OK;
+    }
+    if (ws->last_wide && A.fold) {  // the previous sweep's slots are the wide path's
+        AIY_TRY(launch_reduce_slots(ws->vdiff, A.fold, st));
+        A.fold = nullptr;
+    }
+    ws->last_wide = false;
+    ws->vdiff = ws->diff;
     AIY_TRY(launch_bell_table(A, st));  // also clears the diff slots
     if (!screened) A.coarse = 0, A.hint = nullptr;
     if (screened && A.tree) {
@@ -369,7 +464,8 @@ int bell_sweep_dev(aiy_ws* ws, const BellCall& c, hipStream_t st) {
 
 // read {max|Δ| bits, any} from the workspace diff word (synchronises the stream)
 int ws_read_diff(aiy_ws* ws, hipStream_t st, double* d) {
-    AIY_HIP(hipMemcpyAsync(ws->hdiff, ws->diff, 2 * kDiffSlots * sizeof(unsigned long long),
+    const unsigned long long* sl = ws->vdiff ? ws->vdiff : ws->diff;  // the last sweep's slots
+    AIY_HIP(hipMemcpyAsync(ws->hdiff, sl, 2 * kDiffSlots * sizeof(unsigned long long),
                            hipMemcpyDeviceToHost, st));
     AIY_HIP(hipStreamSynchronize(st));
     *d = fold_slots_host(ws->hdiff);
@@ -790,13 +886,28 @@ int aiy_ws_trace(aiy_ws* ws, int64_t* out, int64_t cap, int64_t* n) {
 int aiy_ws_invalidate(aiy_ws* ws) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
     ws->kf_ok = false;
+    ws->dis_ok = false;
     return AIY_OK;
 }
 
 int aiy_ws_set_variant(aiy_ws* ws, int variant) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
-    if (variant < -1 || variant >= (1 << 25)) return fail(AIY_BAD_ARG, "variant in [-1, 2^25)");
+    if (variant < -1 || variant >= (1 << 26)) return fail(AIY_BAD_ARG, "variant in [-1, 2^26)");
     ws->variant = variant;
+    return AIY_OK;
+}
+
+int aiy_ws_set_wide(aiy_ws* ws, int max_na, int splits, int waves, int states) {
+    if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
+    if (max_na < -1 || splits < 0 || splits > kWideMaxSplits ||
+        (waves != 0 && waves != 4 && waves != 8 && waves != 16) ||
+        (states != 0 && states != 8 && states != 16 && states != 32 && states != 64))
+        return fail(AIY_BAD_ARG, "max_na >= -1, splits in [0, %d], waves in {0, 4, 8, 16}, "
+                    "states in {0, 8, 16, 32, 64}", kWideMaxSplits);
+    ws->wide_max = max_na;
+    ws->wide_S = splits;
+    ws->wide_NW = waves;
+    ws->wide_SB = states;
     return AIY_OK;
 }
 
@@ -890,6 +1001,31 @@ int aiy_labor_vfi_sweep_dev(aiy_ws* ws, const double* v_old, const double* a_gri
     c.sigma = sigma; c.hint = hint; c.v_new = v_new; c.idx = lin; c.pk = policy_k;
     c.pl = policy_l; c.pc = policy_c; c.diff_out = diff;
     return bell_sweep_dev(ws, c, (hipStream_t)stream);
+}
+
+int aiy_labor_vfi_sweeps_dev(aiy_ws* ws, double* v_a, double* v_b, const double* a_grid,
+                             const double* s, const double* P, const double* labor_choice,
+                             double r, double w, double beta, double sigma, double psi,
+                             double eta, const int32_t* hint, int64_t nsweeps, int32_t* lin,
+                             double* policy_k, double* policy_l, double* policy_c, double* diff,
+                             void* stream) {
+    if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
+    if (nsweeps < 1) return fail(AIY_BAD_ARG, "nsweeps >= 1");
+    if (!v_a || !v_b || v_a == v_b) return fail(AIY_BAD_ARG, "two distinct value buffers");
+    if (!lin) return fail(AIY_BAD_ARG, "NULL lin (the next sweep's hint)");
+    BellCall c{};
+    c.labor = true; c.Nl = ws->Nl; c.L = labor_choice; c.psi = psi; c.eta = eta;
+    c.a = a_grid; c.s = s; c.P = P; c.r = r; c.w = w; c.beta = beta; c.sigma = sigma;
+    c.idx = lin; c.pk = policy_k; c.pl = policy_l; c.pc = policy_c;
+    for (int64_t g = 0; g < nsweeps; ++g) {  // sweep g + 1 of the loop: ping-pong v_a / v_b
+        c.v_old = (g & 1) ? v_b : v_a;
+        c.v_new = (g & 1) ? v_a : v_b;
+        c.hint = g ? lin : hint;
+        c.keep_incoming = (g == 0);
+        c.diff_out = (g == nsweeps - 1) ? diff : nullptr;
+        AIY_TRY(bell_sweep_dev(ws, c, (hipStream_t)stream));
+    }
+    return AIY_OK;
 }
 
 }  // extern "C"

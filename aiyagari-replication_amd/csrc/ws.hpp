@@ -41,6 +41,22 @@ struct aiy_ws {
     int perm_cap = 0, perm_key = 0;
     int* kf_last = nullptr;    // [Nl][N][ntile] kf of each tile's last state (ws_tree_perm)
     int kf_last_cap = 0;
+    // disutility per labour level, cached with the key below (aiy_ws_invalidate resets)
+    bool dis_ok = false;
+    const void* dis_L = nullptr;
+    int64_t dis_Nl = 0;
+    double dis_psi = 0, dis_eta = 0;
+    // small-grid one-launch sweep (bellman_wide_kernels.hip; aiy_ws_set_wide): used when
+    // Na <= wide_max (-1: the default bound) with `wide_S` splits of `wide_NW` waves (0: by size)
+    int wide_max = -1, wide_S = 0, wide_NW = 0, wide_SB = 0;
+    unsigned long long* wdiff = nullptr;  // device [2][2*kDiffSlots]: the set not current is zero
+    int wcur = 0;                         // the set the last wide sweep wrote
+    unsigned* wcnt = nullptr;             // device [N·ntile] per-tile arrival counters (zero)
+    size_t wcnt_cap = 0;
+    unsigned long long* wpart = nullptr;  // device [N·ntile][S][64][2] partial bests
+    size_t wpart_cap = 0;
+    bool last_wide = false;               // the last VFI sweep on this workspace was wide
+    unsigned long long* vdiff = nullptr;  // the diff slots the last VFI sweep wrote
     bool perm_ok = false;
     int* partial = nullptr;
     size_t partial_cap = 0;
@@ -163,7 +179,7 @@ struct aiy_ws {
     void free_all() {
         void* ps[] = {EV, T, T32, Dm, Dm8, Dt, Dm512, touched, best0, idx0, mom, dis, kf, partial, diff, hitcount, trace, g0, g1, g2, gi,
                       d_key, d_off, d_wr, d_mass, d_part, egm_x2, egm_y2, egm_seg, tree_perm,
-                      kf_last};
+                      kf_last, wdiff, wcnt, wpart};
         for (void* p : ps)
             if (p) (void)hipFree(p);
         free_spec();
@@ -179,6 +195,8 @@ struct aiy_ws {
         egm_seg = nullptr;
         tree_perm = nullptr; perm_cap = 0; perm_ok = false;
         kf_last = nullptr; kf_last_cap = 0;
+        wdiff = nullptr; wcnt = nullptr; wcnt_cap = 0; wpart = nullptr; wpart_cap = 0; wcur = 0;
+        last_wide = false; vdiff = nullptr; dis_ok = false;
         d_key = d_off = nullptr; d_wr = d_mass = d_part = nullptr;
         partial_cap = 0;
     }

@@ -82,12 +82,27 @@ class Workspace:
         """Records of the last tree sweep: int64 array (items, 16) = start, end (100 MHz clock),
         XCD id, superblock tests, block tests, candidates, exact evaluations, block id, then
         wave-0 shader cycles in startup+superblock tests, block tests, fine screens, exact."""
-        cap = self.N * ((self.Na + 15) // 16)
+        items = self.N * ((self.Na + 7) // 8)  # (the small-grid sweep: a record per block)
+        cap = max(self.N * ((self.Na + 15) // 16), (items + 7) // 8 * 8 * 16)
         out = np.zeros((cap, 16), np.int64)
         n = C.c_int64(0)
         check(lib().aiy_ws_trace(self._h, out.ctypes.data_as(C.c_void_p), i64(cap), C.byref(n)))
         out = out[:n.value]
         return out[out[:, 1] > 0]  # items the last sweep's geometry wrote
+
+    def trace_wide(self):
+        """Records of the last small-grid sweep (bellman_wide_kernels.hip): int64 array
+        (blocks, 64) = entry / end wall clock, XCD, wave 0's phase marks (cycles since entry:
+        table, barrier, bar, screen, all waves, published, outputs), exact evaluations, tests,
+        votes, last-arriver flag, tile, total; then per wave w at 16 + 2w: its bar and screen
+        ends."""
+        items = self.N * ((self.Na + 7) // 8)
+        cap = (items + 7) // 8 * 8 * 16 * 4
+        out = np.zeros((cap, 16), np.int64)
+        n = C.c_int64(0)
+        check(lib().aiy_ws_trace(self._h, out.ctypes.data_as(C.c_void_p), i64(cap), C.byref(n)))
+        out = out[:n.value - n.value % 4].reshape(-1, 64)
+        return out[out[:, 1] > 0]
 
     def timing(self):
         ms, n, hits = C.c_double(0), C.c_int64(0), C.c_int64(0)
@@ -113,6 +128,12 @@ class Workspace:
         """Sweeps a solve enqueues between reads of max|dv| (0/1 = one sync per sweep);
         results do not depend on it, see aiy_ws_set_speculation."""
         check(lib().aiy_ws_set_speculation(self._h, ip(max_batch)))
+
+    def set_wide(self, max_na: int = -1, splits: int = 0, waves: int = 0, states: int = 0):
+        """The small-grid one-launch sweep (aiy_ws_set_wide): used at Na <= max_na (-1: the
+        default bound, 0: never) with `splits` workgroups of `waves` waves per tile of `states`
+        states (0: by size).  Results do not depend on it."""
+        check(lib().aiy_ws_set_wide(self._h, ip(max_na), ip(splits), ip(waves), ip(states)))
 
     def set_search(self, coarse_stride=0, k_chunk=1024):
         check(lib().aiy_ws_set_search(self._h, ip(coarse_stride), ip(k_chunk)))
@@ -221,3 +242,18 @@ def _ws_labor_sweep(self, v_old, a_grid, s, P, labor_choice, r, w, beta, sigma, 
 
 
 Workspace.labor_vfi_sweep = _ws_labor_sweep
+
+
+def _ws_labor_sweeps(self, v_a, v_b, a_grid, s, P, labor_choice, r, w, beta, sigma, psi, eta,
+                     nsweeps, lin, policy_k=None, policy_l=None, policy_c=None, hint=None,
+                     diff=None, stream=None):
+    """nsweeps A3 sweeps on device from one C call (aiy_labor_vfi_sweeps_dev): ping-pong from
+    v_a (v_new ends in v_b when nsweeps is odd), sweep 1's hint `hint`, later ones lin."""
+    check(lib().aiy_labor_vfi_sweeps_dev(self._h, ptr(v_a), ptr(v_b), ptr(a_grid), ptr(s), ptr(P),
+                                         ptr(labor_choice), d(r), d(w), d(beta), d(sigma), d(psi),
+                                         d(eta), ptr(hint), i64(nsweeps), ptr(lin), ptr(policy_k),
+                                         ptr(policy_l), ptr(policy_c), ptr(diff),
+                                         stream_handle(stream)))
+
+
+Workspace.labor_vfi_sweeps = _ws_labor_sweeps

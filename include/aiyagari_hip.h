@@ -252,8 +252,16 @@ int aiy_ws_set_search(aiy_ws* ws, int coarse_stride, int k_chunk);
  * discarded, so iteration count, v_new, v_old and policies do not depend on it; memory: two
  * batches in flight — 2·max_batch + 1 value buffers and 2·max_batch policy sets per workspace. */
 int aiy_ws_set_speculation(aiy_ws* ws, int max_batch);
+/* The small-grid sweep (A1 / A3 at integer sigma in [2, 9], mode 0/1, Nz below the MFMA
+ * expectation's threshold): ONE launch per sweep — expectation, screen, merge and outputs —
+ * with a workgroup of `waves` waves (4, 8 or 16) per tile of `states` states (8, 16, 32 or 64;
+ * each wave splits the candidates into 64 / states slices) and `splits` workgroups per tile
+ * splitting the candidate range further.  Used when Na <= max_na and the variant is the default
+ * (-1) or has bit 25 set.  max_na = -1: the default bound; 0: never.  splits / waves / states =
+ * 0: chosen by size.  Results are identical to the tree sweep's for every setting. */
+int aiy_ws_set_wide(aiy_ws* ws, int max_na, int splits, int waves, int states);
 /* kernel shapes and A/B knobs (tuning only; results are identical for every value in
- * [-1, 2^25)).  VFI, bit 3 clear (default): the bound tree screen, bit 0 = 2 states per lane
+ * [-1, 2^26)).  VFI, bit 3 clear (default): the bound tree screen, bit 0 = 2 states per lane
  * (else 1), bits 1-2 = 1, 2, 4 or 8 cooperating waves per tile, bit 4 = XCD-aware tile order,
  * bit 6 / bit 11 = one-wave tiles dispatched from a per-workspace permutation that keeps each
  * XCD's tile range and deals it heaviest first / row-major with its cheapest tiles last, bit 13 =
@@ -271,7 +279,8 @@ int aiy_ws_set_speculation(aiy_ws* ws, int max_batch);
  * force the VALU / MFMA expectation.  EGM steps on this workspace (their own bits, so a VFI
  * variant never changes the EGM path): bit 18 = two launches per step even when Na <= 1024
  * (default there: one fused launch); bit 19 = no chaining in the solve loops (two launches per
- * step); bit 20 = no interp1 segment windows.  -1 (default): chosen by size — Na <= 4096:
+ * step); bit 20 = no interp1 segment windows.  Bit 25: the small-grid one-launch sweep
+ * (aiy_ws_set_wide) even with an explicit variant.  -1 (default): chosen by size — Na <= 4096:
  * 2 cooperating waves per tile (A1), 4 with bit 12 (labour); else 16 | 2048 | 1 << 16 |
  * 1 << 21 | 1 << 23 | 1 << 24 (A1), 16 | 1 << 21 (labour) and 16 | 1 << 21 (the batched
  * multi-rate solve). */
@@ -321,6 +330,17 @@ int aiy_labor_vfi_sweep_dev(aiy_ws* ws, const double* v_old, const double* a_gri
                             double eta, const int32_t* hint, double* v_new, int32_t* lin,
                             double* policy_k, double* policy_l, double* policy_c, double* diff,
                             void* stream);
+/* nsweeps A3 sweeps on device (Aiyagari_Endogenous_Labor_VFI.m:69-112 repeated, as the loop
+ * :64-122 runs them without the stop test), ping-pong from v_a as aiy_vfi_sweeps_dev: sweep 1
+ * reads v_a and writes v_b (a state with no feasible (l, a') keeps v_b's incoming value), later
+ * sweeps keep v_old there (:120); sweep 1's hint is `hint` (nullable), later ones lin.  lin and
+ * the policies hold the last sweep's; diff (nullable, device double[2]) its {max|dv|, any}. */
+int aiy_labor_vfi_sweeps_dev(aiy_ws* ws, double* v_a, double* v_b, const double* a_grid,
+                             const double* s, const double* P, const double* labor_choice,
+                             double r, double w, double beta, double sigma, double psi,
+                             double eta, const int32_t* hint, int64_t nsweeps, int32_t* lin,
+                             double* policy_k, double* policy_l, double* policy_c, double* diff,
+                             void* stream);
 int aiy_egm_step_dev(aiy_ws* ws, const double* policy_c, const double* a_grid,
                      const double* s, const double* P, double r, double w, double beta,
                      double sigma, double amin, int labor, double phi, double theta,
