@@ -184,15 +184,19 @@ def aiyagari_labor_egm(Na=400, T=10000, tol=1e-5, max_iter=1000, supply="mc", ph
 
 
 def aiyagari_vfi_overlapped(Na=400, rho=0.75, sigma_e=0.75, shocks="tauchen", T=10000, tol=1e-5,
-                            max_iter=1000, r0=0.04, max_r_iter=10, r_tol=1e-5):
-    """Aiyagari_VFI.m's computation (as `aiyagari_vfi`, supply = MC) with the bisection's
-    serial Monte-Carlo chain taken off the critical path.  Step j needs K_s(r_j) only to pick
-    the next midpoint, and both candidates warm-start from the same v_old(r_j): so while the
-    chain for r_j runs (one CU), the solves at both possible next midpoints run beside it on
-    their own streams and workspaces (device tier, one host thread each; ctypes drops the GIL),
-    and the chain's K_s selects one.  Every solve and chain is the one the sequential loop runs,
-    on the same inputs and uniform block, so r_history / k_supply / iters are identical
-    (tests/test_ge_gpu.py); the discarded solve is spare GPU work."""
+                            max_iter=1000, r0=0.04, max_r_iter=10, r_tol=1e-5, lookahead=2):
+    """Aiyagari_VFI.m's computation (as `aiyagari_vfi`, supply = MC) with the bisection run
+    speculatively ahead of its serial Monte-Carlo chains.  Step j needs K_s(r_j) only to pick
+    the next midpoint, and both candidates warm-start from the same v_old(r_j): so every solve
+    that finishes starts its own chain at once AND the solves at both of its possible next
+    midpoints, up to `lookahead` bisection levels ahead of the step still waiting for its
+    chain (each on its own stream and workspace, one host thread per call; ctypes drops the
+    GIL); a chain's K_s selects one subtree and the other is discarded.  With the small-grid
+    sweep a warm solve (~1.4 ms at Na = 400) is shorter than a chain (~2.6 ms), so the
+    critical path becomes the solves plus ONE chain instead of a chain per step.  Every
+    solve and chain is the one the sequential loop runs, on the same inputs and uniform block,
+    so r_history / k_supply / iters are identical (tests/test_ge_gpu.py); lookahead = 1 is the
+    round-1 overlap (the chain beside both next solves)."""
     import concurrent.futures as cf
 
     import torch
@@ -200,6 +204,8 @@ def aiyagari_vfi_overlapped(Na=400, rho=0.75, sigma_e=0.75, shocks="tauchen", T=
     from .sim import sim_capital_dev
     from .vfi import Workspace
 
+    if lookahead < 1:
+        raise ValueError("lookahead >= 1")
     t0 = time.perf_counter()
     cal = cb.aiyagari(Na=Na, rho=rho, sigma_e=sigma_e, shocks=shocks)
     a, s, P, N = cal["a_grid"], cal["s"], cal["P"], cal["N"]
@@ -211,83 +217,222 @@ def aiyagari_vfi_overlapped(Na=400, rho=0.75, sigma_e=0.75, shocks="tauchen", T=
     a_t, s_t, P_t = tt(a), tt(s), tt(P)
     U = tt(st.u[st.pos:])  # block j (the j-th chain's T-1 draws) = U[j(T-1) : (j+1)(T-1)]
 
-    class _Slot:
-        def __init__(self):
-            self.ws = Workspace(N, Na)
-            self.stream = torch.cuda.Stream(device=dev)
-            self.va = torch.zeros((N, Na), dtype=torch.float64, device=dev)
-            self.vb = torch.zeros_like(self.va)
-            self.idx = torch.zeros((N, Na), dtype=torch.int32, device=dev)
-            self.pk, self.pc = torch.empty_like(self.va), torch.empty_like(self.va)
-            self.v_old = None
+    timeline = []  # (kind, r, j, host start, host end) of every solve and chain (diagnostics)
 
-        def solve(self, v_init, r):
-            with torch.cuda.stream(self.stream):
-                self.va.copy_(v_init)
-                self.vb.zero_()
-                it, which = self.ws.vfi_solve(
-                    self.va, self.vb, a_t, s_t, P_t, r, cb.wage(r, cal["alpha"], cal["delta"]),
-                    cal["beta"], cal["sigma"], tol, max_iter, self.idx, self.pk, self.pc,
-                    stream=self.stream)
-                self.stream.synchronize()
-            self.v_old = self.vb if which == 0 else self.va
-            return it
+    def solve(slot, v_init, r, j=-1):
+        t_a = time.perf_counter()
+        stream = streams.get()  # (a bounded set: every stream its own hardware queue)
+        with torch.cuda.stream(stream):
+            slot.va.copy_(v_init)
+            slot.vb.zero_()
+            it, which = slot.ws.vfi_solve(
+                slot.va, slot.vb, a_t, s_t, P_t, r, cb.wage(r, cal["alpha"], cal["delta"]),
+                cal["beta"], cal["sigma"], tol, max_iter, slot.idx, slot.pk, slot.pc,
+                stream=stream)
+            stream.synchronize()
+        streams.put(stream)
+        slot.v_old = slot.vb if which == 0 else slot.va
+        timeline.append(("solve", r, j, t_a - t0, time.perf_counter() - t0, it))
+        return it
 
-    sim_ws = Workspace(N, Na)
-    sim_stream = torch.cuda.Stream(device=dev)
-    k_out = torch.zeros(1, dtype=torch.float64, device=dev)
-    k_status = torch.zeros(1, dtype=torch.int32, device=dev)
-
-    def chain(slot, j):
-        with torch.cuda.stream(sim_stream):
-            sim_capital_dev(sim_ws, slot.pk, a_t, P_t, z1 - 1, k1, U[j * (T - 1):(j + 1) * (T - 1)],
-                            k_out, k_status, stream=sim_stream)
-            sim_stream.synchronize()
-        if int(k_status.item()) != 0:
+    def chain(sim, slot, j):
+        t_a = time.perf_counter()
+        stream = streams.get()
+        with torch.cuda.stream(stream):
+            sim_capital_dev(sim.ws, slot.pk, a_t, P_t, z1 - 1, k1, U[j * (T - 1):(j + 1) * (T - 1)],
+                            sim.k, sim.status, stream=stream)
+            sim.kh.copy_(sim.k, non_blocking=True)
+            sim.sh.copy_(sim.status, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        # a chain runs ~2.7 ms: poll its event instead of a blocking synchronize (a thread
+        # parked in a synchronize slowed the other threads' launches 2-3x)
+        while not ev.query():
+            time.sleep(2e-4)
+        streams.put(stream)
+        if int(sim.sh[0]) != 0:
             raise RuntimeError("find() empty in the capital-supply chain (Aiyagari_VFI.m:106)")
-        return float(k_out.item())
+        timeline.append(("chain", None, j, t_a - t0, time.perf_counter() - t0, 0))
+        return float(sim.kh[0])
 
-    slots = [_Slot(), _Slot(), _Slot()]
-    cur = slots[0]
+    class _Node:  # bisection step j at r (bracket lo, hi before the step)
+        def __init__(self, j, lo, hi, parent):
+            self.j, self.lo, self.hi, self.parent = j, lo, hi, parent
+            self.r = (lo + hi) / 2
+            self.slot = self.it = self.Ks = None
+            self.kids = None        # (lo child, hi child) once spawned
+            self.refs = 0           # outstanding futures using this node's slot (its solve,
+            #                         its chain, its children's solves reading its v_old)
+            self.alive = True
+            self.chained = False
+
+    # solve slots and chain resources persist across calls (per device and grid): a new
+    # workspace allocates its scratch with hipMalloc / hipMemset on first use, which would
+    # synchronise the device in the middle of the speculative pipeline
+    key = (dev.index, N, Na)
+    pools = _GE_POOLS.setdefault(key, ([], []))
+    all_slots, all_sims = [], []
+    free_slots, free_sims = pools[0], pools[1]
+    # streams: as many as solves and chains can run at once (2^lookahead + 2 solves, as many
+    # chains) and no more — the runtime deals streams over its hardware queues (GPU_MAX_HW_QUEUES)
+    # and a kernel queued behind a 2.7 ms chain on a shared queue waits for it
+    import queue
+    nstreams = 2 * (2 ** lookahead + 2)
+    spool = _GE_STREAMS.setdefault(dev.index, [])
+    while len(spool) < nstreams:
+        spool.append(torch.cuda.Stream(device=dev))
+    streams = queue.Queue()
+    for x in spool[:nstreams]:
+        streams.put(x)
+
+    def get(free, pool_all, make):
+        x = free.pop() if free else make()
+        pool_all.append(x)
+        return x
+
     out = dict(r_history=[], k_supply=[], k_demand=[], iters=[])
-    r_low, r_high = -0.05, 1 / cal["beta"] - 1
-    with cf.ThreadPoolExecutor(max_workers=3) as pool:
-        it0 = cur.solve(torch.zeros((N, Na), dtype=torch.float64, device=dev), r0)
-        r = (r_low + r_high) / 2
-        # the chain at r0 (its K_s is not used by the bisection) beside the first midpoint
-        f_chain = pool.submit(chain, cur, 0)
-        nxt = slots[1]
-        it = nxt.solve(cur.v_old, r)
-        f_chain.result()
-        cur, spare = nxt, [slots[0], slots[2]]
-        for j in range(1, max_r_iter + 1):
-            last = j == max_r_iter
-            r_lo_next, r_hi_next = (r_low + r) / 2, (r + r_high) / 2  # Ks > Kd : else
-            f_chain = pool.submit(chain, cur, j)
-            if not last:
-                f_lo = pool.submit(spare[0].solve, cur.v_old, r_lo_next)
-                f_hi = pool.submit(spare[1].solve, cur.v_old, r_hi_next)
-            Ks = f_chain.result()
-            Kd = cb.capital_demand(r, cal["labor"], cal["alpha"], cal["delta"])
-            out["r_history"].append(r); out["k_supply"].append(Ks); out["k_demand"].append(Kd)
-            out["iters"].append(it)
-            if not last:
-                it_lo, it_hi = f_lo.result(), f_hi.result()
-            if last or abs(Ks - Kd) < r_tol:
-                break
-            if Ks > Kd:
-                r_high = r
-                r, it, chosen, other = r_lo_next, it_lo, spare[0], spare[1]
-            else:
-                r_low = r
-                r, it, chosen, other = r_hi_next, it_hi, spare[1], spare[0]
-            spare = [cur, other]
-            cur = chosen
+    fut = {}
+    with cf.ThreadPoolExecutor(max_workers=16) as pool:
+        root = get(free_slots, all_slots, lambda: _GESlot(N, Na, dev))
+        it0 = solve(root, torch.zeros((N, Na), dtype=torch.float64, device=dev), r0)
+        r_low, r_high = -0.05, 1 / cal["beta"] - 1
+        sim0 = get(free_sims, all_sims, lambda: _GESim(N, Na, dev))
+        fut[pool.submit(chain, sim0, root, 0)] = ("chain0", None, sim0)  # (K_s at r0 unused)
+
+        def submit_solve(node, v_init):
+            node.slot = get(free_slots, all_slots, lambda: _GESlot(N, Na, dev))
+            node.refs += 1  # (its own solve: a node killed meanwhile keeps its slot until then)
+            fut[pool.submit(solve, node.slot, v_init, node.r, node.j)] = ("solve", node, None)
+
+        def spawn(node):  # both next midpoints of a solved node, from its v_old
+            node.kids = (_Node(node.j + 1, node.lo, node.r, node),
+                         _Node(node.j + 1, node.r, node.hi, node))
+            for kid in node.kids:
+                node.refs += 1
+                submit_solve(kid, node.slot.v_old)
+
+        def release(node):  # the slot back to the pool when nothing reads it any more
+            if node.slot is not None and node.refs == 0 and (not node.alive or node.j < cur.j):
+                free_slots.append(node.slot)
+                node.slot = None
+
+        def kill(node):
+            if node is None:
+                return
+            node.alive = False
+            release(node)
+            if node.kids:
+                for kid in node.kids:
+                    kill(kid)
+
+        def advance(node):  # a solved live node: its chain, and its children within the window
+            if not node.alive or node.slot is None or node.it is None:
+                return
+            if not node.chained:
+                node.chained = True
+                node.refs += 1
+                sim = get(free_sims, all_sims, lambda: _GESim(N, Na, dev))
+                fut[pool.submit(chain, sim, node.slot, node.j)] = ("chain", node, sim)
+            if node.kids is None and node.j < max_r_iter and node.j - cur.j < lookahead:
+                spawn(node)
+            elif node.kids:
+                for kid in node.kids:
+                    advance(kid)
+
+        cur = _Node(1, r_low, r_high, None)
+        submit_solve(cur, root.v_old)
+        done = False
+        while fut and not done:
+            finished, _ = cf.wait(list(fut), return_when=cf.FIRST_COMPLETED)
+            for f in finished:
+                kind, node, sim = fut.pop(f)
+                res = f.result()
+                if sim is not None:
+                    free_sims.append(sim)
+                if kind == "chain0":
+                    continue
+                if kind == "solve":
+                    node.it = res
+                    node.refs -= 1
+                    if node.parent is not None:
+                        node.parent.refs -= 1
+                        release(node.parent)
+                    if not node.alive:
+                        release(node)
+                        continue
+                    advance(node)
+                    continue
+                node.Ks = res  # a chain
+                node.refs -= 1
+                release(node)
+            # decisions: the current step's chain, then (already chained) the steps after it
+            while not done and cur.Ks is not None:
+                Kd = cb.capital_demand(cur.r, cal["labor"], cal["alpha"], cal["delta"])
+                out["r_history"].append(cur.r); out["k_supply"].append(cur.Ks)
+                out["k_demand"].append(Kd); out["iters"].append(cur.it)
+                if cur.j == max_r_iter or abs(cur.Ks - Kd) < r_tol:
+                    done = True
+                    break
+                nxt, other = (cur.kids[0], cur.kids[1]) if cur.Ks > Kd else (cur.kids[1], cur.kids[0])
+                kill(other)
+                prev, cur = cur, nxt
+                release(prev)
+                advance(cur)
+        for f in list(fut):  # speculative work still running: let it finish before teardown
+            f.result()
     out["r"] = out["r_history"][-1]
     out["iters"] = [it0] + out["iters"]
     out["wall_s"] = time.perf_counter() - t0
     out["cal"] = cal
-    for sl in slots:
-        sl.ws.close()
-    sim_ws.close()
+    out["lookahead"] = lookahead
+    out["solves"] = len(all_slots)
+    out["timeline"] = sorted(timeline, key=lambda e: e[3])
+    free_slots[:] = list({id(x): x for x in free_slots + all_slots}.values())  # all back
+    free_sims[:] = list({id(x): x for x in free_sims + all_sims}.values())
     return out
+
+
+class _GESlot:
+    """One speculative solve's resources (aiyagari_vfi_overlapped): workspace and buffers;
+    state only — the calls that use it pass every input explicitly (a slot outlives a call)."""
+
+    def __init__(self, N, Na, dev):
+        import torch
+
+        from .vfi import Workspace
+        self.ws = Workspace(N, Na)
+        self.va = torch.zeros((N, Na), dtype=torch.float64, device=dev)
+        self.vb = torch.zeros_like(self.va)
+        self.idx = torch.zeros((N, Na), dtype=torch.int32, device=dev)
+        self.pk, self.pc = torch.empty_like(self.va), torch.empty_like(self.va)
+        self.v_old = None
+        # the zero fills above are on the creating thread's current stream: done before this
+        # slot's own stream touches the buffers (no cross-stream order otherwise)
+        torch.cuda.current_stream(dev).synchronize()
+
+
+class _GESim:
+    """One Monte-Carlo chain's resources: workspace and outputs."""
+
+    def __init__(self, N, Na, dev):
+        import torch
+
+        from .vfi import Workspace
+        self.ws = Workspace(N, Na)
+        self.k = torch.zeros(1, dtype=torch.float64, device=dev)
+        self.status = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.kh = torch.zeros(1, dtype=torch.float64).pin_memory()  # host copies (pinned)
+        self.sh = torch.zeros(1, dtype=torch.int32).pin_memory()
+        torch.cuda.current_stream(dev).synchronize()
+
+
+_GE_POOLS = {}  # (device, N, Na) -> (solve slots, chain resources) of aiyagari_vfi_overlapped
+_GE_STREAMS = {}  # device -> the driver's streams
+
+
+def release_pools():
+    """Free the cached workspaces of aiyagari_vfi_overlapped."""
+    for slots, sims in _GE_POOLS.values():
+        for x in slots + sims:
+            x.ws.close()
+    _GE_POOLS.clear()

@@ -28,6 +28,10 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
+# hardware queues per process (HIP's default is 4): the GE drivers run speculative solves and
+# 2.7 ms Monte-Carlo chains on their own streams, and a stream sharing a queue with a chain
+# waits behind it (ge.aiyagari_vfi_overlapped).  Set before the HIP runtime starts.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
 PEAK_FP64_TFLOPS = 78.6   # MI355X fp64 vector (= fp64 matrix) peak, datasheet
 FLOPS_PER_CANDIDATE = 8  # sub, mul, mul, div, sub, mul, add, max
@@ -108,7 +112,9 @@ def ge_wall(pkg, threads):
     return {"workload": "Aiyagari_VFI.m defaults (configs[0]): initial VFI + 10-step bisection + MC",
             "r_gpu": out["r"], "r_cpu": H["r_final"], "identical_trace": out["r_history"] == H["r"],
             "sweeps": int(sum(out["iters"])), "wall_s_gpu": gpu_s, "wall_s_cpu": cpu_s,
-            "driver": "ge.aiyagari_vfi_overlapped (MC chain beside both next solves)",
+            "driver": f"ge.aiyagari_vfi_overlapped (solves speculated {out['lookahead']} "
+                      f"bisection level(s) ahead of the pending MC chain; {out['solves']} solve "
+                      f"slots)",
             "wall_s_gpu_sequential": seq_s, "sequential_trace_equal": seq["r_history"] == out["r_history"]
             and seq["k_supply"] == out["k_supply"] and seq["iters"] == out["iters"],
             "cpu_cores": threads, "wall_s_cpu_1core": cpu[1],

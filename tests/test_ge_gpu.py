@@ -34,9 +34,10 @@ def test_ge_vfi_overlapped_matches_golden_trace(pkg, gpu, golden):
     # a shorter bisection and a tighter grid: still identical to the sequential driver
     kw = dict(Na=300, T=3000)
     seq = pkg.ge.aiyagari_vfi(**kw)
-    ovl = pkg.ge.aiyagari_vfi_overlapped(**kw)
-    for key in ("r_history", "k_supply", "k_demand", "iters", "r"):
-        assert ovl[key] == seq[key], key
+    for la in (1, 2, 3):  # speculation depth (levels solved ahead of the pending chain)
+        ovl = pkg.ge.aiyagari_vfi_overlapped(lookahead=la, **kw)
+        for key in ("r_history", "k_supply", "k_demand", "iters", "r"):
+            assert ovl[key] == seq[key], (la, key)
 
 
 def _oracle_ge(cal, solve_at_factory, policy_of, vfi_layout, T=10000):
