@@ -16,6 +16,10 @@ namespace aiy {
 // ---------------------------------------------------------------- errors (host)
 void set_error(const char* fmt, ...);
 int fail(int code, const char* fmt, ...);
+// Wait for an event without parking the thread in the runtime: hipEventQuery in a loop (spin,
+// then yield).  Several host threads each blocked in hipEventSynchronize slowed one another's
+// launches 2-4x (the GE driver's concurrent solves, tools/ge_concurrency.py); polling does not.
+int wait_event(hipEvent_t ev);
 
 #define AIY_HIP(call)                                                                  \
     do {                                                                               \

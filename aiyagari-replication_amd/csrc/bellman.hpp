@@ -101,8 +101,11 @@ inline size_t bell_wide_lds(int Na, int S, int NW) {
 // (measured slower than the window alone, tools/wide_tune.py)
 constexpr int kWideBatch = 1, kWideClimb = 2;
 constexpr int kWideMaxNl = 16;  // labour levels the small-grid sweep holds in registers
+// a workgroup asking for this much LDS has its CU to itself (160 KiB per CU on gfx950)
+constexpr size_t kExclusiveLds = 88 * 1024;
 int launch_bell_wide(const BellArgs& A, int S, int NW, int SB, unsigned long long* old_slots,
-                     unsigned* cnt, unsigned long long* part, int flags, hipStream_t st);
+                     unsigned* cnt, unsigned long long* part, int flags, size_t min_lds,
+                     hipStream_t st);
 int launch_bell_ev_mfma(const BellArgs& A, hipStream_t st);
 int launch_bell_table(const BellArgs& A, hipStream_t st);
 int launch_bell_kf(const BellArgs& A, hipStream_t st);

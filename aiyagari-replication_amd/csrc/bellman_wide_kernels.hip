@@ -461,11 +461,12 @@ __global__ __launch_bounds__(64 * NW) void bell_wide_kernel(
 // ------------------------------------------------------------------------------ launcher
 template <int NP, bool LAB, int NW>
 static void wide_geo(const BellArgs& A, int S, int lsb, unsigned long long* old_slots,
-                     unsigned* cnt, unsigned long long* part, int flags, hipStream_t st) {
+                     unsigned* cnt, unsigned long long* part, int flags, size_t min_lds,
+                     hipStream_t st) {
     const int ntile = (A.Na + (1 << lsb) - 1) >> lsb;
     const int items = A.N * ntile;
     const int grid = ((items + 7) / 8) * 8 * S;
-    const size_t lds = bell_wide_lds(A.Na, S, NW);
+    const size_t lds = std::max(bell_wide_lds(A.Na, S, NW), min_lds);
     static bool big = false;  // dynamic LDS past 64 KiB needs the attribute (idempotent)
     if (!big && lds > 64 * 1024) {
         (void)hipFuncSetAttribute((const void*)bell_wide_kernel<NP, LAB, NW>,
@@ -478,16 +479,18 @@ static void wide_geo(const BellArgs& A, int S, int lsb, unsigned long long* old_
 }
 template <int NP, bool LAB>
 static void wide_w(const BellArgs& A, int S, int NW, int lsb, unsigned long long* old_slots,
-                   unsigned* cnt, unsigned long long* part, int flags, hipStream_t st) {
+                   unsigned* cnt, unsigned long long* part, int flags, size_t min_lds,
+                   hipStream_t st) {
     switch (NW) {
-        case 4: wide_geo<NP, LAB, 4>(A, S, lsb, old_slots, cnt, part, flags, st); break;
-        case 8: wide_geo<NP, LAB, 8>(A, S, lsb, old_slots, cnt, part, flags, st); break;
-        default: wide_geo<NP, LAB, 16>(A, S, lsb, old_slots, cnt, part, flags, st); break;
+        case 4: wide_geo<NP, LAB, 4>(A, S, lsb, old_slots, cnt, part, flags, min_lds, st); break;
+        case 8: wide_geo<NP, LAB, 8>(A, S, lsb, old_slots, cnt, part, flags, min_lds, st); break;
+        default: wide_geo<NP, LAB, 16>(A, S, lsb, old_slots, cnt, part, flags, min_lds, st); break;
     }
 }
 
 int launch_bell_wide(const BellArgs& A, int S, int NW, int SB, unsigned long long* old_slots,
-                     unsigned* cnt, unsigned long long* part, int flags, hipStream_t st) {
+                     unsigned* cnt, unsigned long long* part, int flags, size_t min_lds,
+                     hipStream_t st) {
     if (A.np < 1 || A.np > 8) return fail(AIY_BAD_ARG, "wide sweep needs integer sigma in [2, 9]");
     if (A.C > 1) return fail(AIY_BAD_ARG, "wide sweep: one candidate rate");
     if (S < 1 || S > kWideMaxSplits || (NW != 4 && NW != 8 && NW != 16) ||
@@ -499,8 +502,8 @@ int launch_bell_wide(const BellArgs& A, int S, int NW, int SB, unsigned long lon
         return fail(AIY_BAD_SHAPE, "wide sweep: the candidate slice does not fit in LDS");
 #define AIY_WCASE(n)                                                               \
     case n:                                                                        \
-        if (A.labor) wide_w<n, true>(A, S, NW, lsb, old_slots, cnt, part, flags, st); \
-        else wide_w<n, false>(A, S, NW, lsb, old_slots, cnt, part, flags, st);        \
+        if (A.labor) wide_w<n, true>(A, S, NW, lsb, old_slots, cnt, part, flags, min_lds, st); \
+        else wide_w<n, false>(A, S, NW, lsb, old_slots, cnt, part, flags, min_lds, st);        \
         break;
     switch (A.np) {
         AIY_WCASE(1) AIY_WCASE(2) AIY_WCASE(3) AIY_WCASE(4) AIY_WCASE(5) AIY_WCASE(6)

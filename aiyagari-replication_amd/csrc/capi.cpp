@@ -9,12 +9,25 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "aiy_common.hpp"
 #include "ws.hpp"
 
 namespace aiy {
+
+int wait_event(hipEvent_t ev) {
+    for (int spin = 0;; ++spin) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e == hipSuccess) return AIY_OK;
+        if (e != hipErrorNotReady) {
+            (void)hipGetLastError();
+            return fail(AIY_HIP_ERROR, "hipEventQuery failed: %s", hipGetErrorString(e));
+        }
+        if (spin > 256) std::this_thread::yield();
+    }
+}
 
 static thread_local std::string g_err;
 
@@ -409,7 +422,8 @@ static int bell_sweep_wide(aiy_ws* ws, BellArgs& A, int S, int NW, int SB, hipSt
     }
     const char* fl = getenv("AIY_WIDE_FLAGS");  // (A/B tooling: tools/wide_tune.py)
     AIY_TRY(ws_dispatch_arm(ws));
-    const int rc = launch_bell_wide(A, S, NW, SB, cur, ws->wcnt, ws->wpart, fl ? atoi(fl) : 0, st);
+    const int rc = launch_bell_wide(A, S, NW, SB, cur, ws->wcnt, ws->wpart, fl ? atoi(fl) : 0,
+                                    ws->cu_exclusive ? kExclusiveLds : 0, st);
     ws_dispatch_commit(ws);
     AIY_TRY(rc);
     ws->wcur ^= 1;
@@ -577,7 +591,7 @@ static int bell_solve_spec(aiy_ws* ws, BellCall c, double* v_a, double* v_b, dou
     while (nq > 0) {
         if (nq < 2 && enq < max_iter) AIY_TRY(enqueue());
         const Batch b = q[0];
-        AIY_HIP(hipEventSynchronize(ws->spec_ev[b.hb]));
+        AIY_TRY(wait_event(ws->spec_ev[b.hb]));
         const unsigned long long* hs = ws->spec_hdiff + (size_t)b.hb * 2 * D;
         for (int64_t t = 0; t < b.m; ++t) {
             const unsigned long long* h = hs + 2 * ((b.s0 + 1 + t) % D);
@@ -908,6 +922,12 @@ int aiy_ws_set_wide(aiy_ws* ws, int max_na, int splits, int waves, int states) {
     ws->wide_S = splits;
     ws->wide_NW = waves;
     ws->wide_SB = states;
+    return AIY_OK;
+}
+
+int aiy_ws_set_cu_exclusive(aiy_ws* ws, int on) {
+    if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
+    ws->cu_exclusive = on != 0;
     return AIY_OK;
 }
 

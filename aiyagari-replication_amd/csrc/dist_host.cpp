@@ -177,7 +177,7 @@ int dist_stationary_dev(aiy_ws* ws, const double* lam0, const int* idx, const do
     while (nq > 0) {
         if (nq < 2 && enq < max_iter) AIY_TRY(enqueue());  // keep the device busy while reading
         const Batch b = q[0];
-        AIY_HIP(hipEventSynchronize(ws->dist_ev[b.hb]));
+        AIY_TRY(wait_event(ws->dist_ev[b.hb]));
         const unsigned long long* hs = ws->dist_hslots + (size_t)b.hb * R * SW;
         for (int64_t t = 0; t < b.m; ++t) {
             const double d = fold_slots_host(hs + (size_t)((b.s0 + 1 + t) % R) * SW);

@@ -206,7 +206,7 @@ static int egm_solve_spec(aiy_ws* ws, const EgmArgs& A0, double* c0, double tol,
     while (nq > 0) {
         if (nq < 2 && enq < max_iter) AIY_TRY(enqueue());  // keep the device busy while reading
         const Batch b = q[0];
-        AIY_HIP(hipEventSynchronize(ws->egm_ev[b.hb]));
+        AIY_TRY(wait_event(ws->egm_ev[b.hb]));
         const unsigned long long* hs = ws->egm_hslots + (size_t)b.hb * R * SW;
         for (int64_t t = 0; t < b.m; ++t) {
             const unsigned long long* h = hs + (size_t)((b.s0 + 1 + t) % R) * SW;

@@ -286,18 +286,274 @@ __global__ __launch_bounds__(256) void sim_chain_kernel(SimArgs A0) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// A chain's workgroup asks for at least this much LDS so that no other workgroup that uses LDS
+// (a solve's sweep blocks in the GE driver) shares its CU: a co-resident block competes with
+// the chain's serial wave for issue slots and becomes the straggler of its sweep
+// (tools/ge_concurrency.py: 2 solves + 2 chains on shared CUs ran the solves 2.7x slower).
+constexpr int kSimExclusiveLds = 88 * 1024;
+
+// Two-wave pipeline (N <= 8, 64 <= Na, Na + 64 <= SS).  One wave running the whole step is
+// bound by its instruction issue (~4 cycles per instruction; ~100 per step, half of them scalar
+// bookkeeping of the state chain and the window), so the k-independent half moves to a second
+// wave: wave 1 walks the state chain z_t = find(u_t < cumsum(P(z_{t-1},:)), 1) one chunk ahead
+// (lane 8z + m holds cumsum(P(z,:))(m): one ballot per step) and leaves per step the byte offset
+// of row z_t's policy record; wave 0 runs only the k recurrence, ~56 instructions per step:
+//   * tables at fixed strides (SS doubles): X0 = a_i (clamped), H = a_{i+1} - a_i, and per row
+//     {y_i, y_{i+1} - y_i} — the same subtractions, so t = (k - a_i) / h and k' = y_i + t·dy
+//     are sim_chain_kernel's values; one address + immediate offsets per window load;
+//   * the window of step t+1 (w0 from step t's segment, row from z_{t+1}) is loaded while step t
+//     divides; 32-step unrolled blocks read z offsets with constant lane indices;
+//   * every exception (window miss -> 64-ary search) is one branch not taken on the common path.
+// w0 stays in [0, Na - 64], so no lane reads past the grid.  A9 chain at Na = 400: 2.54 ->
+// 1.58 ms per 10^4 steps, bit-identical (profiles/r05_g30_sim_chain_pipe_ab.txt; the
+// reciprocal-table quotient of fastdiv_check.c measured slower, r05_g31).
+template <int SS, bool PATH>
+__global__ __launch_bounds__(128) void sim_chain_pipe_kernel(SimArgs A0) {
+    SimArgs A = A0;
+    if (A0.C > 1) {
+        A.pol += blockIdx.x * A0.pcs;
+        A.U += blockIdx.x * A0.ucs;
+        A.out += blockIdx.x;
+        A.status += blockIdx.x;
+    }
+    extern __shared__ double lds[];  // X0[SS] | H[SS] | Y[N][SS][2] = {y_i, y_{i+1} - y_i}
+    __shared__ int zoff[2][kSimChunk];
+    __shared__ int stop_at;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int N = A.N, Na = A.Na, T = A.T;
+    double* X0 = lds;
+    double* H = lds + SS;
+    double* Y = lds + 2 * SS;
+    for (int i = tid; i < SS; i += 128) {
+        const double x0 = A.a[min(i, Na - 1)], x1 = A.a[min(i + 1, Na - 1)];
+        X0[i] = x0;
+        H[i] = x1 - x0;
+    }
+    for (int q = tid; q < N * SS; q += 128) {
+        const int zz = q / SS, i = q - zz * SS;
+        const double* row = A.pol + (size_t)zz * A.zs;
+        const double y0 = i < Na ? row[(size_t)i * A.as] : 0.0;
+        const double y1 = i + 1 < Na ? row[(size_t)(i + 1) * A.as] : 0.0;
+        Y[2 * (size_t)q] = y0;
+        Y[2 * (size_t)q + 1] = y1 - y0;
+    }
+    if (tid == 0) stop_at = T;
+    // wave 1: lane 8z + m holds cumsum(P(z,:))(m) (sequential sums, as cumsum), -inf elsewhere
+    double csl = -__builtin_inf();
+    if (wave == 1 && (lane >> 3) < N && (lane & 7) < N) {
+        const int zz = lane >> 3, m = lane & 7;
+        double acc = 0.0;
+        for (int q = 0; q <= m; ++q) acc = acc + A.P[zz * N + q];
+        csl = acc;
+    }
+    int zc = A.z1;
+    bool walking = true;
+    // steps c0 .. c0 + cn - 1 of the state chain -> out[i] = byte offset of row z_{c0+i} in Y
+    auto walk = [&](int c0, int cn, int* out) {
+        for (int i0 = 0; i0 < cn && walking; i0 += 64) {
+            const double Uv = i0 + lane < cn ? A.U[c0 + i0 + lane - 1] : 0.0;
+            int ov = 0;
+            const int jn = min(64, cn - i0);
+            for (int j = 0; j < jn; ++j) {
+                const double u = readlane_d(Uv, j);
+                const unsigned row = (unsigned)(__ballot(u < csl) >> (8 * zc)) & 0xFFu;
+                if (row == 0) {  // the reference's find() would return empty and error
+                    if (lane == 0) stop_at = c0 + i0 + j;
+                    walking = false;
+                    break;
+                }
+                zc = __builtin_ctz(row);
+                if (lane == j) ov = zc * (SS * 16);
+            }
+            if (i0 + lane < cn) out[i0 + lane] = ov;
+        }
+    };
+    if (wave == 1 && T > 1) walk(1, min(kSimChunk, T - 1), zoff[0]);
+    __syncthreads();
+    const int wmax = Na - 64;
+    double k = A.k1;
+    double sum = k;
+    int w0 = 0;
+    int status = 0;
+    double kbuf = k;
+    int zbuf = A.z1;
+    int t_last = 0;
+    double x0 = 0.0, h = 0.0, y0 = 0.0, dy = 0.0;
+    bool primed = false;
+    auto ldwin = [&](int w, int zo) {
+        const int p = w + lane;
+        x0 = X0[p];
+        h = H[p];
+        const double2 yy = *reinterpret_cast<const double2*>(
+            reinterpret_cast<const char*>(Y) + zo + 16 * p);
+        y0 = yy.x;
+        dy = yy.y;
+    };
+    auto step = [&](int t, int zo, int zo1) __attribute__((always_inline)) {
+        if (__builtin_expect(!primed, 0)) {
+            ldwin(w0, zo);
+            primed = true;
+        }
+        const int c = __popcll(__ballot(x0 <= k));
+        int sl = min(c - 1, Na - 2 - w0);
+        sl = sl < 0 ? 0 : sl;
+        int seg = w0 + sl;
+        const int hit = ((c > 0) | (w0 == 0)) & ((c < 64) | (w0 == wmax));
+        int w0n = seg - 31;
+        w0n = w0n < 0 ? 0 : (w0n > wmax ? wmax : w0n);
+        const double d = k - x0;
+        const double ch = h, cy0 = y0, cdy = dy;
+        ldwin(w0n, zo1);  // step t+1's window, issued before this step's division
+        __builtin_amdgcn_sched_barrier(0);
+        const double kn = cy0 + (d / ch) * cdy;
+        const double kw = readlane_d(kn, sl);
+        if (__builtin_expect(!hit, 0)) {  // the window missed k: 64-ary search
+            int lo = 0, hi = Na;
+            while (hi - lo > 64) {
+                int stp = (hi - lo + 63) / 64;
+                int pp = lo + lane * stp;
+                bool le = pp < hi && X0[pp] <= k;
+                int cc = __popcll(__ballot(le));
+                if (cc == 0) {
+                    hi = lo;
+                    break;
+                }
+                lo = lo + (cc - 1) * stp;
+                hi = min(lo + stp, hi);
+            }
+            int pp = lo + lane;
+            int cc = __popcll(__ballot(pp < hi && X0[pp] <= k));
+            seg = lo + cc - 1;
+            seg = seg < 0 ? 0 : (seg > Na - 2 ? Na - 2 : seg);
+            w0n = seg - 31;
+            w0n = w0n < 0 ? 0 : (w0n > wmax ? wmax : w0n);
+            primed = false;
+            const double T0 = (k - X0[seg]) / H[seg];
+            const double* Yz = reinterpret_cast<const double*>(
+                reinterpret_cast<const char*>(Y) + zo) + 2 * seg;
+            k = Yz[0] + T0 * Yz[1];
+        } else {
+            k = kw;
+        }
+        w0 = w0n;
+        sum += k;
+        if constexpr (PATH) {
+            if (lane == (t & 63)) {
+                kbuf = k;
+                zbuf = zo / (SS * 16);
+            }
+            t_last = t;
+            if ((t & 63) == 63) {
+                const int base = t & ~63;
+                if (A.sim_k) A.sim_k[base + lane] = kbuf;
+                if (A.sim_z) A.sim_z[base + lane] = zbuf;
+            }
+        }
+    };
+    int b = 0;
+    for (int c0 = 1; c0 < T; c0 += kSimChunk, b ^= 1) {
+        const int cn = min(kSimChunk, T - c0);
+        const int lim = min(cn, stop_at - c0);  // steps of this chunk before a find() failure
+        if (wave == 1 && walking && c0 + cn < T)
+            walk(c0 + cn, min(kSimChunk, T - c0 - cn), zoff[b ^ 1]);
+        if (wave == 0) {
+            const int* zb = zoff[b];
+            int i = 0;
+            for (; i + 64 <= lim; i += 64) {
+                const int Zv = zb[i + lane];
+                const int Zn = i + 64 + lane < lim ? zb[i + 64 + lane] : 0;
+#pragma unroll
+                for (int j = 0; j < 32; ++j)
+                    step(c0 + i + j, __builtin_amdgcn_readlane(Zv, j),
+                         __builtin_amdgcn_readlane(Zv, j + 1));
+#pragma unroll
+                for (int j = 32; j < 64; ++j)
+                    step(c0 + i + j, __builtin_amdgcn_readlane(Zv, j),
+                         j < 63 ? __builtin_amdgcn_readlane(Zv, j + 1)
+                                : __builtin_amdgcn_readlane(Zn, 0));
+            }
+            if (i < lim) {
+                const int Zv = zb[i + lane];
+                const int Zn = i + 64 + lane < lim ? zb[i + 64 + lane] : 0;
+                for (int j = 0; i + j < lim; ++j)
+                    step(c0 + i + j, __builtin_amdgcn_readlane(Zv, j),
+                         j < 63 ? __builtin_amdgcn_readlane(Zv, j + 1)
+                                : __builtin_amdgcn_readlane(Zn, 0));
+            }
+            primed = false;  // the last prefetch read a placeholder row
+            if (lim < cn) status = 1;
+        }
+        __syncthreads();
+        if (lim < cn) break;
+    }
+    if (wave == 0) {
+        if (PATH && T > 1 && (t_last & 63) != 63) {
+            const int base = t_last & ~63;
+            if (base + lane <= t_last) {
+                if (A.sim_k) A.sim_k[base + lane] = kbuf;
+                if (A.sim_z) A.sim_z[base + lane] = zbuf;
+            }
+        }
+        if (PATH && T == 1 && lane == 0) {
+            if (A.sim_k) A.sim_k[0] = k;
+            if (A.sim_z) A.sim_z[0] = zbuf;
+        }
+        if (lane == 0) {
+            A.out[0] = sum / (double)A.T;
+            A.status[0] = status;
+        }
+    }
+}
+
+// the two-wave chain; AIY_BAD_SHAPE when it does not apply (N > 8, Na < 64, tables past LDS)
+int launch_sim_chain_pipe(const SimArgs& A, hipStream_t st) {
+    if (A.N < 1 || A.N > 8 || A.Na < 64) return fail(AIY_BAD_SHAPE, "pipe chain: N <= 8, Na >= 64");
+    const int S = A.Na + 64;
+    const int SS = S <= 512 ? 512 : (S <= 1024 && A.N <= 7 ? 1024 : 0);
+    if (!SS) return fail(AIY_BAD_SHAPE, "pipe chain tables exceed LDS");
+    const size_t bytes = std::max(sizeof(double) * (size_t)(2 + 2 * A.N) * SS,
+                                  (size_t)kSimExclusiveLds);
+    const int g = std::max(A.C, 1);
+    const bool path = A.sim_k || A.sim_z;
+#define AIY_PIPE(SS_, PA_)                                                                         \
+    do {                                                                                           \
+        AIY_HIP(hipFuncSetAttribute((const void*)sim_chain_pipe_kernel<SS_, PA_>,                  \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));      \
+        sim_chain_pipe_kernel<SS_, PA_><<<g, 128, bytes, st>>>(A);                                 \
+    } while (0)
+    if (SS == 512) {
+        if (path) AIY_PIPE(512, true);
+        else AIY_PIPE(512, false);
+    } else {
+        if (path) AIY_PIPE(1024, true);
+        else AIY_PIPE(1024, false);
+    }
+#undef AIY_PIPE
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
+}
+
 int launch_sim_capital(const SimArgs& A, hipStream_t st) {
     if (A.N > 16 || A.N < 1) return fail(AIY_BAD_SHAPE, "simulation supports 1 <= N <= 16");
     const long long need = (long long)A.Na * (A.N + 1);
+    if (A.N <= 8 && A.Na >= 64 && (A.Na + 64 <= 512 || (A.Na + 64 <= 1024 && A.N <= 7)))
+        return launch_sim_chain_pipe(A, st);
     if (A.N <= 15) {
         const long long need_pad = (long long)(A.Na + 64) * (A.N + 1);
         const bool path = A.sim_k || A.sim_z;
+        const int g = std::max(A.C, 1);
         if (need_pad <= kSimChainLdsMax) {
-            if (path) sim_chain_kernel<true, true><<<std::max(A.C, 1), 256, sizeof(double) * need_pad, st>>>(A);
-            else sim_chain_kernel<true, false><<<std::max(A.C, 1), 256, sizeof(double) * need_pad, st>>>(A);
+            const size_t bytes = std::max(sizeof(double) * (size_t)need_pad, (size_t)kSimExclusiveLds);
+            const void* fn = path ? (const void*)sim_chain_kernel<true, true>
+                                  : (const void*)sim_chain_kernel<true, false>;
+            AIY_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+            if (path) sim_chain_kernel<true, true><<<g, 256, bytes, st>>>(A);
+            else sim_chain_kernel<true, false><<<g, 256, bytes, st>>>(A);
         } else {
-            if (path) sim_chain_kernel<false, true><<<std::max(A.C, 1), 256, 0, st>>>(A);
-            else sim_chain_kernel<false, false><<<std::max(A.C, 1), 256, 0, st>>>(A);
+            if (path) sim_chain_kernel<false, true><<<g, 256, 0, st>>>(A);
+            else sim_chain_kernel<false, false><<<g, 256, 0, st>>>(A);
         }
     } else if (need <= kSimLdsMax) {
         sim_capital_kernel<true><<<std::max(A.C, 1), 64, sizeof(double) * need, st>>>(A);

@@ -49,6 +49,7 @@ struct aiy_ws {
     // small-grid one-launch sweep (bellman_wide_kernels.hip; aiy_ws_set_wide): used when
     // Na <= wide_max (-1: the default bound) with `wide_S` splits of `wide_NW` waves (0: by size)
     int wide_max = -1, wide_S = 0, wide_NW = 0, wide_SB = 0;
+    bool cu_exclusive = false;  // aiy_ws_set_cu_exclusive
     unsigned long long* wdiff = nullptr;  // device [2][2*kDiffSlots]: the set not current is zero
     int wcur = 0;                         // the set the last wide sweep wrote
     unsigned* wcnt = nullptr;             // device [N·ntile] per-tile arrival counters (zero)

@@ -184,19 +184,20 @@ def aiyagari_labor_egm(Na=400, T=10000, tol=1e-5, max_iter=1000, supply="mc", ph
 
 
 def aiyagari_vfi_overlapped(Na=400, rho=0.75, sigma_e=0.75, shocks="tauchen", T=10000, tol=1e-5,
-                            max_iter=1000, r0=0.04, max_r_iter=10, r_tol=1e-5, lookahead=2):
+                            max_iter=1000, r0=0.04, max_r_iter=10, r_tol=1e-5, lookahead=1):
     """Aiyagari_VFI.m's computation (as `aiyagari_vfi`, supply = MC) with the bisection run
     speculatively ahead of its serial Monte-Carlo chains.  Step j needs K_s(r_j) only to pick
     the next midpoint, and both candidates warm-start from the same v_old(r_j): so every solve
     that finishes starts its own chain at once AND the solves at both of its possible next
     midpoints, up to `lookahead` bisection levels ahead of the step still waiting for its
     chain (each on its own stream and workspace, one host thread per call; ctypes drops the
-    GIL); a chain's K_s selects one subtree and the other is discarded.  With the small-grid
-    sweep a warm solve (~1.4 ms at Na = 400) is shorter than a chain (~2.6 ms), so the
-    critical path becomes the solves plus ONE chain instead of a chain per step.  Every
-    solve and chain is the one the sequential loop runs, on the same inputs and uniform block,
-    so r_history / k_supply / iters are identical (tests/test_ge_gpu.py); lookahead = 1 is the
-    round-1 overlap (the chain beside both next solves)."""
+    GIL); a chain's K_s selects one subtree and the other is discarded.  Every solve and chain
+    is the one the sequential loop runs, on the same inputs and uniform block, so r_history /
+    k_supply / iters are identical (tests/test_ge_gpu.py).  Default lookahead = 1 (the chain
+    of step j beside both solves of step j+1): with the two-wave chain (~1.6 ms per 10^4 steps)
+    and a warm small-grid solve (~1.5 ms) about equal, one level keeps the critical path at one
+    of them per step, and deeper trees run 4+ solves at once, which this runtime serves slower
+    than 2 (tools/ge_concurrency.py, profiles/r05_g32_ge_lookahead.txt)."""
     import concurrent.futures as cf
 
     import torch
@@ -229,7 +230,7 @@ def aiyagari_vfi_overlapped(Na=400, rho=0.75, sigma_e=0.75, shocks="tauchen", T=
                 slot.va, slot.vb, a_t, s_t, P_t, r, cb.wage(r, cal["alpha"], cal["delta"]),
                 cal["beta"], cal["sigma"], tol, max_iter, slot.idx, slot.pk, slot.pc,
                 stream=stream)
-            stream.synchronize()
+        _wait_polled(stream)
         streams.put(stream)
         slot.v_old = slot.vb if which == 0 else slot.va
         timeline.append(("solve", r, j, t_a - t0, time.perf_counter() - t0, it))
@@ -243,12 +244,9 @@ def aiyagari_vfi_overlapped(Na=400, rho=0.75, sigma_e=0.75, shocks="tauchen", T=
                             sim.k, sim.status, stream=stream)
             sim.kh.copy_(sim.k, non_blocking=True)
             sim.sh.copy_(sim.status, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(stream)
-        # a chain runs ~2.7 ms: poll its event instead of a blocking synchronize (a thread
+        # a chain runs ~2.5 ms: poll its event instead of a blocking synchronize (a thread
         # parked in a synchronize slowed the other threads' launches 2-3x)
-        while not ev.query():
-            time.sleep(2e-4)
+        _wait_polled(stream, nap=2e-4)
         streams.put(stream)
         if int(sim.sh[0]) != 0:
             raise RuntimeError("find() empty in the capital-supply chain (Aiyagari_VFI.m:106)")
@@ -390,6 +388,17 @@ def aiyagari_vfi_overlapped(Na=400, rho=0.75, sigma_e=0.75, shocks="tauchen", T=
     free_slots[:] = list({id(x): x for x in free_slots + all_slots}.values())  # all back
     free_sims[:] = list({id(x): x for x in free_sims + all_sims}.values())
     return out
+
+
+def _wait_polled(stream, nap=0.0):
+    """Wait for the work queued so far on `stream` by polling an event (hipEventQuery), not
+    parking the thread in a blocking synchronize: concurrent host threads blocked in the runtime
+    slowed one another's launches (tools/ge_concurrency.py)."""
+    import torch
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    while not ev.query():
+        time.sleep(nap)
 
 
 class _GESlot:

@@ -1,0 +1,90 @@
+% aiyagari_labor_egm_gpu.m -- host script for the MI355X solver (SURVEY.md §8(b) B6), the
+% endogenous-labour EGM model of Aiyagari_Endogenous_Labor_EGM.m.
+%
+% Calibration, bisection and reporting stay in MATLAB/Octave; the two inner loops are one
+% gateway call each:
+%   * the EGM iteration with the labour FOC (Aiyagari_Endogenous_Labor_EGM.m:67-107, GE copy
+%     :173-214)                                                   -> aiy_labor_egm_solve_mex
+%   * the Monte-Carlo capital path (:127-152, GE copy :223-242)  -> aiy_sim_capital_mex
+% As in the exogenous-labour EGM script, the GE loop sets r = r_guess (:178) but keeps the wage
+% of r = 0.04 (:55): kept below (w_stale), so the bisection trace is the script's.
+% Build the gateways first (aiyagari-replication_amd/mex/Makefile header, or
+%   mex -I../../include -L.. -laiyagari_hip <gateway>.c   /   mkoctfile --mex ...).
+
+clear; clc;
+
+% ---------------------------------------------------------------- calibration (:6-52)
+beta = 0.96; sigma = 5; alpha = 0.36; delta = 0.08; phi = 1; theta = 1; b = 0;
+rho = 0.6; sigma_e = 0.2; N = 7; Na = 400; tol = 1e-5; max_iter = 1000; T = 10000;
+
+l_grid = ((1:N) - 4) * sigma_e;
+edges = [-Inf, ((1:N-1) - 3.5) * sigma_e, Inf];
+sd = sigma_e * sqrt(1 - rho^2);
+P = zeros(N, N);
+for i = 1:N
+    for j = 1:N
+        P(i, j) = integral(@(x) normpdf(x, rho * l_grid(i), sd), edges(j), edges(j + 1));
+    end
+end
+A = [P' - eye(N); ones(1, N)];
+pi_stat = A \ [zeros(N, 1); 1];
+s = exp(l_grid);
+labor = s * pi_stat;
+
+wmin = (1 - alpha) * (alpha / ((1 / beta - 1) + delta))^(alpha / (1 - alpha));
+amin = min(b, wmin * s(1));
+kmax = delta^(1 / (alpha - 1));
+amax = kmax^alpha + (1 - delta) * kmax;
+a_grid = amin + (amax - amin) * (linspace(0, 1, Na).^2)';
+
+kdemand = @(r) labor * (alpha / (r + delta))^(1 / (1 - alpha));
+
+% ---------------------------------------------------------------- initial solve at r = 0.04
+r = 0.04;
+w = (1 - alpha) * (alpha / (r + delta))^(alpha / (1 - alpha));   % :55
+w_stale = w;
+policy_c = repmat((1 + r) * a_grid + w * mean(s), 1, N);          % :56, Na x N
+tic;
+[policy_c, policy_k, policy_l, dist, iter] = aiy_labor_egm_solve_mex( ...
+    policy_c, a_grid, s, P, r, w, beta, sigma, phi, theta, amin, tol, max_iter);
+fprintf('r = %.4f: %d iterations, dist %.3e\n', r, iter, dist);
+
+z1 = randi(N);                               % :124-125
+k1 = a_grid(randi(Na));
+[K_s, sim_k, sim_z] = aiy_sim_capital_mex(policy_k, a_grid, P, z1, k1, rand(T - 1, 1), 0);
+fprintf('K_s = %.6f\n', K_s);
+
+% ---------------------------------------------------------------- bisection on r (:154-255)
+r_low = -0.05; r_high = 1 / beta - 1;
+max_r_iter = 10; r_tol = 1e-5;
+r_history = zeros(max_r_iter, 1); k_supply = zeros(max_r_iter, 1); k_demand = zeros(max_r_iter, 1);
+for r_iter = 1:max_r_iter
+    r = (r_low + r_high) / 2;
+    [policy_c, policy_k, policy_l, dist, iter] = aiy_labor_egm_solve_mex( ...
+        policy_c, a_grid, s, P, r, w_stale, beta, sigma, phi, theta, amin, tol, max_iter);
+    [K_s, sim_k, sim_z] = aiy_sim_capital_mex(policy_k, a_grid, P, z1, k1, rand(T - 1, 1), 0);
+    K_d = kdemand(r);
+    r_history(r_iter) = r; k_supply(r_iter) = K_s; k_demand(r_iter) = K_d;
+    fprintf('step %2d: r = %.6f, K_s = %.6f, K_d = %.6f (%d iterations)\n', r_iter, r, K_s, ...
+            K_d, iter);
+    if abs(K_s - K_d) < r_tol
+        break;
+    elseif K_s > K_d
+        r_high = r;
+    else
+        r_low = r;
+    end
+end
+fprintf('equilibrium r = %.10f after %.3f s\n', r, toc);
+
+% ---------------------------------------------------------------- the script's reporting paths
+sim_c = zeros(T, 1); sim_y = zeros(T, 1); sim_s = zeros(T, 1);
+for t = 2:T
+    sim_c(t) = interp1(a_grid, policy_c(:, sim_z(t)), sim_k(t - 1), 'linear', 'extrap');
+    sim_y(t) = r * sim_k(t) + w_stale * s(sim_z(t));
+    sim_s(t) = sim_y(t) + delta * sim_k(t) - sim_c(t);
+end
+sorted_k = sort(sim_k);
+lorenz_k = cumsum(sorted_k) / sum(sorted_k);
+gini_k = 1 - 2 * trapz((1:T) / T, lorenz_k);
+fprintf('Gini coefficient for wealth: %.4f\n', gini_k);

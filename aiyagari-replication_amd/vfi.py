@@ -135,6 +135,11 @@ class Workspace:
         states (0: by size).  Results do not depend on it."""
         check(lib().aiy_ws_set_wide(self._h, ip(max_na), ip(splits), ip(waves), ip(states)))
 
+    def set_cu_exclusive(self, on: bool = True):
+        """Small-grid sweep workgroups reserve whole CUs (aiy_ws_set_cu_exclusive): for solves
+        running concurrently on other streams.  Results do not depend on it."""
+        check(lib().aiy_ws_set_cu_exclusive(self._h, ip(int(bool(on)))))
+
     def set_search(self, coarse_stride=0, k_chunk=1024):
         check(lib().aiy_ws_set_search(self._h, ip(coarse_stride), ip(k_chunk)))
 

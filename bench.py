@@ -30,8 +30,11 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 # hardware queues per process (HIP's default is 4): the GE drivers run speculative solves and
 # 2.7 ms Monte-Carlo chains on their own streams, and a stream sharing a queue with a chain
-# waits behind it (ge.aiyagari_vfi_overlapped).  Set before the HIP runtime starts.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+# waits behind it (ge.aiyagari_vfi_overlapped; tools/ge_concurrency.py: with 4 queues two
+# solves beside two chains ran 2.6x slower).  Raised (never lowered) before the HIP runtime starts:
+# an inherited smaller value (the GPU box exports 4) would otherwise win.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 PEAK_FP64_TFLOPS = 78.6   # MI355X fp64 vector (= fp64 matrix) peak, datasheet
 FLOPS_PER_CANDIDATE = 8  # sub, mul, mul, div, sub, mul, add, max
@@ -98,9 +101,12 @@ def ge_wall(pkg, threads):
     t0 = time.perf_counter()
     seq = pkg.ge.aiyagari_vfi()
     seq_s = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    out = pkg.ge.aiyagari_vfi_overlapped()
-    gpu_s = time.perf_counter() - t0
+    walls = []
+    for _ in range(5):  # the same equilibrium computed 5 times: value = the median wall
+        t0 = time.perf_counter()
+        out = pkg.ge.aiyagari_vfi_overlapped()
+        walls.append(time.perf_counter() - t0)
+    gpu_s = sorted(walls)[len(walls) // 2]
     cal = no.calib_aiyagari()
     cpu = {}
     for th in sorted({1, threads}):
@@ -112,6 +118,7 @@ def ge_wall(pkg, threads):
     return {"workload": "Aiyagari_VFI.m defaults (configs[0]): initial VFI + 10-step bisection + MC",
             "r_gpu": out["r"], "r_cpu": H["r_final"], "identical_trace": out["r_history"] == H["r"],
             "sweeps": int(sum(out["iters"])), "wall_s_gpu": gpu_s, "wall_s_cpu": cpu_s,
+            "wall_s_gpu_runs": walls,
             "driver": f"ge.aiyagari_vfi_overlapped (solves speculated {out['lookahead']} "
                       f"bisection level(s) ahead of the pending MC chain; {out['solves']} solve "
                       f"slots)",
@@ -144,6 +151,25 @@ def solve_wall(pkg, ws, cal, r, w, a_t, s_t, P_t, dev):
 def _json_profile(name):
     f = ROOT / "profiles" / name
     return json.loads(f.read_text()) if f.exists() else None
+
+
+PMC_ROUNDS = ("r05", "r04", "r03")  # newest first: counter passes of the kernels at HEAD
+
+
+def _counters(name, traffic_name=None):
+    """(derived PMC, HBM bytes per launch, source note) of the newest round's counter passes of
+    one kernel workload (profiles/<round>_pmc_<name>.json, <round>_traffic_<name>.json; made by
+    tools/pmc.sh + tools/pmc_summary.py / pmc_traffic.py)."""
+    traffic_name = traffic_name or name
+    for rnd in PMC_ROUNDS:
+        pmc = _json_profile(f"{rnd}_pmc_{name}.json")
+        if pmc is None:
+            continue
+        tf = _json_profile(f"{rnd}_traffic_{traffic_name}.json")
+        src = f"profiles/{rnd}_pmc_{name}.json" + (f", profiles/{rnd}_traffic_{traffic_name}.json"
+                                                    if tf else "")
+        return pmc.get("derived"), (tf or {}).get("bytes_per_launch"), src
+    return None, None, None
 
 
 def main():
@@ -341,14 +367,9 @@ def main():
         # SURVEY §8(d) D3 basis: 8 flops x every candidate (i, j, a') of the exhaustive scan the
         # result is bit-identical to -- the rate an exhaustive kernel would need to match it
         effective = FLOPS_PER_CANDIDATE * evals_per_sweep / (kern_avg_ms * 1e-3) / 1e12
-        traffic = None
         # PMC / HBM-traffic passes over the same sweeps 6..25 on the current kernels
-        # (tools/exp/r04_g8.sh / r04_g16.sh: tools/pmc.sh + pmc_summary / pmc_traffic, skip 5 take 20)
-        tf_name, pmc_name = "r04_traffic_vfi_tree.json", "r04_pmc_tree.json"
-        tf = _json_profile(tf_name)
-        if tf:
-            traffic = tf.get("bytes_per_launch")
-        pmc = _json_profile(pmc_name)
+        # (tools/exp/r05_pmc.sh: tools/pmc.sh + pmc_summary / pmc_traffic, skip 5 take 20)
+        pmc_d, traffic, pmc_src = _counters("tree", "vfi_tree")
         step_ms = sorted(blocks)
         out = {
             "metric": "Bellman evals/sec (Na·Na'·Nz, fp64)",
@@ -401,10 +422,10 @@ def main():
                          "effective_basis": f"SURVEY D3: {FLOPS_PER_CANDIDATE} flops x Na*Na'*Nz = "
                                             f"{evals_per_sweep} candidates per launch, the exhaustive "
                                             f"scan this kernel reproduces bit for bit",
-                         "pmc": (pmc or {}).get("derived"),
-                         "pmc_source": f"profiles/{pmc_name}, profiles/{tf_name} (rocprofv3 "
-                                       f"--pmc, tools/pmc.sh + tools/pmc_summary.py / "
-                                       f"pmc_traffic.py, same sweeps 6..25)"},
+                         "pmc": pmc_d,
+                         "pmc_source": f"{pmc_src} (rocprofv3 --pmc, tools/pmc.sh + "
+                                       f"tools/pmc_summary.py / pmc_traffic.py, same sweeps "
+                                       f"6..25)"},
         }
         out.update(legs)
         if exh is not None:  # the plain exhaustive scan's own roofline (mode 2)
@@ -426,32 +447,28 @@ def main():
             progress("batch_config4_share done")
             out["dist"] = BL.dist_leg(pkg, dev, cpu_threads=threads)
             progress("dist done")
-            # counter passes of these kernels (tools/pmc_workloads.py under tools/pmc.sh)
-            pm = lambda n: ((_json_profile(f"r03_pmc_{n}.json") or {}).get("derived"))
-            tr = lambda n: ((_json_profile(f"r03_traffic_{n}.json") or {}).get("bytes_per_launch"))
-            out["batch_config4_share"]["roofline"].update(
-                pmc=pm("batch"), traffic=tr("batch"),
-                pmc_source="profiles/r03_pmc_batch.json, r03_traffic_batch.json")
+            # counter passes of the kernels these legs time (tools/pmc_workloads_r05.py under
+            # tools/pmc.sh, one workload per pass set: tools/exp/r05_pmc.sh)
+            def attach(leg, name, kernel):
+                pmc_d, tf, src = _counters(name)
+                leg["roofline"].update(pmc={kernel: pmc_d}, traffic=tf, pmc_source=src)
+
+            attach(out["batch_config4_share"], "batch", "bell_tree_kernel")
             out["labor_vfi"] = {"Na400": BL.labor_leg(pkg, dev, 400, cpu_threads=threads,
                                                       cpu=not args.no_cpu_baseline),
-                                "Na20000": BL.labor_leg(pkg, dev, 20000, steps=5, reps=3, cpu=False)}
+                                "Na20000": BL.labor_leg(pkg, dev, 20000, steps=5, reps=3,
+                                                        cpu_threads=threads,
+                                                        cpu=not args.no_cpu_baseline)}
             out["egm"] = {"Na20000": BL.egm_leg(pkg, dev, 20000, cpu_threads=threads),
                           "Na400": BL.egm_leg(pkg, dev, 400, cpu_threads=threads)}
             progress("labor_vfi, egm done")
             out["labor_egm"] = {"Na20000": BL.egm_leg(pkg, dev, 20000, labor=True,
                                                       cpu_threads=threads)}
-            out["labor_vfi"]["Na400"]["roofline"]["pmc"] = pm("labor_na400")
-            out["labor_vfi"]["Na20000"]["roofline"]["pmc"] = pm("labor_na20000")
-            pm4 = lambda n: ((_json_profile(f"r04_pmc_{n}.json") or {}).get("derived"))
-            tr4 = lambda n: ((_json_profile(f"r04_traffic_{n}.json") or {}).get("bytes_per_launch"))
-            for leg, nm in (("egm", "egm_chain"), ("labor_egm", "labor_egm_chain")):
-                out[leg]["Na20000"]["roofline"].update(
-                    pmc={"egm_chain_kernel": pm4(nm)}, traffic=tr4(nm),
-                    pmc_source=f"profiles/r04_pmc_{nm}.json, r04_traffic_{nm}.json (the timed "
-                               f"kernel, egm_chain_kernel, 200 launches of the solve loop)")
-            out["dist"]["roofline"].update(
-                pmc=pm4("dist_push"), traffic=tr4("dist_push"),
-                pmc_source="profiles/r04_pmc_dist_push.json, r04_traffic_dist_push.json")
+            attach(out["labor_vfi"]["Na400"], "labor_na400", "bell_wide_kernel")
+            attach(out["labor_vfi"]["Na20000"], "labor_na20000", "bell_tree_kernel")
+            attach(out["egm"]["Na20000"], "egm_chain", "egm_chain_kernel")
+            attach(out["labor_egm"]["Na20000"], "labor_egm_chain", "egm_chain_kernel")
+            attach(out["dist"], "dist_push", "dist_push_kernel")
         if not args.no_panel and world == 1:   # F3/F2: KS shock panel + agent simulation
             import bench_panel
             out["ks_panel"] = bench_panel.panel_leg(pkg, dev, cpu_threads=threads)

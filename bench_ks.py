@@ -20,6 +20,7 @@ import time
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent
+KS_FLOPS_PER_NODE = 126  # algorithmic fp64 flops of one fused Howard node (ks_leg)
 sys.path.insert(0, str(ROOT))
 
 
@@ -86,17 +87,35 @@ def ks_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, exchange="halo", r
     # columns its forecast reads (16 B, each column once) and writes V (8 B) -> 52 B.
     bpn = 52
     gbs = nodes * bpn / (th / howard) / 1e9 / world  # per GPU
+    # The sweep is VALU-bound (PMC: ~73 % VALU busy, 5 waves/SIMD; traffic ~1.6x algorithmic),
+    # so the roof is fp64 vector throughput on the algorithmic flops of one node:
+    #   bellman_value: 4 pchip evaluations (pwch coefficients + Horner, 16 flops each with 4
+    #   divisions, + the shared h and x - x_i: 66), the expectation (8), the budget (3), aiy_log
+    #   (fdlibm, 28 with 1 division), beta*E + u (2) = 107; the fused next-sweep slope
+    #   (Fritsch-Butland interior rule, 19 with 7 divisions) -> 126 flops, divisions counted as
+    #   one flop as in SURVEY D3.
+    fpn = KS_FLOPS_PER_NODE
+    tfs = nodes * fpn / (th / howard) / 1e12 / world
+    pmc, pmc_src = _ks_pmc()
     return {"metric": "Krusell-Smith bellman_value evals/sec (Howard sweeps, fp64)",
             "value": nodes * howard / th, "unit": "evals/s", "n_gpus": world,
-            "roofline": {"bound": "hbm", "achieved": gbs, "peak": 8000.0, "unit": "GB/s",
-                         "frac": gbs / 8000.0,
-                         "basis": f"{bpn} B algorithmic per node per Howard sweep (slopes: V in, dV "
-                                  f"out; sweep: k_opt, segment hint, forecast V/dV columns in, V "
-                                  f"out) x {nodes // world} nodes per GPU / sweep time; the "
-                                  f"working set (V, dV, k_opt: 200 MB) is HBM-resident"},
-            "pmc": _ks_pmc(),
-            "pmc_source": "profiles/r04_pmc_ks_howard_slopes.json, "
-                          "profiles/r04_traffic_ks_howard_slopes.json (the timed kernel)",
+            "roofline": {"bound": "valu", "achieved": tfs, "peak": 78.6, "unit": "TFLOP/s",
+                         "frac": tfs / 78.6,
+                         "traffic": (pmc or {}).get("ks_howard_slopes_kernel", {}).get(
+                             "hbm_bytes_per_launch"),
+                         "basis": f"{fpn} fp64 flops per node per Howard sweep (4 pchip "
+                                  f"evaluations 66, expectation 8, budget 3, aiy_log 28, "
+                                  f"beta*E + u 2, fused pchip slope 19; 24 divisions counted "
+                                  f"as one flop each, SURVEY D3) x {nodes // world} nodes per "
+                                  f"GPU / sweep time; peak = fp64 vector 78.6 TF/s",
+                         "hbm_secondary": {"achieved": gbs, "peak": 8000.0, "unit": "GB/s",
+                                           "frac": gbs / 8000.0,
+                                           "basis": f"{bpn} B algorithmic per node per sweep "
+                                                    f"(slopes: V in, dV out; sweep: k_opt, "
+                                                    f"segment hint, forecast V/dV columns in, "
+                                                    f"V out)"}},
+            "pmc": pmc,
+            "pmc_source": pmc_src,
             "scaling": "strong", "vfi_iteration_ms": (ti + th) * 1e3,
             "howard_ms_per_sweep": th / howard * 1e3, "improve_ms": ti * 1e3,
             "workload": f"Krusell_Smith_VFI k={nk} K={nK} S=4 ({nodes} nodes, BASELINE "
@@ -205,19 +224,21 @@ def ks_direct_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, reps=3, che
 
 def _ks_pmc():
     """Counter summary of the kernel this leg times — ks_howard_slopes_kernel, one launch per
-    Howard sweep at k = 32,768, K = 64 (rocprofv3 --pmc passes over tools/pmc_workloads_r04.py,
-    tools/exp/r04_g2.sh) — if committed under profiles/."""
-    out = {}
-    for name, f, t in (("ks_howard_slopes_kernel", "r04_pmc_ks_howard_slopes.json",
-                        "r04_traffic_ks_howard_slopes.json"),):
-        p, q = ROOT / "profiles" / f, ROOT / "profiles" / t
-        if p.exists():
-            d = json.loads(p.read_text())["derived"]
-            out[name] = {k: d[k] for k in ("valu_busy", "waves_per_simd", "valu_per_wave",
-                                           "wait_frac")}
-            if q.exists():
-                out[name]["hbm_bytes_per_launch"] = json.loads(q.read_text())["bytes_per_launch"]
-    return out or None
+    Howard sweep at k = 32,768, K = 64 (rocprofv3 --pmc passes over tools/pmc_workloads_r05.py
+    ks, tools/exp/r05_pmc.sh) — from the newest round's files committed under profiles/."""
+    name = "ks_howard_slopes_kernel"
+    for rnd in ("r05", "r04"):
+        p = ROOT / "profiles" / f"{rnd}_pmc_ks_howard_slopes.json"
+        q = ROOT / "profiles" / f"{rnd}_traffic_ks_howard_slopes.json"
+        if not p.exists():
+            continue
+        d = json.loads(p.read_text())["derived"]
+        out = {name: {k: d[k] for k in ("valu_busy", "waves_per_simd", "valu_per_wave",
+                                        "wait_frac") if k in d}}
+        if q.exists():
+            out[name]["hbm_bytes_per_launch"] = json.loads(q.read_text())["bytes_per_launch"]
+        return out, f"profiles/{p.name}, profiles/{q.name} (the timed kernel)"
+    return None, None
 
 
 def ghost_model(pkg, dev, world=8, nk=32768, nK=64, depths=(1, 2, 3, 4, 6, 8), sweeps=24):

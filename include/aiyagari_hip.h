@@ -260,6 +260,12 @@ int aiy_ws_set_speculation(aiy_ws* ws, int max_batch);
  * (-1) or has bit 25 set.  max_na = -1: the default bound; 0: never.  splits / waves / states =
  * 0: chosen by size.  Results are identical to the tree sweep's for every setting. */
 int aiy_ws_set_wide(aiy_ws* ws, int max_na, int splits, int waves, int states);
+/* on = 1: every small-grid sweep launch of this workspace (aiy_ws_set_wide) reserves whole CUs
+ * (each workgroup asks for >= 88 KiB of LDS, so no second workgroup that uses LDS can share its
+ * CU).  For solves run concurrently on several streams (the speculative GE driver): a workgroup
+ * sharing its CU with another solve's becomes the straggler of its sweep.  Default 0.  Results do
+ * not depend on it. */
+int aiy_ws_set_cu_exclusive(aiy_ws* ws, int on);
 /* kernel shapes and A/B knobs (tuning only; results are identical for every value in
  * [-1, 2^26)).  VFI, bit 3 clear (default): the bound tree screen, bit 0 = 2 states per lane
  * (else 1), bits 1-2 = 1, 2, 4 or 8 cooperating waves per tile, bit 4 = XCD-aware tile order,

@@ -38,6 +38,24 @@ def test_sim_offgrid_egm_layout(pkg, gpu, Na):
     assert Ks == Ko
 
 
+@pytest.mark.parametrize("Na,t_bad", [(400, 5), (400, 2100), (400, 6000), (1500, 2100)])
+def test_sim_find_empty_late_in_the_chain(pkg, gpu, Na, t_bad):
+    """find() empty at a step in a later chunk (the two-wave kernel's state walker runs one
+    chunk ahead of the capital recurrence): the same error, and the C restatement agrees."""
+    rng = np.random.default_rng(Na + t_bad)
+    a = np.sort(rng.uniform(0, 50, Na))
+    a[0] = 0.0
+    N = 7
+    P = rng.random((N, N)) + 0.05
+    P /= P.sum(axis=1, keepdims=True) * (1 + 1e-6)  # rows sum below 1
+    U = rng.random(9999) * 0.99
+    U[t_bad - 1] = 0.9999999  # above every row sum: step t_bad finds nothing
+    pol = np.sort(rng.uniform(0, a[-1], (N, Na)), axis=1)
+    with pytest.raises(pkg.AiyError) as e:
+        pkg.sim_capital(pol, a, P, 3, float(a[Na // 2]), U)
+    assert e.value.status == "AIY_FIND_EMPTY"
+
+
 def test_sim_find_empty_is_an_error(pkg, gpu):
     P = np.array([[0.5, 0.4999], [0.5, 0.5]])  # row 1 sums below 1
     with pytest.raises(pkg.AiyError) as e:
@@ -48,11 +66,17 @@ def test_sim_find_empty_is_an_error(pkg, gpu):
 
 @pytest.mark.parametrize("N,Na,T", [(7, 400, 1), (7, 400, 2), (7, 400, 65), (7, 400, 4097),
                                     (1, 50, 300), (3, 2, 300), (5, 37, 1000), (16, 300, 3000),
-                                    (15, 1100, 3000), (7, 3000, 2049)])
+                                    (15, 1100, 3000), (7, 3000, 2049), (7, 400, 10000),
+                                    (7, 448, 2200), (7, 449, 2200), (7, 960, 4200),
+                                    (8, 448, 700), (8, 449, 700), (7, 64, 300), (7, 63, 300),
+                                    (7, 1500, 3000), (15, 480, 700)])
 def test_sim_chain_shapes_and_jumps(pkg, gpu, N, Na, T):
-    """Chain kernel edge cases vs the C restatement: T = 1, block/chunk boundaries (64, 2048),
-    tiny grids (Na < 64 window), N = 1 and the N = 16 wide-state path, and policies that jump
-    across the grid every step (the 64-point window misses, the full search runs)."""
+    """Chain kernel edge cases vs the C restatement: T = 1, block/chunk boundaries (64, 2048,
+    the GE's T = 10,000 with a 15-step tail), tiny grids (Na < 64 window), N = 1 and the N = 16
+    wide-state path, the two-wave kernel at both table strides and their edges (Na = 64,
+    448 / 449, 960 at N = 7; N = 8 at 448 and past it), the window kernel beyond (Na = 63,
+    N = 15, Na = 1,100 / 1,500) and the global-memory path, and policies that jump across the
+    grid every step (the 64-point window misses, the full search runs)."""
     rng = np.random.default_rng(N * 1000 + Na)
     a = np.sort(rng.uniform(0, 50, Na))
     a[0] = 0.0
