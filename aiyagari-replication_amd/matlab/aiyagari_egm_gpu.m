@@ -16,6 +16,7 @@ clear; clc;
 % ---------------------------------------------------------------- calibration (:7-56)
 beta = 0.96; sigma = 5; alpha = 0.36; delta = 0.08; b = 0;
 rho = 0.75; sigma_e = 0.75; N = 7; Na = 400; tol = 1e-5; max_iter = 1000; T = 10000;
+use_step_gateways = false;   % true: keep the script's own while loop, one gateway call per step
 
 l_grid = ((1:N) - 4) * sigma_e;
 edges = [-Inf, ((1:N-1) - 3.5) * sigma_e, Inf];
@@ -45,8 +46,19 @@ w = (1 - alpha) * (alpha / (r + delta))^(alpha / (1 - alpha));   % :61
 w_stale = w;                                 % the GE loop below never updates it (:180)
 policy_c = repmat((1 + r) * a_grid + w * mean(s), 1, N);          % :64, Na x N
 tic;
-[policy_c, policy_k, dist, iter] = ...
-    aiy_egm_solve_mex(policy_c, a_grid, s, P, r, w, beta, sigma, amin, tol, max_iter);
+if use_step_gateways
+    % the reference's loop (:74-110) with its body (:75-107) swapped for the gateway
+    dist = 1; iter = 0;
+    while dist > tol && iter < max_iter
+        iter = iter + 1;
+        [policy_c_next, policy_k, dist] = aiy_egm_step_mex(policy_c, a_grid, s, P, r, w, beta, ...
+                                                           sigma, amin);
+        policy_c = policy_c_next;
+    end
+else
+    [policy_c, policy_k, dist, iter] = ...
+        aiy_egm_solve_mex(policy_c, a_grid, s, P, r, w, beta, sigma, amin, tol, max_iter);
+end
 fprintf('r = %.4f: %d iterations, dist %.3e\n', r, iter, dist);
 
 z1 = randi(N);                               % :127-128

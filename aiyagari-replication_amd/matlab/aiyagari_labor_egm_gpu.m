@@ -16,6 +16,7 @@ clear; clc;
 % ---------------------------------------------------------------- calibration (:6-52)
 beta = 0.96; sigma = 5; alpha = 0.36; delta = 0.08; phi = 1; theta = 1; b = 0;
 rho = 0.6; sigma_e = 0.2; N = 7; Na = 400; tol = 1e-5; max_iter = 1000; T = 10000;
+use_step_gateways = false;   % true: keep the script's own while loop, one gateway call per step
 
 l_grid = ((1:N) - 4) * sigma_e;
 edges = [-Inf, ((1:N-1) - 3.5) * sigma_e, Inf];
@@ -45,8 +46,19 @@ w = (1 - alpha) * (alpha / (r + delta))^(alpha / (1 - alpha));   % :55
 w_stale = w;
 policy_c = repmat((1 + r) * a_grid + w * mean(s), 1, N);          % :56, Na x N
 tic;
-[policy_c, policy_k, policy_l, dist, iter] = aiy_labor_egm_solve_mex( ...
-    policy_c, a_grid, s, P, r, w, beta, sigma, phi, theta, amin, tol, max_iter);
+if use_step_gateways
+    % the reference's loop (:67-107) with its body (:68-104) swapped for the gateway
+    dist = 1; iter = 0;
+    while dist > tol && iter < max_iter
+        iter = iter + 1;
+        [policy_c_next, policy_k, policy_l, dist] = aiy_labor_egm_step_mex(policy_c, a_grid, s, ...
+            P, r, w, beta, sigma, phi, theta, amin);
+        policy_c = policy_c_next;
+    end
+else
+    [policy_c, policy_k, policy_l, dist, iter] = aiy_labor_egm_solve_mex( ...
+        policy_c, a_grid, s, P, r, w, beta, sigma, phi, theta, amin, tol, max_iter);
+end
 fprintf('r = %.4f: %d iterations, dist %.3e\n', r, iter, dist);
 
 z1 = randi(N);                               % :124-125

@@ -17,6 +17,7 @@ clear; clc;
 beta = 0.96; sigma = 5; alpha = 0.36; delta = 0.08; b = 0;
 rho = 0.6; sigma_e = 0.2; N = 7; psi = 1; eta = 2;
 Na = 400; tol = 1e-5; max_iter = 1000; T = 10000;
+use_step_gateways = false;   % true: keep the script's own VFI loop, one gateway call per sweep
 
 l_grid = ((1:N) - 4) * sigma_e;
 edges = [-Inf, ((1:N-1) - 3.5) * sigma_e, Inf];
@@ -49,9 +50,22 @@ v_old = zeros(N, Na); v_new = zeros(N, Na);
 policy_k = zeros(N, Na); policy_l = zeros(N, Na); policy_c = zeros(N, Na);
 r = 0.04;
 tic;
-[v_new, v_old, policy_k, policy_l, policy_c, iter] = aiy_labor_vfi_solve_mex( ...
-    v_old, a_grid, s, P, labor_choice, r, wage(r), beta, sigma, psi, eta, tol, max_iter, ...
-    v_new, policy_k, policy_l, policy_c);
+if use_step_gateways
+    % the reference's loop (:64-122) with its sweep (:69-112) swapped for the gateway; the
+    % workspace arrays go back in so infeasible states keep their values (:85)
+    for iter = 1:max_iter
+        [v_new, policy_k, policy_l, policy_c] = aiy_labor_vfi_sweep_mex(v_old, a_grid, s, P, ...
+            labor_choice, r, wage(r), beta, sigma, psi, eta, v_new, policy_k, policy_l, policy_c);
+        if max(abs(v_new(:) - v_old(:))) < tol
+            break;
+        end
+        v_old = v_new;
+    end
+else
+    [v_new, v_old, policy_k, policy_l, policy_c, iter] = aiy_labor_vfi_solve_mex( ...
+        v_old, a_grid, s, P, labor_choice, r, wage(r), beta, sigma, psi, eta, tol, max_iter, ...
+        v_new, policy_k, policy_l, policy_c);
+end
 fprintf('r = %.4f: %d sweeps\n', r, iter);
 
 % the simulation's first state (:135-136), then one rand per step (:139)

@@ -15,6 +15,7 @@ clear; clc;
 beta = 0.96; sigma = 5; alpha = 0.36; delta = 0.08; b = 0;
 rho = 0.75; sigma_e = 0.75; N = 7; Na = 400;
 tol = 1e-5; max_iter = 1000; T = 10000;
+use_step_gateways = false;   % true: keep the script's own VFI loop, one gateway call per sweep
 
 % seven-state discretisation: grid points (i-4)*sigma_e, transition probabilities by
 % integrating the conditional normal density over the fixed interval edges
@@ -47,8 +48,21 @@ z1 = randi(N);
 k1 = a_grid(randi(Na));
 r = 0.04;
 tic;
-[v_new, v_old, policy_k, policy_c, iter] = ...
-    aiy_vfi_solve_mex(zeros(N, Na), a_grid, s, P, r, wage(r), beta, sigma, tol, max_iter);
+if use_step_gateways
+    % the reference's loop (:65-90) with its sweep body (:68-83) swapped for the gateway
+    v_old = zeros(N, Na);
+    for iter = 1:max_iter
+        [v_new, policy_k, policy_c, idx] = aiy_vfi_sweep_mex(v_old, a_grid, s, P, r, wage(r), ...
+                                                             beta, sigma);
+        if max(abs(v_new(:) - v_old(:))) < tol
+            break;
+        end
+        v_old = v_new;
+    end
+else
+    [v_new, v_old, policy_k, policy_c, iter] = ...
+        aiy_vfi_solve_mex(zeros(N, Na), a_grid, s, P, r, wage(r), beta, sigma, tol, max_iter);
+end
 K_s = aiy_sim_capital_mex(policy_k, a_grid, P, z1, k1, rand(T - 1, 1), 1);
 fprintf('r = %.4f: %d sweeps, K_s = %.6f\n', r, iter, K_s);
 

@@ -16,6 +16,7 @@ z_grid = [1.01, 0.99]; eps_grid = [1, 0];
 k_size = 100; K_size = 4; T = 1100; population = 10000; T_discard = 100;
 howard_steps = 50; tol_vfi = 1e-6; max_vfi = 10000; tol_B = 1e-6; max_B = 100;
 update_B = 0.3; n_devices = 1;
+use_step_gateways = false;   % true: keep the script's own VFI loop (:143-204) around the steps
 params = [beta alpha delta k_min k_max ug ub l_bar mu z_grid eps_grid];
 
 k_grid = linspace(0, 1, k_size).^7 * (k_max - k_min) + k_min;
@@ -55,8 +56,25 @@ k_population = ones(population, 1) * K_grid(1);
 B = [0, 1, 0, 1];
 for B_iter = 1:max_B
     tic;
-    [value, k_opt, vfi_iter] = ks_vfi_solve_mex(value, k_opt, k_grid, K_grid, B, P, params, ...
-                                                howard_steps, tol_vfi, max_vfi, n_devices);
+    if use_step_gateways
+        % the reference's loop with its improvement (:148-168) and Howard sweeps (:172-192)
+        % swapped for the step gateways; the relative-difference stop (:195-203) stays here
+        for vfi_iter = 1:max_vfi
+            value_old = value;
+            if mod(vfi_iter - 1, 5) == 0
+                k_opt = ks_policy_improve_mex(value, k_grid, K_grid, B, P, params);
+            end
+            value = ks_howard_mex(value, k_opt, k_grid, K_grid, B, P, params, howard_steps);
+            rel = abs(value(:) - value_old(:)) ./ (abs(value_old(:)) + 1e-10);
+            if max(rel) < tol_vfi
+                break;
+            end
+        end
+    else
+        [value, k_opt, vfi_iter] = ks_vfi_solve_mex(value, k_opt, k_grid, K_grid, B, P, ...
+                                                    params, howard_steps, tol_vfi, max_vfi, ...
+                                                    n_devices);
+    end
     [K_ts, k_population] = ks_simulate_capital_mex(k_opt, k_grid, K_grid, zi_shock, ...
                                                    epsi_shock, k_population);
     % OLS of log K(t+1) on [1, log K(t)] per aggregate state (t >= T_discard)

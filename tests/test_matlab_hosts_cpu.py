@@ -91,5 +91,15 @@ def test_script_blocks_and_brackets_balance(script):
 
 def test_every_script_is_covered():
     names = {p.name for p in SCRIPTS}
-    assert {"aiyagari_vfi_gpu.m", "aiyagari_ge_multisection_gpu.m",
-            "krusell_smith_vfi_gpu.m"} <= names
+    assert {"aiyagari_vfi_gpu.m", "aiyagari_ge_multisection_gpu.m", "aiyagari_labor_vfi_gpu.m",
+            "aiyagari_egm_gpu.m", "aiyagari_labor_egm_gpu.m", "krusell_smith_vfi_gpu.m",
+            "krusell_smith_egm_gpu.m"} <= names
+
+
+def test_every_gateway_is_called_by_a_host_script():
+    """Every gateway in mex/ (the replacement for one inner loop of one reference script) is
+    called by at least one committed host script."""
+    called = set()
+    for f in SCRIPTS:
+        called |= {c[0] for c in _calls(_join_continuations(_strip(f.read_text())))}
+    assert set(gateway_bounds()) - called == set()

@@ -190,3 +190,20 @@ def test_step_gateways(pkg, gpu, golden):
                                                      1.0, 2.0)
     assert np.array_equal(v1, vo) and np.array_equal(lin - 1, lino)
     assert np.array_equal(k1, pko) and np.array_equal(l1, plo) and np.array_equal(c1, pco)
+
+
+def test_ks_step_gateways(pkg, gpu, golden):
+    """ks_policy_improve_mex (Krusell_Smith_VFI.m:148-168) and ks_howard_mex (:172-192) return
+    the golden policy, fminbnd evaluation counts and two-sweep Howard values."""
+    g = golden("ks_defaults")
+    prm = np.array([g["beta"], g["alpha"], g["delta"], g["k_min"], g["k_max"], g["ug"], g["ub"],
+                    g["l_bar"], g["mu"], 1.01, 0.99, 1.0, 0.0])
+    shape = g["V0"].shape
+    ko, nf = mexstub.call("ks_policy_improve_mex", 2, g["V0"], g["k_grid"], g["K_grid"], g["B"],
+                          g["P"], prm)
+    ko = ko.reshape(shape, order="F")
+    assert np.array_equal(ko, g["k_opt"])
+    assert np.array_equal(nf.reshape(shape, order="F"), g["nfev"])
+    (V2,) = mexstub.call("ks_howard_mex", 1, g["V0"], ko, g["k_grid"], g["K_grid"], g["B"], g["P"],
+                         prm, 2.0)
+    assert np.array_equal(V2.reshape(shape, order="F"), g["V_howard2"])
