@@ -7,6 +7,7 @@
 #include <cstring>
 
 #include "aiy_common.hpp"
+#include "ks.hpp"
 
 namespace aiy {
 int launch_flags_wait(const unsigned long long* flags, unsigned long long mask,
@@ -79,25 +80,81 @@ int aiy_flag_set(void* flags, int32_t slot, uint64_t value, void* stream) {
 
 extern "C" {
 // nsweeps Jacobi Howard sweeps of the direct schedule in one call (ks_dist.DirectPeers.sweeps):
-// sweep i reads parity p = parity ^ (i & 1) through tab[p] and writes parity p ^ 1, after the
-// neighbours in `mask` have published n0 + i, and publishes n0 + i + 1 in `slot`
+// sweep i reads parity p = parity ^ (i & 1) and writes parity p ^ 1, after the neighbours in
+// `mask` have published n0 + i, and publishes n0 + i + 1 in `slot`.  Staged: the forecast columns
+// peers own are read from a local halo, refreshed every sweep by one copy launch from the
+// owners' buffers (device pointer arrays src_p[q] -> dst[q], `col_bytes` each, q < ncopy;
+// system-scope loads) on `copy_stream` while the interior columns sweep on `stream`; the
+// boundary columns sweep after the copies.  The publish follows a
+// system-scope release of the sweep's writes (an event recorded with hipEventReleaseToSystem), so
+// a peer's copy after its wait reads this sweep's values from HBM, not from this device's L2.
 int ks_dev_direct_sweeps(ks_dev* h, const void* const* tab0, const void* const* tab1,
                          double* V0, double* V1, double* dV0, double* dV1, double* kopt,
-                         int32_t parity, int64_t nsweeps, void* flags, int32_t slot, uint64_t mask,
-                         uint64_t n0, double timeout_s, void* err, void* stream) {
+                         int32_t parity, int64_t nsweeps, const void* const* src0,
+                         const void* const* src1, void* const* dst, int32_t ncopy,
+                         int64_t col_bytes, void* flags, int32_t slot, uint64_t mask, uint64_t n0,
+                         double timeout_s, void* err, void* stream, void* copy_stream) {
     if (!h || !tab0 || !tab1 || !V0 || !V1 || !dV0 || !dV1 || !kopt || !flags || !err ||
-        nsweeps < 0 || (parity & ~1))
+        nsweeps < 0 || (parity & ~1) || ncopy < 0 || (ncopy && (!src0 || !src1 || !dst)) ||
+        (ncopy && (!copy_stream || col_bytes <= 0 || col_bytes % 8)))
         return fail(AIY_BAD_ARG, "bad argument");
     const void* const* tab[2] = {tab0, tab1};
+    const void* const* src[2] = {src0, src1};
     double* V[2] = {V0, V1};
     double* dV[2] = {dV0, dV1};
+    hipStream_t st = (hipStream_t)stream, cst = (hipStream_t)copy_stream;
+    hipEvent_t ev_go = nullptr, ev_copied = nullptr, ev_rel = nullptr;
+    int rc = AIY_OK;
+    auto done = [&](int r) {
+        for (hipEvent_t e : {ev_go, ev_copied, ev_rel})
+            if (e) (void)hipEventDestroy(e);
+        return r;
+    };
+#define DS_TRY(x)                   \
+    do {                            \
+        rc = (x);                   \
+        if (rc != AIY_OK) return done(rc); \
+    } while (0)
+#define DS_HIP(x)                                                                        \
+    do {                                                                                 \
+        const hipError_t e_ = (x);                                                       \
+        if (e_ != hipSuccess)                                                            \
+            return done(fail(AIY_HIP_ERROR, "%s failed: %s", #x, hipGetErrorString(e_))); \
+    } while (0)
+    DS_HIP(hipEventCreateWithFlags(&ev_go, hipEventDisableTiming));
+    DS_HIP(hipEventCreateWithFlags(&ev_copied, hipEventDisableTiming));
+    DS_HIP(hipEventCreateWithFlags(&ev_rel, hipEventDisableTiming | hipEventReleaseToSystem));
     for (int64_t i = 0; i < nsweeps; ++i) {
         const int p = parity ^ (int)(i & 1);
-        AIY_TRY(aiy_flags_wait(flags, mask, n0 + (uint64_t)i, timeout_s, err, stream));
-        AIY_TRY(ks_dev_set_columns(h, tab[p]));
-        AIY_TRY(ks_dev_howard_fused(h, V[p], dV[p], kopt, V[p ^ 1], dV[p ^ 1], stream));
-        AIY_TRY(aiy_flag_set(flags, slot, n0 + (uint64_t)i + 1, stream));
+        DS_TRY(aiy_flags_wait(flags, mask, n0 + (uint64_t)i, timeout_s, err, stream));
+        DS_TRY(ks_dev_set_columns(h, tab[p]));
+        if (ncopy) {  // the halo: after the wait (and after the previous boundary launch)
+            DS_HIP(hipEventRecord(ev_go, st));
+            DS_HIP(hipStreamWaitEvent(cst, ev_go, 0));
+            DS_TRY(launch_ks_halo_copy(reinterpret_cast<const double* const*>(src[p]),
+                                       reinterpret_cast<double* const*>(dst), ncopy,
+                                       (int)(col_bytes / 8), cst));
+            DS_HIP(hipEventRecord(ev_copied, cst));
+        }
+        DS_TRY(ks_dev_howard_fused_part(h, 0, V[p], dV[p], kopt, V[p ^ 1], dV[p ^ 1], stream));
+        if (ncopy) DS_HIP(hipStreamWaitEvent(st, ev_copied, 0));
+        DS_TRY(ks_dev_howard_fused_part(h, 1, V[p], dV[p], kopt, V[p ^ 1], dV[p ^ 1], stream));
+        DS_HIP(hipEventRecord(ev_rel, st));  // system-scope release before the publish
+        DS_TRY(aiy_flag_set(flags, slot, n0 + (uint64_t)i + 1, stream));
     }
-    return AIY_OK;
+#undef DS_TRY
+#undef DS_HIP
+    // the events may be destroyed with work pending (the runtime keeps them until it completes)
+    return done(AIY_OK);
+}
+
+// the halo refresh alone (before an improvement): the same copies, stream-ordered
+int ks_dev_halo_copy(const void* const* src, void* const* dst, int32_t ncopy, int64_t col_bytes,
+                     void* stream) {
+    if (ncopy < 0 || (ncopy && (!src || !dst || col_bytes <= 0 || col_bytes % 8)))
+        return fail(AIY_BAD_ARG, "bad argument");
+    return launch_ks_halo_copy(reinterpret_cast<const double* const*>(src),
+                               reinterpret_cast<double* const*>(dst), ncopy, (int)(col_bytes / 8),
+                               (hipStream_t)stream);
 }
 }  // extern "C"

@@ -30,6 +30,10 @@ struct KsArgs {
     // the launch's own V / dV arrays
     const double* const* colV;
     const double* const* coldV;
+    // staged direct schedule: the fused Howard launch runs the columns col_list[0 .. n_list)
+    // (interior or boundary subset of the shard's own columns) instead of the node range
+    const int* col_list;
+    int n_list;
 };
 struct KsParams {  // the 13-double parameter block, in order
     double beta, alpha, delta, k_min, k_max, ug, ub, l_bar, mu, z1, z2, e1, e2;
@@ -52,6 +56,8 @@ int launch_ks_howard(const KsArgs& A, const double* V, const double* dV, const d
                      double* Vn, hipStream_t st);
 // Howard sweep writing the next sweep's slopes too (dV must hold the slopes of V on every
 // column the launch reads; Vn and dVn are written on the launch's nodes)
+int launch_ks_halo_copy(const double* const* src, double* const* dst, int ncols, int nk,
+                        hipStream_t st);
 int launch_ks_howard_slopes(const KsArgs& A, const double* V, const double* dV,
                             const double* kopt, double* Vn, double* dVn, hipStream_t st);
 int launch_ks_hints(const KsArgs& A, const double* kopt, hipStream_t st);

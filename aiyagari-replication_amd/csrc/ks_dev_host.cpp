@@ -37,6 +37,11 @@ struct ks_dev {
     // direct schedule (ks_dev_set_columns): device table of 4·nK value then 4·nK slope column
     // pointers into the owners' buffers; null = the caller's full arrays
     const double* const* colV = nullptr;
+    // staged direct schedule (ks_dev_set_split): own columns whose four forecast columns are all
+    // owned (interior) and the rest (boundary), device lists
+    int* cols_int = nullptr;
+    int* cols_bnd = nullptr;
+    int n_int = 0, n_bnd = 0;
 };
 
 namespace aiy {
@@ -73,7 +78,7 @@ int ks_dev_destroy(ks_dev* h) {
                     "destroy them first", h->sharers);
     if (h->seg_owner) h->seg_owner->sharers--;
     void* ps[] = {h->kg, h->P, h->sl, h->dV, h->cols, h->own_cols, h->slots,
-                  h->seg_owner ? nullptr : h->seg};
+                  h->seg_owner ? nullptr : h->seg, h->cols_int, h->cols_bnd};
     for (void* q : ps)
         if (q) (void)hipFree(q);
     delete h;
@@ -192,6 +197,55 @@ int ks_dev_set_columns(ks_dev* h, const void* const* table) {
     if (!h) return fail(AIY_BAD_ARG, "NULL handle");
     h->colV = reinterpret_cast<const double* const*>(table);
     return AIY_OK;
+}
+
+// The staged direct schedule's split of the shard's own columns (c = s·nK + K): `interior`
+// columns read only owned forecast columns, `boundary` columns read at least one a peer owns
+// (through the local halo copy).  Every own column must be in exactly one list.
+int ks_dev_set_split(ks_dev* h, const int32_t* interior, int32_t n_int, const int32_t* boundary,
+                     int32_t n_bnd) {
+    if (!h || n_int < 0 || n_bnd < 0 || (n_int && !interior) || (n_bnd && !boundary))
+        return fail(AIY_BAD_ARG, "bad argument");
+    if (n_int + n_bnd != h->n_own)
+        return fail(AIY_BAD_ARG, "ks_dev_set_split: %d + %d columns, the shard owns %d", n_int,
+                    n_bnd, h->n_own);
+    std::vector<char> seen(4 * h->nK, 0);
+    for (int i = 0; i < n_int + n_bnd; ++i) {
+        const int c = i < n_int ? interior[i] : boundary[i - n_int];
+        const int s = c / h->nK, K = c % h->nK;
+        if (c < 0 || c >= 4 * h->nK || s < h->s0 || s >= h->s1 || K < h->K0 || K >= h->K1 || seen[c])
+            return fail(AIY_BAD_ARG, "ks_dev_set_split: column %d is not an own column (or repeats)", c);
+        seen[c] = 1;
+    }
+    for (int** q : {&h->cols_int, &h->cols_bnd})
+        if (*q) {
+            AIY_HIP(hipFree(*q));
+            *q = nullptr;
+        }
+    if (n_int) {
+        AIY_HIP(hipMalloc((void**)&h->cols_int, n_int * sizeof(int)));
+        AIY_HIP(hipMemcpy(h->cols_int, interior, n_int * sizeof(int), hipMemcpyHostToDevice));
+    }
+    if (n_bnd) {
+        AIY_HIP(hipMalloc((void**)&h->cols_bnd, n_bnd * sizeof(int)));
+        AIY_HIP(hipMemcpy(h->cols_bnd, boundary, n_bnd * sizeof(int), hipMemcpyHostToDevice));
+    }
+    h->n_int = n_int;
+    h->n_bnd = n_bnd;
+    return AIY_OK;
+}
+
+// the fused Howard sweep over one subset of the own columns (0 = interior, 1 = boundary)
+int ks_dev_howard_fused_part(ks_dev* h, int part, const double* V, const double* dV,
+                             const double* kopt, double* Vout, double* dVout, void* stream) {
+    if (!h || !V || !dV || !kopt || !Vout || !dVout || (part & ~1)) return fail(AIY_BAD_ARG, "bad argument");
+    if (h->n_int + h->n_bnd == 0)  // no split set: part 0 is the whole shard, part 1 nothing
+        return part ? AIY_OK : ks_dev_howard_fused(h, V, dV, kopt, Vout, dVout, stream);
+    KsArgs A = shard_args(h);
+    A.col_list = part ? h->cols_bnd : h->cols_int;
+    A.n_list = part ? h->n_bnd : h->n_int;
+    if (!A.n_list) return AIY_OK;
+    return launch_ks_howard_slopes(A, V, dV, kopt, Vout, dVout, (hipStream_t)stream);
 }
 
 // the slopes of the shard's own columns of V into dV (the start of a direct schedule)

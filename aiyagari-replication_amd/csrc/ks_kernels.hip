@@ -244,12 +244,12 @@ __global__ __launch_bounds__(256) void ks_howard_slopes_kernel(KsArgs A, const d
     const int q = lo + (int)threadIdx.x;
     const bool comp = q < hi, mine = q >= q0 && q < own_hi;
     const int col0 = A.node0 / nk + (int)blockIdx.z * (A.sstride / nk);  // block-uniform
-    const int ncl = A.n_local / nk;
+    const int ncl = A.col_list ? A.n_list : A.n_local / nk;
     KsView W{A.k_grid, V, dV};
     const double k = comp ? W.kg[q] : 0.0;
     const LdsCol yl{s_v, lo};
     for (int y = blockIdx.y; y < ncl; y += gridDim.y) {  // block-uniform trip count
-        const int col = col0 + y;
+        const int col = A.col_list ? A.col_list[y] : col0 + y;
         const int si = col / A.nK;
         const size_t n = (size_t)col * nk + q;
         double v = 0.0;
@@ -260,11 +260,49 @@ __global__ __launch_bounds__(256) void ks_howard_slopes_kernel(KsArgs A, const d
         s_v[threadIdx.x] = v;
         __syncthreads();
         if (mine) {
-            Vn[n] = v;
-            dVn[n] = pchip_slope_t(A.k_grid, yl, nk, q);
+            const double d = pchip_slope_t(A.k_grid, yl, nk, q);
+            if (A.col_list) {  // staged direct schedule: peers copy these columns after the
+                // publish — write them through to memory (system-scope vector stores), so the
+                // system-scope release before the publish has little left to flush
+                __hip_atomic_store(reinterpret_cast<unsigned long long*>(Vn + n),
+                                   __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(reinterpret_cast<unsigned long long*>(dVn + n),
+                                   __builtin_bit_cast(unsigned long long, d), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            } else {
+                Vn[n] = v;
+                dVn[n] = d;
+            }
         }
         __syncthreads();
     }
+}
+
+// The staged direct schedule's halo refresh: column q (nk doubles) from src[q] (a peer's buffer,
+// mapped through IPC) to dst[q] (this device).  The reads are system-scope loads, so they are
+// served coherently from the owner's memory, not from lines this device's caches kept from an
+// earlier copy of the same buffer; one launch for every column of the sweep.
+__global__ __launch_bounds__(256) void ks_halo_copy_kernel(const double* const* __restrict__ src,
+                                                           double* const* __restrict__ dst,
+                                                           int nk) {
+    const double* s = src[blockIdx.y];
+    double* d = dst[blockIdx.y];
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < nk; i += gridDim.x * 256) {
+        const unsigned long long u = __hip_atomic_load(
+            reinterpret_cast<const unsigned long long*>(s + i), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_SYSTEM);
+        d[i] = __builtin_bit_cast(double, u);
+    }
+}
+int launch_ks_halo_copy(const double* const* src, double* const* dst, int ncols, int nk,
+                        hipStream_t st) {
+    if (ncols <= 0) return AIY_OK;
+    if (ncols > 65535 || nk < 1) return fail(AIY_BAD_SHAPE, "halo copy: 1 <= columns <= 65535");
+    ks_halo_copy_kernel<<<dim3((unsigned)std::min((nk + 255) / 256, 64), (unsigned)ncols), 256, 0, st>>>(
+        src, dst, nk);
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
 }
 
 // the segment hints of the shard's nodes from k_opt (what ks_improve_kernel stores), for nodes
@@ -455,8 +493,9 @@ int launch_ks_howard_slopes(const KsArgs& A, const double* V, const double* dV,
         return fail(AIY_BAD_SHAPE, "Howard launch: node range must be whole columns");
     const int B = (int)ks_col_block(A.nk).x;  // 64 .. 256
     const int O = A.nk <= B ? A.nk : B - 4;
-    const dim3 g(cdiv(A.nk, O), (unsigned)std::max(1, std::min(A.n_local / A.nk, 65535)),
-                 std::max(A.ns, 1));
+    const dim3 g(cdiv(A.nk, O),
+                 (unsigned)std::max(1, std::min(A.col_list ? A.n_list : A.n_local / A.nk, 65535)),
+                 A.col_list ? 1 : std::max(A.ns, 1));
     ks_howard_slopes_kernel<<<g, B, 0, st>>>(A, V, dV, kopt, Vn, dVn, O);
     AIY_HIP(hipGetLastError());
     return AIY_OK;

@@ -389,9 +389,41 @@ class DirectPeers:
             for c in owned_columns(nK, q, world, bounds):
                 owner[c] = q
         cb = 8 * self.nk
-        self.tab = [torch.tensor([addr[owner[c]][b] + cb * c for c in range(4 * nK)] +
-                                 [addr[owner[c]][2 + b] + cb * c for c in range(4 * nK)],
+        # staged reads: the forecast columns peers own are copied into a
+        # local halo once per sweep (after the wait, beside the interior launch), so no kernel
+        # reads a peer's memory; the own columns split into interior (every forecast column
+        # owned) and boundary (at least one copied)
+        kp = np.asarray(shard.kp_idx)
+        targets = {c: [sn * nK + int(kp[c // nK, c % nK]) for sn in range(4)] for c in self.own}
+        self.remote = sorted({t for c in self.own for t in targets[c] if owner[t] != rank})
+        interior = [c for c in self.own if all(owner[t] == rank for t in targets[c])]
+        boundary = [c for c in self.own if c not in set(interior)]
+        ii = np.ascontiguousarray(interior, np.int32)
+        bb = np.ascontiguousarray(boundary, np.int32)
+        check(lib().ks_dev_set_split(shard._h, ptr(ii), C.c_int32(ii.size), ptr(bb),
+                                     C.c_int32(bb.size)))
+        nr = len(self.remote)
+        self.hV = torch.empty((max(nr, 1), self.nk), dtype=V.dtype, device=V.device)
+        self.hdV = torch.empty_like(self.hV)
+        slot = {c: i for i, c in enumerate(self.remote)}
+        hv, hdv = self.hV.data_ptr(), self.hdV.data_ptr()
+
+        def col(c, b, slope):
+            if owner[c] != rank and c in slot:
+                return (hdv if slope else hv) + cb * slot[c]
+            return addr[owner[c]][(2 if slope else 0) + b] + cb * c
+        self.tab = [torch.tensor([col(c, b, False) for c in range(4 * nK)] +
+                                 [col(c, b, True) for c in range(4 * nK)],
                                  dtype=torch.int64, device=V.device) for b in (0, 1)]
+        # the copies of one sweep: the owners' parity-b value then slope columns -> the halo
+        dev_arr = lambda xs: torch.tensor(xs or [0], dtype=torch.int64, device=V.device)
+        self._src = [dev_arr([addr[owner[c]][b] + cb * c for c in self.remote] +
+                             [addr[owner[c]][2 + b] + cb * c for c in self.remote])
+                     for b in (0, 1)]
+        self._dst = dev_arr([hv + cb * i for i in range(nr)] + [hdv + cb * i for i in range(nr)])
+        self._ncopy = 2 * nr
+        self._col_bytes = cb
+        self.copy_stream = torch.cuda.Stream(device=V.device)
         # the counter page: rank 0 creates it, every rank maps and registers it
         name, fail_msg = [None], None
         if rank == 0:
@@ -470,22 +502,29 @@ class DirectPeers:
         self.publish()
 
     def improve(self, kopt):
-        """Policy improvement (:148-168) of the own nodes, forecast columns read in place."""
+        """Policy improvement (:148-168) of the own nodes: after the wait, the peers' forecast
+        columns are copied into the halo (stream-ordered), the own ones read in place."""
         self.wait()
+        check(lib().ks_dev_halo_copy(ptr(self._src[self.cur]), ptr(self._dst),
+                                     C.c_int32(self._ncopy), i64(self._col_bytes),
+                                     stream_handle(None)))
         self.shard.set_columns(self.tab[self.cur])
         self.shard.improve_direct(kopt)
 
     def sweeps(self, kopt, n):
-        """n Jacobi Howard sweeps (:172-192): per sweep the hand-off wait, one fused launch and
-        the publish, all enqueued by one C call (ks_dev_direct_sweeps)."""
+        """n Jacobi Howard sweeps (:172-192): per sweep the hand-off wait, the halo copies on
+        the copy stream beside the interior launch, the boundary launch, a system-scope release
+        and the publish, all enqueued by one C call (ks_dev_direct_sweeps)."""
         if n <= 0:
             return
         check(lib().ks_dev_direct_sweeps(
             self.shard._h, ptr(self.tab[0]), ptr(self.tab[1]), ptr(self.V[0]), ptr(self.V[1]),
             ptr(self.dV[0]), ptr(self.dV[1]), ptr(kopt), C.c_int32(self.cur), i64(n),
+            ptr(self._src[0]), ptr(self._src[1]), ptr(self._dst), C.c_int32(self._ncopy),
+            i64(self._col_bytes),
             C.c_void_p(self._flags), C.c_int32(self.rank), C.c_uint64(self.mask),
             C.c_uint64(self.n), C.c_double(self.timeout_s), C.c_void_p(self._err),
-            stream_handle(None)))
+            stream_handle(None), stream_handle(self.copy_stream)))
         self.n += n
         self.cur ^= n & 1
 

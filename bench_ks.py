@@ -372,14 +372,47 @@ def direct_model(pkg, dev, world=8, nk=32768, nK=64, sweeps=24, howard=50):
         e1.record()
         torch.cuda.synchronize()
         swp.append(e0.elapsed_time(e1) / sweeps)
-    # the cross-process hand-off's own cost (ks_dist.DirectPeers): the slowest shard's sweeps
-    # through ks_dev_direct_sweeps, waiting on (and publishing to) a counter slot in a mapped
-    # host page — here its own slot, always satisfied, so the difference to the plain sweeps is
-    # the two extra one-wave launches and the host-memory poll per sweep
+    # the cross-process schedule's own cost (ks_dist.DirectPeers, staged): the slowest shard's
+    # sweeps through ks_dev_direct_sweeps — per sweep a counter wait on a mapped host page (its
+    # own slot, always satisfied), the copies of the peers' forecast columns into a local halo on
+    # a second stream beside the interior launch, the boundary launch, the system-scope release
+    # and the publish.  The copies here are device-local (the peers' buffers are on this GPU),
+    # so their time is an HBM lower bound on the xGMI copy (DESIGN.md §6 budgets the link).
     import ctypes as C
     import mmap
     check, lib = pkg._capi.check, pkg._capi.lib
-    q = max(range(world), key=lambda x: swp[x])
+    def remote_of(x):
+        K0x, K1x, s0x, s1x = slices[x]
+        kpx = np.asarray(sh[x].kp_idx)
+        ownx = [sidx * nK + K for sidx in range(s0x, s1x) for K in range(K0x, K1x)]
+        tg = {c: [sn * nK + int(kpx[c // nK, c % nK]) for sn in range(4)] for c in ownx}
+        return ownx, tg, sorted({t for c in ownx for t in tg[c] if owner[t] != x})
+    # the shard with the most peer-owned forecast columns (ties: the slowest sweep)
+    q = max(range(world), key=lambda x: (len(remote_of(x)[2]), swp[x]))
+    own, targets, remote = remote_of(q)
+    interior = np.ascontiguousarray([c for c in own if all(owner[t] == q for t in targets[c])],
+                                    np.int32)
+    boundary = np.ascontiguousarray([c for c in own if c not in set(interior.tolist())], np.int32)
+    check(lib().ks_dev_set_split(sh[q]._h, C.c_void_p(interior.ctypes.data),
+                                 C.c_int32(interior.size), C.c_void_p(boundary.ctypes.data),
+                                 C.c_int32(boundary.size)))
+    nr = len(remote)
+    hV = torch.empty((max(nr, 1), nk), dtype=torch.float64, device=dev)
+    hdV = torch.empty_like(hV)
+    cb = 8 * nk
+    slot = {c: i for i, c in enumerate(remote)}
+    stab = []
+    for b in range(2):
+        a = [(hV.data_ptr() + cb * slot[c]) if c in slot else Vb[owner[c]][b].data_ptr() + cb * c
+             for c in range(4 * nK)]
+        a += [(hdV.data_ptr() + cb * slot[c]) if c in slot else dVb[owner[c]][b].data_ptr() + cb * c
+              for c in range(4 * nK)]
+        stab.append(torch.tensor(a, dtype=torch.int64, device=dev))
+    darr = lambda xs: torch.tensor(xs or [0], dtype=torch.int64, device=dev)
+    src = [darr([Vb[owner[c]][b].data_ptr() + cb * c for c in remote] +
+                [dVb[owner[c]][b].data_ptr() + cb * c for c in remote]) for b in range(2)]
+    dst = darr([hV.data_ptr() + cb * i for i in range(nr)] + [hdV.data_ptr() + cb * i for i in range(nr)])
+    cstream = torch.cuda.Stream(device=dev)
     page = mmap.mmap(-1, 16384)
     host = C.c_char.from_buffer(page)
     hp = C.addressof(host)
@@ -391,9 +424,11 @@ def direct_model(pkg, dev, world=8, nk=32768, nK=64, sweeps=24, howard=50):
 
     def run_direct(n, n0):
         check(lib().ks_dev_direct_sweeps(
-            sh[q]._h, P_(tabs[q][0]), P_(tabs[q][1]), P_(Vb[q][0]), P_(Vb[q][1]), P_(dVb[q][0]),
-            P_(dVb[q][1]), P_(ko), C.c_int32(0), C.c_int64(n), dptr, C.c_int32(0),
-            C.c_uint64(1), C.c_uint64(n0), C.c_double(30.0), C.c_void_p(dptr.value + 8192), st))
+            sh[q]._h, P_(stab[0]), P_(stab[1]), P_(Vb[q][0]), P_(Vb[q][1]), P_(dVb[q][0]),
+            P_(dVb[q][1]), P_(ko), C.c_int32(0), C.c_int64(n), P_(src[0]), P_(src[1]), P_(dst),
+            C.c_int32(2 * nr), C.c_int64(cb), dptr, C.c_int32(0), C.c_uint64(1),
+            C.c_uint64(n0), C.c_double(30.0), C.c_void_p(dptr.value + 8192), st,
+            C.c_void_p(cstream.cuda_stream)))
     run_direct(2, 1)
     e0, e1 = ev(), ev()
     e0.record()
@@ -407,6 +442,7 @@ def direct_model(pkg, dev, world=8, nk=32768, nK=64, sweeps=24, howard=50):
     page.close()
     for x in sh:
         x.close()
+    remote_bytes = 2 * nr * cb
     it_ms = max(imp) + howard * max(swp)
     return {"world": world, "sweeps": sweeps, "improve_ms_by_shard": imp,
             "gpu_ms_per_sweep_by_shard": swp, "gpu_ms_per_sweep_slowest": max(swp),
@@ -414,14 +450,20 @@ def direct_model(pkg, dev, world=8, nk=32768, nK=64, sweeps=24, howard=50):
             "handoff": {"shard": q, "gpu_ms_per_sweep_with_handoff": hand,
                         "handoff_us_per_sweep": (hand - swp[q]) * 1e3, "timeouts": err,
                         "projected_vfi_iteration_ms": max(imp) + howard * (max(swp) + hand - swp[q]),
-                        "note": "ks_dev_direct_sweeps on the slowest shard with a self-satisfied "
-                                "counter wait + publish per sweep (the multi-process schedule's "
-                                "launches; the neighbours' skew is not in it)"},
+                        "remote_columns": nr, "remote_bytes_per_sweep": remote_bytes,
+                        "interior_columns": int(interior.size),
+                        "boundary_columns": int(boundary.size),
+                        "xgmi_us_per_sweep_at_link_rate": remote_bytes / 153e9 * 1e6,
+                        "note": "ks_dev_direct_sweeps (staged) on the slowest shard: self-satisfied "
+                                "counter wait, halo copies of the peers' columns on a second stream "
+                                "beside the interior launch, boundary launch, system-scope release, "
+                                "publish; the copies are device-local here (xGMI time at one link's "
+                                "153 GB/s: xgmi_us_per_sweep_at_link_rate); the neighbours' skew is "
+                                "not in it"},
             "note": f"direct schedule (ks_vfi_solve_sharded depth 0) emulated on one GPU: each of "
                     f"{world} shards timed alone, reading the other shards' buffers through its "
                     f"column table; projected iteration = slowest improvement + {howard} x "
-                    f"slowest sweep (the per-sweep stream-event waits between devices are not in "
-                    f"it; no columns are copied)"}
+                    f"slowest sweep; `handoff` adds the staged schedule's copies and second launch"}
 
 
 def main():

@@ -446,13 +446,33 @@ int aiy_host_unregister(void* p);
 int aiy_flags_wait(const void* flags, uint64_t mask, uint64_t value, double timeout_s, void* err,
                    void* stream);
 int aiy_flag_set(void* flags, int32_t slot, uint64_t value, void* stream);
-/* nsweeps fused Howard sweeps of the direct schedule in one call: sweep i reads parity
- * p = parity ^ (i & 1) (V/dV p, column table tab_p) and writes parity p ^ 1, once the slots in
- * `mask` hold >= n0 + i; then slot `slot` := n0 + i + 1. */
+/* The staged direct schedule.  ks_dev_set_split: the shard's own columns c = s·K_size + K in
+ * two host lists — `interior` columns read only forecast columns the shard owns, `boundary`
+ * columns read at least one a peer owns; ks_dev_howard_fused_part sweeps one list (part 0 / 1)
+ * like ks_dev_howard_fused.
+ * ks_dev_direct_sweeps: nsweeps fused Howard sweeps; sweep i reads parity p = parity ^ (i & 1)
+ * (V/dV p, column table tab_p) and writes parity p ^ 1, once the slots in `mask` hold >= n0 + i.
+ * The forecast columns peers own are read from a local halo that the table points at: per
+ * sweep, after the wait, ONE launch copies src_p[q] -> dst[q], col_bytes each, q < ncopy (DEVICE
+ * arrays of pointers; the owners' parity-p value and slope columns, read with system-scope
+ * loads) on copy_stream while the interior columns sweep on `stream`; the boundary columns
+ * sweep after it and store their values write-through (system scope).  Then a
+ * system-scope release (an event recorded with hipEventReleaseToSystem) and slot `slot` :=
+ * n0 + i + 1.  ncopy = 0: every forecast column is read through the table as it is (one process,
+ * or no peer columns).  ks_dev_halo_copy: the same copies once, stream-ordered (before an
+ * improvement). */
+int ks_dev_set_split(ks_dev* h, const int32_t* interior, int32_t n_int, const int32_t* boundary,
+                     int32_t n_bnd);
+int ks_dev_howard_fused_part(ks_dev* h, int part, const double* V, const double* dV,
+                             const double* kopt, double* Vout, double* dVout, void* stream);
 int ks_dev_direct_sweeps(ks_dev* h, const void* const* tab0, const void* const* tab1,
                          double* V0, double* V1, double* dV0, double* dV1, double* kopt,
-                         int32_t parity, int64_t nsweeps, void* flags, int32_t slot, uint64_t mask,
-                         uint64_t n0, double timeout_s, void* err, void* stream);
+                         int32_t parity, int64_t nsweeps, const void* const* src0,
+                         const void* const* src1, void* const* dst, int32_t ncopy,
+                         int64_t col_bytes, void* flags, int32_t slot, uint64_t mask, uint64_t n0,
+                         double timeout_s, void* err, void* stream, void* copy_stream);
+int ks_dev_halo_copy(const void* const* src, void* const* dst, int32_t ncopy, int64_t col_bytes,
+                     void* stream);
 /* Ghost shards (ks_dist.py exchanges halos every m Howard sweeps and sweeps a widening
  * rectangle of other ranks' columns redundantly in between — same kernels, so still bit-exact):
  * h uses owner's segment-hint array (same grid and device; destroying owner while a handle
