@@ -82,10 +82,10 @@ extern "C" {
 // nsweeps Jacobi Howard sweeps of the direct schedule in one call (ks_dist.DirectPeers.sweeps):
 // sweep i reads parity p = parity ^ (i & 1) and writes parity p ^ 1, after the neighbours in
 // `mask` have published n0 + i, and publishes n0 + i + 1 in `slot`.  Staged: the forecast columns
-// peers own are read from a local halo, refreshed every sweep by one copy launch from the
-// owners' buffers (device pointer arrays src_p[q] -> dst[q], `col_bytes` each, q < ncopy;
-// system-scope loads) on `copy_stream` while the interior columns sweep on `stream`; the
-// boundary columns sweep after the copies.  The publish follows a
+// peers own are read from a local halo, refreshed every sweep from the owners' buffers (device
+// pointer arrays src_p[q] -> dst[q], `col_bytes` each, q < ncopy; system-scope loads) by extra
+// block rows of the interior launch, so the copies run beside the interior columns; the
+// boundary columns sweep in the next launch.  The publish follows a
 // system-scope release of the sweep's writes (an event recorded with hipEventReleaseToSystem), so
 // a peer's copy after its wait reads this sweep's values from HBM, not from this device's L2.
 int ks_dev_direct_sweeps(ks_dev* h, const void* const* tab0, const void* const* tab1,
@@ -102,12 +102,12 @@ int ks_dev_direct_sweeps(ks_dev* h, const void* const* tab0, const void* const* 
     const void* const* src[2] = {src0, src1};
     double* V[2] = {V0, V1};
     double* dV[2] = {dV0, dV1};
-    hipStream_t st = (hipStream_t)stream, cst = (hipStream_t)copy_stream;
-    hipEvent_t ev_go = nullptr, ev_copied = nullptr, ev_rel = nullptr;
+    hipStream_t st = (hipStream_t)stream;
+    (void)copy_stream;  // (the copies now run inside the interior launch)
+    hipEvent_t ev_rel = nullptr;
     int rc = AIY_OK;
     auto done = [&](int r) {
-        for (hipEvent_t e : {ev_go, ev_copied, ev_rel})
-            if (e) (void)hipEventDestroy(e);
+        if (ev_rel) (void)hipEventDestroy(ev_rel);
         return r;
     };
 #define DS_TRY(x)                   \
@@ -115,36 +115,24 @@ int ks_dev_direct_sweeps(ks_dev* h, const void* const* tab0, const void* const* 
         rc = (x);                   \
         if (rc != AIY_OK) return done(rc); \
     } while (0)
-#define DS_HIP(x)                                                                        \
-    do {                                                                                 \
-        const hipError_t e_ = (x);                                                       \
-        if (e_ != hipSuccess)                                                            \
-            return done(fail(AIY_HIP_ERROR, "%s failed: %s", #x, hipGetErrorString(e_))); \
-    } while (0)
-    DS_HIP(hipEventCreateWithFlags(&ev_go, hipEventDisableTiming));
-    DS_HIP(hipEventCreateWithFlags(&ev_copied, hipEventDisableTiming));
-    DS_HIP(hipEventCreateWithFlags(&ev_rel, hipEventDisableTiming | hipEventReleaseToSystem));
+    {
+        const hipError_t e = hipEventCreateWithFlags(&ev_rel, hipEventDisableTiming | hipEventReleaseToSystem);
+        if (e != hipSuccess) return fail(AIY_HIP_ERROR, "hipEventCreateWithFlags: %s", hipGetErrorString(e));
+    }
     for (int64_t i = 0; i < nsweeps; ++i) {
         const int p = parity ^ (int)(i & 1);
         DS_TRY(aiy_flags_wait(flags, mask, n0 + (uint64_t)i, timeout_s, err, stream));
         DS_TRY(ks_dev_set_columns(h, tab[p]));
-        if (ncopy) {  // the halo: after the wait (and after the previous boundary launch)
-            DS_HIP(hipEventRecord(ev_go, st));
-            DS_HIP(hipStreamWaitEvent(cst, ev_go, 0));
-            DS_TRY(launch_ks_halo_copy(reinterpret_cast<const double* const*>(src[p]),
-                                       reinterpret_cast<double* const*>(dst), ncopy,
-                                       (int)(col_bytes / 8), cst));
-            DS_HIP(hipEventRecord(ev_copied, cst));
-        }
-        DS_TRY(ks_dev_howard_fused_part(h, 0, V[p], dV[p], kopt, V[p ^ 1], dV[p ^ 1], stream));
-        if (ncopy) DS_HIP(hipStreamWaitEvent(st, ev_copied, 0));
+        // interior columns + the halo copy rows in one launch, then the boundary columns
+        DS_TRY(ks_dev_howard_fused_part_halo(h, 0, V[p], dV[p], kopt, V[p ^ 1], dV[p ^ 1],
+                                             ncopy ? src[p] : nullptr, ncopy ? dst : nullptr,
+                                             ncopy, stream));
         DS_TRY(ks_dev_howard_fused_part(h, 1, V[p], dV[p], kopt, V[p ^ 1], dV[p ^ 1], stream));
-        DS_HIP(hipEventRecord(ev_rel, st));  // system-scope release before the publish
+        const hipError_t e = hipEventRecord(ev_rel, st);  // system-scope release before the publish
+        if (e != hipSuccess) return done(fail(AIY_HIP_ERROR, "hipEventRecord: %s", hipGetErrorString(e)));
         DS_TRY(aiy_flag_set(flags, slot, n0 + (uint64_t)i + 1, stream));
     }
 #undef DS_TRY
-#undef DS_HIP
-    // the events may be destroyed with work pending (the runtime keeps them until it completes)
     return done(AIY_OK);
 }
 

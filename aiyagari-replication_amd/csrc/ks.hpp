@@ -34,6 +34,11 @@ struct KsArgs {
     // (interior or boundary subset of the shard's own columns) instead of the node range
     const int* col_list;
     int n_list;
+    // ... and, in the same launch, n_halo extra block rows copy halo column q from halo_src[q]
+    // (a peer's buffer: system-scope loads) to halo_dst[q]
+    const double* const* halo_src;
+    double* const* halo_dst;
+    int n_halo;
 };
 struct KsParams {  // the 13-double parameter block, in order
     double beta, alpha, delta, k_min, k_max, ug, ub, l_bar, mu, z1, z2, e1, e2;

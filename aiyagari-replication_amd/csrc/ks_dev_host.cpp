@@ -238,13 +238,31 @@ int ks_dev_set_split(ks_dev* h, const int32_t* interior, int32_t n_int, const in
 // the fused Howard sweep over one subset of the own columns (0 = interior, 1 = boundary)
 int ks_dev_howard_fused_part(ks_dev* h, int part, const double* V, const double* dV,
                              const double* kopt, double* Vout, double* dVout, void* stream) {
-    if (!h || !V || !dV || !kopt || !Vout || !dVout || (part & ~1)) return fail(AIY_BAD_ARG, "bad argument");
-    if (h->n_int + h->n_bnd == 0)  // no split set: part 0 is the whole shard, part 1 nothing
+    return ks_dev_howard_fused_part_halo(h, part, V, dV, kopt, Vout, dVout, nullptr, nullptr, 0,
+                                         stream);
+}
+// ... with `n_halo` halo columns copied (src[q] -> dst[q], device pointer arrays, system-scope
+// loads) by extra block rows of the same launch
+int ks_dev_howard_fused_part_halo(ks_dev* h, int part, const double* V, const double* dV,
+                                  const double* kopt, double* Vout, double* dVout,
+                                  const void* const* src, void* const* dst, int32_t n_halo,
+                                  void* stream) {
+    if (!h || !V || !dV || !kopt || !Vout || !dVout || (part & ~1) || n_halo < 0 ||
+        (n_halo && (!src || !dst)))
+        return fail(AIY_BAD_ARG, "bad argument");
+    if (h->n_int + h->n_bnd == 0) {  // no split set: part 0 is the whole shard, part 1 nothing
+        if (n_halo) return fail(AIY_BAD_ARG, "halo copies need ks_dev_set_split");
         return part ? AIY_OK : ks_dev_howard_fused(h, V, dV, kopt, Vout, dVout, stream);
+    }
     KsArgs A = shard_args(h);
     A.col_list = part ? h->cols_bnd : h->cols_int;
     A.n_list = part ? h->n_bnd : h->n_int;
-    if (!A.n_list) return AIY_OK;
+    // an empty list stays in list mode (the launch may be copy rows only): any non-null pointer
+    if (!A.col_list) A.col_list = h->own_cols;
+    A.halo_src = reinterpret_cast<const double* const*>(src);
+    A.halo_dst = reinterpret_cast<double* const*>(dst);
+    A.n_halo = n_halo;
+    if (!A.n_list && !n_halo) return AIY_OK;
     return launch_ks_howard_slopes(A, V, dV, kopt, Vout, dVout, (hipStream_t)stream);
 }
 

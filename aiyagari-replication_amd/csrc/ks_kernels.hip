@@ -243,6 +243,18 @@ __global__ __launch_bounds__(256) void ks_howard_slopes_kernel(KsArgs A, const d
     const int hi = min(nk, q0 + O + 2);
     const int q = lo + (int)threadIdx.x;
     const bool comp = q < hi, mine = q >= q0 && q < own_hi;
+    if (A.col_list && (int)blockIdx.y >= A.n_list) {  // a halo copy row (staged schedule)
+        const int hq = (int)blockIdx.y - A.n_list;
+        const double* src = A.halo_src[hq];
+        double* dst = A.halo_dst[hq];
+        for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nk; i += gridDim.x * blockDim.x) {
+            const unsigned long long u = __hip_atomic_load(
+                reinterpret_cast<const unsigned long long*>(src + i), __ATOMIC_RELAXED,
+                __HIP_MEMORY_SCOPE_SYSTEM);
+            dst[i] = __builtin_bit_cast(double, u);
+        }
+        return;  // (block-uniform: no barrier below is skipped by part of a block)
+    }
     const int col0 = A.node0 / nk + (int)blockIdx.z * (A.sstride / nk);  // block-uniform
     const int ncl = A.col_list ? A.n_list : A.n_local / nk;
     KsView W{A.k_grid, V, dV};
@@ -493,8 +505,11 @@ int launch_ks_howard_slopes(const KsArgs& A, const double* V, const double* dV,
         return fail(AIY_BAD_SHAPE, "Howard launch: node range must be whole columns");
     const int B = (int)ks_col_block(A.nk).x;  // 64 .. 256
     const int O = A.nk <= B ? A.nk : B - 4;
+    if (A.col_list && A.n_list + A.n_halo > 65535)
+        return fail(AIY_BAD_SHAPE, "Howard launch: at most 65,535 listed + halo columns");
     const dim3 g(cdiv(A.nk, O),
-                 (unsigned)std::max(1, std::min(A.col_list ? A.n_list : A.n_local / A.nk, 65535)),
+                 (unsigned)std::max(1, A.col_list ? A.n_list + A.n_halo
+                                                  : std::min(A.n_local / A.nk, 65535)),
                  A.col_list ? 1 : std::max(A.ns, 1));
     ks_howard_slopes_kernel<<<g, B, 0, st>>>(A, V, dV, kopt, Vn, dVn, O);
     AIY_HIP(hipGetLastError());

@@ -453,10 +453,12 @@ int aiy_flag_set(void* flags, int32_t slot, uint64_t value, void* stream);
  * ks_dev_direct_sweeps: nsweeps fused Howard sweeps; sweep i reads parity p = parity ^ (i & 1)
  * (V/dV p, column table tab_p) and writes parity p ^ 1, once the slots in `mask` hold >= n0 + i.
  * The forecast columns peers own are read from a local halo that the table points at: per
- * sweep, after the wait, ONE launch copies src_p[q] -> dst[q], col_bytes each, q < ncopy (DEVICE
- * arrays of pointers; the owners' parity-p value and slope columns, read with system-scope
- * loads) on copy_stream while the interior columns sweep on `stream`; the boundary columns
- * sweep after it and store their values write-through (system scope).  Then a
+ * sweep, after the wait, the interior launch also copies src_p[q] -> dst[q], col_bytes each,
+ * q < ncopy (DEVICE arrays of pointers; the owners' parity-p value and slope columns, read with
+ * system-scope loads) in extra block rows, beside the interior columns; the boundary columns
+ * sweep in the next launch; both store their values write-through (system scope).  copy_stream
+ * is unused (kept for the ABI).  ks_dev_howard_fused_part_halo: the part launch with such
+ * copy rows.  Then a
  * system-scope release (an event recorded with hipEventReleaseToSystem) and slot `slot` :=
  * n0 + i + 1.  ncopy = 0: every forecast column is read through the table as it is (one process,
  * or no peer columns).  ks_dev_halo_copy: the same copies once, stream-ordered (before an
@@ -465,6 +467,10 @@ int ks_dev_set_split(ks_dev* h, const int32_t* interior, int32_t n_int, const in
                      int32_t n_bnd);
 int ks_dev_howard_fused_part(ks_dev* h, int part, const double* V, const double* dV,
                              const double* kopt, double* Vout, double* dVout, void* stream);
+int ks_dev_howard_fused_part_halo(ks_dev* h, int part, const double* V, const double* dV,
+                                  const double* kopt, double* Vout, double* dVout,
+                                  const void* const* src, void* const* dst, int32_t n_halo,
+                                  void* stream);
 int ks_dev_direct_sweeps(ks_dev* h, const void* const* tab0, const void* const* tab1,
                          double* V0, double* V1, double* dV0, double* dV1, double* kopt,
                          int32_t parity, int64_t nsweeps, const void* const* src0,
