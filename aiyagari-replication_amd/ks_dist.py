@@ -314,6 +314,20 @@ def column_table(owners_V, owners_dV, owner, nk):
     return torch.tensor(addr, dtype=torch.int64, device=dev)
 
 
+def staged_plan(own, kp_idx, owner, nK: int, rank: int):
+    """The staged direct schedule's plan for one rank: (remote, interior, boundary) — the sorted
+    forecast columns s'·nK + K'_idx(s, K) its own columns read that other ranks own (its halo),
+    and its own columns split into those whose four forecast columns are all its own and the
+    rest (Krusell_Smith_VFI.m:343-349: node (k, K, s) reads column K'_idx(s, K) of every s')."""
+    kp = np.asarray(kp_idx)
+    targets = {c: [sn * nK + int(kp[c // nK, c % nK]) for sn in range(4)] for c in own}
+    remote = sorted({t for c in own for t in targets[c] if owner[t] != rank})
+    interior = [c for c in own if all(owner[t] == rank for t in targets[c])]
+    inner = set(interior)
+    boundary = [c for c in own if c not in inner]
+    return remote, interior, boundary
+
+
 class DirectPeers:
     """The direct schedule (ks_vfi_solve_sharded depth = 0) under one process per
     GPU.  Every rank keeps its own columns of value and slopes in two parity buffers; the
@@ -393,11 +407,7 @@ class DirectPeers:
         # local halo once per sweep (after the wait, beside the interior launch), so no kernel
         # reads a peer's memory; the own columns split into interior (every forecast column
         # owned) and boundary (at least one copied)
-        kp = np.asarray(shard.kp_idx)
-        targets = {c: [sn * nK + int(kp[c // nK, c % nK]) for sn in range(4)] for c in self.own}
-        self.remote = sorted({t for c in self.own for t in targets[c] if owner[t] != rank})
-        interior = [c for c in self.own if all(owner[t] == rank for t in targets[c])]
-        boundary = [c for c in self.own if c not in set(interior)]
+        self.remote, interior, boundary = staged_plan(self.own, shard.kp_idx, owner, nK, rank)
         ii = np.ascontiguousarray(interior, np.int32)
         bb = np.ascontiguousarray(boundary, np.int32)
         check(lib().ks_dev_set_split(shard._h, ptr(ii), C.c_int32(ii.size), ptr(bb),

@@ -381,18 +381,15 @@ def direct_model(pkg, dev, world=8, nk=32768, nK=64, sweeps=24, howard=50):
     import ctypes as C
     import mmap
     check, lib = pkg._capi.check, pkg._capi.lib
-    def remote_of(x):
+    def plan_of(x):
         K0x, K1x, s0x, s1x = slices[x]
-        kpx = np.asarray(sh[x].kp_idx)
         ownx = [sidx * nK + K for sidx in range(s0x, s1x) for K in range(K0x, K1x)]
-        tg = {c: [sn * nK + int(kpx[c // nK, c % nK]) for sn in range(4)] for c in ownx}
-        return ownx, tg, sorted({t for c in ownx for t in tg[c] if owner[t] != x})
+        return kd.staged_plan(ownx, sh[x].kp_idx, owner, nK, x)
     # the shard with the most peer-owned forecast columns (ties: the slowest sweep)
-    q = max(range(world), key=lambda x: (len(remote_of(x)[2]), swp[x]))
-    own, targets, remote = remote_of(q)
-    interior = np.ascontiguousarray([c for c in own if all(owner[t] == q for t in targets[c])],
-                                    np.int32)
-    boundary = np.ascontiguousarray([c for c in own if c not in set(interior.tolist())], np.int32)
+    q = max(range(world), key=lambda x: (len(plan_of(x)[0]), swp[x]))
+    remote, interior, boundary = plan_of(q)
+    interior = np.ascontiguousarray(interior, np.int32)
+    boundary = np.ascontiguousarray(boundary, np.int32)
     check(lib().ks_dev_set_split(sh[q]._h, C.c_void_p(interior.ctypes.data),
                                  C.c_int32(interior.size), C.c_void_p(boundary.ctypes.data),
                                  C.c_int32(boundary.size)))

@@ -326,3 +326,33 @@ def test_direct_peers_bound_to_their_shard():
     a, b = _Shard(), _Shard()
     with pytest.raises(ValueError, match="another shard"):
         kd._solve_direct(None, None, b, 4, 3, 1e-6, 1, 0, 2, None, peers=_Peers(a))
+
+
+def test_staged_plan_matches_the_forecast_reads():
+    """ks_dist.staged_plan (the staged direct schedule's halo and interior/boundary split)
+    against a brute-force walk over every node of every rank: the halo is exactly the peer-owned
+    columns some own node's forecast reads, interior columns read only own columns, and every
+    own column is in exactly one list — for K-range and (K, Z) slices, identity and shifted ALMs."""
+    kd = _pkg().ks_dist
+    rng = np.random.default_rng(7)
+    for nK, world in ((4, 8), (6, 2), (12, 3), (64, 8), (16, 5)):
+        for shift in (0, -1, 1, "rand"):
+            if shift == "rand":
+                kp = rng.integers(0, nK, size=(4, nK))
+            else:
+                kp = np.clip(np.arange(nK)[None, :] + shift, 0, nK - 1).repeat(4, axis=0)
+            owner = [0] * (4 * nK)
+            for q in range(world):
+                for c in kd.owned_columns(nK, q, world):
+                    owner[c] = q
+            for rank in range(world):
+                own = kd.owned_columns(nK, rank, world)
+                remote, interior, boundary = kd.staged_plan(own, kp, owner, nK, rank)
+                reads = {c: {sn * nK + int(kp[c // nK, c % nK]) for sn in range(4)} for c in own}
+                assert remote == sorted({t for c in own for t in reads[c] if owner[t] != rank})
+                assert sorted(interior + boundary) == sorted(own)
+                assert not set(interior) & set(boundary)
+                for c in interior:
+                    assert all(owner[t] == rank for t in reads[c])
+                for c in boundary:
+                    assert any(owner[t] != rank for t in reads[c])
