@@ -230,6 +230,9 @@ __global__ void ks_howard_kernel(KsArgs A, const double* __restrict__ V,
 // ks_howard_kernel + ks_slopes_kernel, so bit for bit the two-launch sweep.  Columns of
 // length <= blockDim are one block each (O = nk: nothing evaluated twice); longer columns
 // evaluate 4 of every 256 nodes twice.
+// LIST: the staged direct schedule's launches (a column list, halo copy rows, write-through
+// stores); the node-range instantiation is the plain sweep.
+template <bool LIST>
 __global__ __launch_bounds__(256) void ks_howard_slopes_kernel(KsArgs A, const double* __restrict__ V,
                                                                const double* __restrict__ dV,
                                                                const double* __restrict__ k_opt,
@@ -243,7 +246,7 @@ __global__ __launch_bounds__(256) void ks_howard_slopes_kernel(KsArgs A, const d
     const int hi = min(nk, q0 + O + 2);
     const int q = lo + (int)threadIdx.x;
     const bool comp = q < hi, mine = q >= q0 && q < own_hi;
-    if (A.col_list && (int)blockIdx.y >= A.n_list) {  // a halo copy row (staged schedule)
+    if (LIST && (int)blockIdx.y >= A.n_list) {  // a halo copy row (staged schedule)
         const int hq = (int)blockIdx.y - A.n_list;
         const double* src = A.halo_src[hq];
         double* dst = A.halo_dst[hq];
@@ -256,12 +259,12 @@ __global__ __launch_bounds__(256) void ks_howard_slopes_kernel(KsArgs A, const d
         return;  // (block-uniform: no barrier below is skipped by part of a block)
     }
     const int col0 = A.node0 / nk + (int)blockIdx.z * (A.sstride / nk);  // block-uniform
-    const int ncl = A.col_list ? A.n_list : A.n_local / nk;
+    const int ncl = LIST ? A.n_list : A.n_local / nk;
     KsView W{A.k_grid, V, dV};
     const double k = comp ? W.kg[q] : 0.0;
     const LdsCol yl{s_v, lo};
     for (int y = blockIdx.y; y < ncl; y += gridDim.y) {  // block-uniform trip count
-        const int col = A.col_list ? A.col_list[y] : col0 + y;
+        const int col = LIST ? A.col_list[y] : col0 + y;
         const int si = col / A.nK;
         const size_t n = (size_t)col * nk + q;
         double v = 0.0;
@@ -273,7 +276,7 @@ __global__ __launch_bounds__(256) void ks_howard_slopes_kernel(KsArgs A, const d
         __syncthreads();
         if (mine) {
             const double d = pchip_slope_t(A.k_grid, yl, nk, q);
-            if (A.col_list) {  // staged direct schedule: peers copy these columns after the
+            if (LIST) {  // staged direct schedule: peers copy these columns after the
                 // publish — write them through to memory (system-scope vector stores), so the
                 // system-scope release before the publish has little left to flush
                 __hip_atomic_store(reinterpret_cast<unsigned long long*>(Vn + n),
@@ -511,7 +514,8 @@ int launch_ks_howard_slopes(const KsArgs& A, const double* V, const double* dV,
                  (unsigned)std::max(1, A.col_list ? A.n_list + A.n_halo
                                                   : std::min(A.n_local / A.nk, 65535)),
                  A.col_list ? 1 : std::max(A.ns, 1));
-    ks_howard_slopes_kernel<<<g, B, 0, st>>>(A, V, dV, kopt, Vn, dVn, O);
+    if (A.col_list) ks_howard_slopes_kernel<true><<<g, B, 0, st>>>(A, V, dV, kopt, Vn, dVn, O);
+    else ks_howard_slopes_kernel<false><<<g, B, 0, st>>>(A, V, dV, kopt, Vn, dVn, O);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }
