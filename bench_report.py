@@ -77,6 +77,11 @@ def leg_summary(leg):
     if isinstance(rf, dict) and _num(rf.get("frac")) is not None:
         s["frac"] = rf["frac"]
         s["bound"] = rf.get("bound")
+    # the counter pass behind the leg's PMC block: its first file's name (profiles/<round>_pmc_*)
+    src = (rf or {}).get("pmc_source") if isinstance(rf, dict) else None
+    src = src or leg.get("pmc_source")
+    if isinstance(src, str) and src:
+        s["pmc"] = src.split(",")[0].split(" ")[0].replace("profiles/", "")
     cv, cores = _cpu_value(leg.get("cpu_baseline"))
     if cv is not None:
         s["cpu"] = cv
