@@ -81,6 +81,16 @@ __device__ __forceinline__ unsigned long long wave_max_u64_lane63(unsigned long 
     k = mx(k, dpp_u64<0x143, 0xc>(k));
     return k;
 }
+// the same ladder on a 32-bit signed key (a quarter of the 64-bit ladder's instructions)
+__device__ __forceinline__ int wave_max_i32_lane63(int k) {
+    k = max(k, (int)dpp_u32<0xB1>((unsigned)k));
+    k = max(k, (int)dpp_u32<0x4E>((unsigned)k));
+    k = max(k, (int)dpp_u32<0x141>((unsigned)k));
+    k = max(k, (int)dpp_u32<0x140>((unsigned)k));
+    k = max(k, (int)dpp_u32<0x142, 0xa>((unsigned)k));
+    k = max(k, (int)dpp_u32<0x143, 0xc>((unsigned)k));
+    return k;
+}
 
 // first k in [0, n) with a[k] >= x  (== count of a[k] < x), a non-decreasing.
 __device__ __forceinline__ int lower_bound_dev(const double* __restrict__ a, int n, double x) {

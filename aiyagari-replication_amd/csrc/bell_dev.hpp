@@ -124,20 +124,29 @@ __device__ __forceinline__ double cash(double x, double y, double Ll) {
     else return x + y;                     // (1+r)a_j + w s_i          (Aiyagari_VFI.m:72)
 }
 
-// EV(i,k) = Σ_m (β·P(i,m))·V(m,k) in m order (Aiyagari_VFI.m:79).  The V column is loaded 16
-// rows at a time, every load in flight before the ordered sum (a plain loop waits one L2 round
-// trip per row: N of them per thread); i is uniform, so P comes by scalar loads.
+// EV(i,k) = Σ_m (β·P(i,m))·V(m,k) in m order (Aiyagari_VFI.m:79).  Eight rows at a time, every
+// load of a chunk (the V column and the P row, at indices clamped into range) in flight before
+// the ordered sum, and every term used unconditionally (a row past N adds +0.0, which leaves
+// the sum bit for bit as it is: it never holds −0.0).  A load guarded by `m < N` gets sunk
+// into its guarded use, after the first wait: one dependent round trip per row (7 in the
+// small-grid sweep's prologue before this form).
 __device__ __forceinline__ double table_ev(int N, int Na, const double* __restrict__ P,
                                            const double* __restrict__ V, double beta, int i,
                                            int k) {
     double acc = 0.0;
-    for (int m0 = 0; m0 < N; m0 += 16) {
-        double vv[16];
+    for (int m0 = 0; m0 < N; m0 += 8) {
+        double pm[8], vv[8];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) vv[u] = m0 + u < N ? V[(size_t)(m0 + u) * Na + k] : 0.0;
+        for (int u = 0; u < 8; ++u) {
+            const int m = min(m0 + u, N - 1);
+            pm[u] = P[i * N + m];
+            vv[u] = V[(size_t)m * Na + k];
+        }
 #pragma unroll
-        for (int u = 0; u < 16; ++u)
-            if (m0 + u < N) acc = acc + (beta * P[i * N + m0 + u]) * vv[u];
+        for (int u = 0; u < 8; ++u) {
+            const double term = (beta * pm[u]) * vv[u];
+            acc = acc + (m0 + u < N ? term : 0.0);
+        }
     }
     return acc;
 }

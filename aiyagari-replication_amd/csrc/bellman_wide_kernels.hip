@@ -103,6 +103,13 @@ __global__ __launch_bounds__(64 * NW) void bell_wide_kernel(
     const double vo = (okj && wave == 0) ? A.v_old[t] : 0.0;
     const int h = (A.hint && okj) ? A.hint[t] : -1;
     const double y = A.w * A.s[i];
+    // (labour) the levels and their disutilities, loaded with the rest (stored to LDS below: a
+    // load issued after the table's would be a second dependent round trip)
+    double lv_pre = 1.0, ds_pre = 0.0;
+    if (LAB && threadIdx.x < Nl) {
+        lv_pre = A.L[threadIdx.x];
+        ds_pre = A.dis[threadIdx.x];
+    }
     // 1. EV and D of the whole row into LDS (the table kernel's operations: bell_dev.hpp); no
     // dependence on this tile's feasible prefixes, so its loads leave with the ones above
     // and the maxima of D over aligned 8-candidate blocks (the screen's block bounds: DPP over
@@ -113,9 +120,10 @@ __global__ __launch_bounds__(64 * NW) void bell_wide_kernel(
         const int k = k0 + (int)threadIdx.x;
         double D = -__builtin_inf();
         if (k < Na) {
+            const double ak = a[k];  // (issued with the V column, not after the sum)
             const double ev = table_ev(N, Na, A.P, A.v_old, A.beta, i, k);
             D = table_D(ev, NP);
-            s_tab[k] = make_double2(a[k], D);
+            s_tab[k] = make_double2(ak, D);
             s_ev[k] = ev;
         }
         double d8 = fmax(D, dpp_d<0xB1>(D));
@@ -134,17 +142,20 @@ __global__ __launch_bounds__(64 * NW) void bell_wide_kernel(
         }
     const bool anyfeas = kmx > 0;
     if (LAB && threadIdx.x < Nl) {
-        s_L[threadIdx.x] = A.L[threadIdx.x];
-        s_dis[threadIdx.x] = A.dis[threadIdx.x];
+        s_L[threadIdx.x] = lv_pre;
+        s_dis[threadIdx.x] = ds_pre;
     }
-    if (wave == 0) {  // the tile's feasible range per level (a wave maximum: any sign of 1 + r)
+    // the tile's feasible range per level (a wave maximum: any sign of 1 + r), level l by wave
+    // l mod NW and the widest by the last wave — spread out, not one wave doing all Nl + 1
+    // reductions while the others wait at the barrier (≈ 4 k cycles at Nl = 10)
 #pragma unroll
-        for (int l = 0; l < NLM; ++l)
-            if (l < Nl) {
-                const int m = (int)wave_max_u64_lane63((unsigned long long)kfr[l]);
-                if (lane == 63) s_kfl[l] = m;
-            }
-        const int km = (int)wave_max_u64_lane63((unsigned long long)kmx);
+    for (int l = 0; l < NLM; ++l)
+        if (l < Nl && l % NW == wave) {
+            const int m = wave_max_i32_lane63(kfr[l]);
+            if (lane == 63) s_kfl[l] = m;
+        }
+    if (wave == NW - 1) {
+        const int km = wave_max_i32_lane63(kmx);
         if (lane == 63) s_kfl[Nl] = km;
     }
     int hl = lwide, hk = 0, kfh = kmx;
@@ -171,8 +182,8 @@ __global__ __launch_bounds__(64 * NW) void bell_wide_kernel(
     int idx = -1;
     unsigned nhits = 0;
     if (okj && anyfeas) {
-        const double coh = cash<LAB>(x, y, LAB ? A.L[hl] : 1.0);
-        const double dis = LAB ? A.dis[hl] : 0.0;
+        const double coh = cash<LAB>(x, y, LAB ? s_L[hl] : 1.0);
+        const double dis = LAB ? s_dis[hl] : 0.0;
         auto val_at = [&](int k) __attribute__((always_inline)) {
             return bell_val<NP, LAB>(coh - s_tab[k].x, s_ev[k], A.sigma, dis);
         };
@@ -221,15 +232,18 @@ __global__ __launch_bounds__(64 * NW) void bell_wide_kernel(
     // passes.
     const int gw0 = (sp * NW + wave) * Q, gstride = S * NW * Q;  // (the wave's first slice)
     const int gw = gw0 + qs;                                        // this lane's slice
-    unsigned ntests = 0, nvotes = 0;
+    unsigned ntests = 0, nvotes = 0, nblk = 0, nrnd = 0;  // (instrumentation)
     // the eight candidates of the lane's block k0 at level l (every lane of the wave runs it)
     auto block = [&](int l, int k0, int kend, double coh, double dis)
                      __attribute__((always_inline)) {
         double B = okj ? screen_B(best, idx, dis, NP) : __builtin_nan("");
         double2 tk[8];
 #pragma unroll
+        for (int u = 0; u < 8; ++u)  // (every read in range, then the selects: one LDS wait)
+            tk[u] = s_tab[min(k0 + u, Na - 1)];
+#pragma unroll
         for (int u = 0; u < 8; ++u)  // (past the range: a = +inf, c < 0, the test fails)
-            tk[u] = k0 + u < kend ? s_tab[k0 + u] : make_double2(__builtin_inf(), 0.0);
+            tk[u] = k0 + u < kend ? tk[u] : make_double2(__builtin_inf(), 0.0);
         double cx[8], dd[8], tv[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
@@ -249,6 +263,7 @@ __global__ __launch_bounds__(64 * NW) void bell_wide_kernel(
             pall = pall || pk[u];
         }
         ntests += max(0, min(8, kend - k0));
+        if (TR) ++nblk;
         if (!__any(pall)) return;
         unsigned vote = 0;
 #pragma unroll
@@ -277,12 +292,13 @@ __global__ __launch_bounds__(64 * NW) void bell_wide_kernel(
             const int u = __builtin_ctz(vote);
             vote &= vote - 1;
             const int k = min(k0 + u, Na - 1);
-            const double c = coh - s_tab[k].x;
+            const double2 tkk = s_tab[k];  // (both reads before any use)
+            const double evk = s_ev[k];
+            const double c = coh - tkk.x;
             const int lin = l + Nl * k;
-            if (okj && pk[u] && lin != idx && c > 0 &&
-                (s_tab[k].y - B) * aiy_ipow(c, NP) >= kThr) {
+            if (okj && pk[u] && lin != idx && c > 0 && (tkk.y - B) * aiy_ipow(c, NP) >= kThr) {
                 ++nhits;
-                const double val = bell_val<NP, LAB>(c, s_ev[k], A.sigma, dis);
+                const double val = bell_val<NP, LAB>(c, evk, A.sigma, dis);
                 if (lexi_take(val, lin, best, idx)) B = screen_B(best, idx, dis, NP);
             }
         }
@@ -295,26 +311,38 @@ __global__ __launch_bounds__(64 * NW) void bell_wide_kernel(
         // bound-tested VB at a time (independent chains across levels; one level at a time
         // would test one or two blocks per dependent round)
         const int npair = nbl > 0 ? Nl * nbl : 0;
+        const int lsh = nbl == 2 ? 1 : 0;  // pair p: level p >> lsh, the lane's (p & lsh)-th block
         for (int p0 = 0; p0 < npair; p0 += VB) {
             double cx[VB], dd[VB], tb[VB], coh[VB], dis[VB];
             int lv[VB], k0v[VB], kev[VB];
+            // every LDS read of the VB pairs first, at indices clamped into range (no branch
+            // around a read: one wait for all of them), then the selects
+            double Lv[VB], av[VB], dmv[VB];
 #pragma unroll
             for (int v = 0; v < VB; ++v) {
                 const int pp = min(p0 + v, npair - 1);
-                const int l = pp / nbl;
+                const int l = pp >> lsh;
                 lv[v] = l;
-                k0v[v] = 8 * (gw + (pp - l * nbl) * gstride);
+                k0v[v] = 8 * (gw + (pp & lsh) * gstride);
+                const int kc = min(k0v[v], Na - 1);
                 kev[v] = s_kfl[l];
-                coh[v] = okj ? cash<LAB>(x, y, LAB ? s_L[l] : 1.0) : 0.0;
-                dis[v] = LAB ? s_dis[l] : 0.0;
+                Lv[v] = s_L[l];
+                dis[v] = s_dis[l];
+                av[v] = s_tab[kc].x;
+                dmv[v] = s_dm8[kc >> 3];
+            }
+#pragma unroll
+            for (int v = 0; v < VB; ++v) {
+                coh[v] = okj ? cash<LAB>(x, y, Lv[v]) : 0.0;
                 const double B = okj ? screen_B(best, idx, dis[v], NP) : __builtin_nan("");
                 const bool okb = p0 + v < npair && k0v[v] < kev[v];
-                cx[v] = okb ? coh[v] - s_tab[k0v[v]].x : -1.0;
-                dd[v] = okb ? s_dm8[k0v[v] >> 3] - B : __builtin_nan("");
+                cx[v] = okb ? coh[v] - av[v] : -1.0;
+                dd[v] = okb ? dmv[v] - B : __builtin_nan("");
             }
             AIY_SCHED_BARRIER();
             screen_t<NP, VB>(tb, cx, dd);
             ntests += VB;  // (bound tests, counted per lane like the candidates)
+            if (TR) ++nrnd;
 #pragma unroll
             for (int v = 0; v < VB; ++v)
                 if (__any(tb[v] >= kThr)) block(lv[v], k0v[v], kev[v], coh[v], dis[v]);
@@ -328,18 +356,25 @@ __global__ __launch_bounds__(64 * NW) void bell_wide_kernel(
             const double dis = LAB ? s_dis[l] : 0.0;
             for (int kw = 8 * gw0; kw < kend; kw += VB * 8 * gstride) {  // (wave-uniform trips)
                 const double B = okj ? screen_B(best, idx, dis, NP) : __builtin_nan("");
-                double cx[VB], dd[VB], tb[VB];
+                double cx[VB], dd[VB], tb[VB], av[VB], dmv[VB];
                 int k0v[VB];
 #pragma unroll
-                for (int v = 0; v < VB; ++v) {
+                for (int v = 0; v < VB; ++v) {  // (reads first, clamped: one LDS wait)
                     k0v[v] = kw + v * 8 * gstride + 8 * qs;
+                    const int kc = min(k0v[v], Na - 1);
+                    av[v] = s_tab[kc].x;
+                    dmv[v] = s_dm8[kc >> 3];
+                }
+#pragma unroll
+                for (int v = 0; v < VB; ++v) {
                     const bool okb = k0v[v] < kend;
-                    cx[v] = okb ? coh - s_tab[k0v[v]].x : -1.0;
-                    dd[v] = okb ? s_dm8[k0v[v] >> 3] - B : __builtin_nan("");
+                    cx[v] = okb ? coh - av[v] : -1.0;
+                    dd[v] = okb ? dmv[v] - B : __builtin_nan("");
                 }
                 AIY_SCHED_BARRIER();
                 screen_t<NP, VB>(tb, cx, dd);
                 ntests += VB;
+                if (TR) ++nrnd;
 #pragma unroll
                 for (int v = 0; v < VB; ++v)
                     if (__any(tb[v] >= kThr)) block(l, k0v[v], kend, coh, dis);
@@ -351,6 +386,8 @@ __global__ __launch_bounds__(64 * NW) void bell_wide_kernel(
         long long* tr = A.trace + 64 * (size_t)blockIdx.x;
         tr[16 + 2 * wave] = tr_mark[3] - tr_mark[0];
         tr[17 + 2 * wave] = tr_mark[4] - tr_mark[0];
+        // its screen's work: bound-test rounds | entered 8-blocks << 16 | voted candidates << 32
+        tr[48 + wave] = (long long)nrnd | ((long long)nblk << 16) | ((long long)nvotes << 32);
     }
     if (A.hitcount) {  // instrumentation (aiy_ws_set_timing bit 1): exact evaluations, tests
         unsigned long long* hc = A.hitcount + 4 * (blockIdx.x % kDiffSlots);
@@ -444,8 +481,8 @@ __global__ __launch_bounds__(64 * NW) void bell_wide_kernel(
             const double kp = s_tab[k].x;
             A.idx[t] = q;
             if (A.pk) A.pk[t] = kp;
-            if (A.pc) A.pc[t] = cash<LAB>(x, y, LAB ? A.L[l] : 1.0) - kp;
-            if (LAB && A.pl) A.pl[t] = A.L[l];
+            if (A.pc) A.pc[t] = cash<LAB>(x, y, LAB ? s_L[l] : 1.0) - kp;
+            if (LAB && A.pl) A.pl[t] = s_L[l];
         }
         A.v_new[t] = bv;
         const double d = fabs(bv - vo);

@@ -27,7 +27,7 @@ LAB_GEOS = [(4, 8, 64), (1, 8, 16), (1, 8, 8), (1, 16, 16), (1, 16, 8), (2, 8, 1
             (4, 8, 16), (1, 4, 8)]
 
 
-def run(pkg, kind, Na, geo, n=50, warm=10, reps=3):
+def run(pkg, kind, Na, geo, n=50, warm=10, reps=3, excl=False):
     dev = torch.device("cuda:0")
     t = lambda x: torch.as_tensor(np.ascontiguousarray(x), device=dev)
     if kind == "a1":
@@ -42,6 +42,8 @@ def run(pkg, kind, Na, geo, n=50, warm=10, reps=3):
     w = pkg.calibration.wage(r, cal["alpha"], cal["delta"])
     a_t, s_t, P_t = t(cal["a_grid"]), t(cal["s"]), t(cal["P"])
     ws = pkg.Workspace(N, Na, Nl)
+    if excl:
+        ws.set_cu_exclusive(True)
     v = [torch.zeros((N, Na), dtype=torch.float64, device=dev) for _ in range(2)]
     idx = torch.zeros((N, Na), dtype=torch.int32, device=dev)
     pk, pl, pc = (torch.zeros((N, Na), dtype=torch.float64, device=dev) for _ in range(3))
@@ -111,6 +113,23 @@ def run(pkg, kind, Na, geo, n=50, warm=10, reps=3):
             rec["wave_bar_med"] = [int(x) for x in np.median(bars, axis=0)]
             rec["wave_screen_med"] = [int(x) for x in np.median(scr, axis=0)]
             rec["wave_screen_work_med"] = [int(x) for x in np.median(scr - bars, axis=0)]
+            # per wave: bound-test rounds, entered 8-blocks, voted candidates (words 48 + w);
+            # then the same for each block's slowest wave
+            wk = tr[:, 48:48 + nw]
+            rnd, blk, vot = wk & 0xffff, (wk >> 16) & 0xffff, wk >> 32
+            work = scr - bars
+            slow = np.argmax(work, axis=1)
+            rows = np.arange(len(tr))
+            rec["wave_work_med_max"] = {
+                "cycles": [int(np.median(work)), int(work.max())],
+                "rounds": [float(np.median(rnd)), int(rnd.max())],
+                "blocks": [float(np.median(blk)), int(blk.max())],
+                "votes": [float(np.median(vot)), int(vot.max())]}
+            rec["slowest_wave_med"] = {
+                "cycles": int(np.median(work[rows, slow])),
+                "rounds": float(np.median(rnd[rows, slow])),
+                "blocks": float(np.median(blk[rows, slow])),
+                "votes": float(np.median(vot[rows, slow]))}
             ph = {}
             for q, name in enumerate(("table_issued", "table_done", "bar", "screen_wave",
                                       "screen_all", "published", "outputs"), start=3):
@@ -133,6 +152,9 @@ def main():
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--flags", type=int, default=None, help="AIY_WIDE_FLAGS (A/B)")
     ap.add_argument("--cases", default=None, help="e.g. a1:400,lab:400")
+    ap.add_argument("--geos", default=None, help="e.g. 1,8,32;1,8,16 (instead of the lists)")
+    ap.add_argument("--excl", action="store_true", help="CU-exclusive sweep workgroups")
+    ap.add_argument("--no-tree", action="store_true", help="skip the tree reference runs")
     args = ap.parse_args()
     if args.flags is not None:
         import os
@@ -148,10 +170,15 @@ def main():
         for kind, Na in cases:
             ref, vref = run(pkg, kind, Na, None)
             ref["same"] = True
-            print(json.dumps(ref), flush=True)
-            f.write(json.dumps(ref) + "\n")
-            for geo in (A1_GEOS if kind == "a1" else LAB_GEOS):
-                rec, vv = run(pkg, kind, Na, geo)
+            if not args.no_tree:
+                print(json.dumps(ref), flush=True)
+                f.write(json.dumps(ref) + "\n")
+            geos = A1_GEOS if kind == "a1" else LAB_GEOS
+            if args.geos:
+                geos = [tuple(int(x) for x in g.split(",")) for g in args.geos.split(";")]
+            for geo in geos:
+                rec, vv = run(pkg, kind, Na, geo, excl=args.excl)
+                rec["excl"] = args.excl
                 rec["same"] = bool(np.array_equal(vv, vref))
                 rec["speedup_vs_tree"] = ref["us_per_sweep"] / rec["us_per_sweep"]
                 print(json.dumps(rec), flush=True)
