@@ -96,10 +96,12 @@ inline size_t bell_wide_lds(int Na, int S, int NW) {
     (void)NW;
     return (size_t)Na * 24 + ((size_t)Na + 7) / 8 * 8;
 }
-// flags (A/B only, results identical): kWideBatch = a block with >= 4 voted candidates
-// evaluates all eight as independent chains; kWideClimb = the bar climbs from the hint's window
-// (measured slower than the window alone, tools/wide_tune.py)
-constexpr int kWideBatch = 1, kWideClimb = 2;
+// flags (results identical): kWideBatch = a block with >= 4 voted candidates evaluates all
+// eight as independent chains, kWideBatch2 from 2 (the default: tools/wide_tune.py,
+// profiles/r05_g47_wide_flags.txt); kWideClimb = the bar climbs from the hint's window (measured
+// slower than the window alone)
+constexpr int kWideBatch = 1, kWideClimb = 2, kWideBatch2 = 4;
+constexpr int kWideDefaultFlags = kWideBatch2;
 constexpr int kWideMaxNl = 16;  // labour levels the small-grid sweep holds in registers
 // a workgroup asking for this much LDS has its CU to itself (160 KiB per CU on gfx950)
 constexpr size_t kExclusiveLds = 88 * 1024;

@@ -269,7 +269,8 @@ __global__ __launch_bounds__(64 * NW) void bell_wide_kernel(
 #pragma unroll
         for (int u = 0; u < 8; ++u) vote |= (__any(pk[u]) ? 1u : 0u) << u;
         nvotes += __builtin_popcount(vote);
-        if ((flags & kWideBatch) && __builtin_popcount(vote) >= 4) {
+        if ((flags & (kWideBatch | kWideBatch2)) &&
+            __builtin_popcount(vote) >= ((flags & kWideBatch2) ? 2 : 4)) {
             // many voted: all eight exact values as independent chains, then the ordered
             // merges; a candidate outside the feasible prefix (c <= 0) is NaN, as in the
             // reference (any exactly evaluated candidate may be merged)

@@ -422,7 +422,7 @@ static int bell_sweep_wide(aiy_ws* ws, BellArgs& A, int S, int NW, int SB, hipSt
     }
     const char* fl = getenv("AIY_WIDE_FLAGS");  // (A/B tooling: tools/wide_tune.py)
     AIY_TRY(ws_dispatch_arm(ws));
-    const int rc = launch_bell_wide(A, S, NW, SB, cur, ws->wcnt, ws->wpart, fl ? atoi(fl) : 0,
+    const int rc = launch_bell_wide(A, S, NW, SB, cur, ws->wcnt, ws->wpart, fl ? atoi(fl) : kWideDefaultFlags,
                                     ws->cu_exclusive ? kExclusiveLds : 0, st);
     ws_dispatch_commit(ws);
     AIY_TRY(rc);
