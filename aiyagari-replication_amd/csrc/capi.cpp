@@ -372,7 +372,10 @@ static bool wide_pick(const aiy_ws* ws, const BellArgs& A, int* S, int* NW, int*
     const int vmax = ws->wide_max >= 0 ? ws->wide_max : (A.labor ? 2048 : 1536);
     if (A.Na > vmax) return false;
     if (ws->variant >= 0 && !(ws->variant & (1 << 25))) return false;
-    const int sb = ws->wide_SB > 0 ? ws->wide_SB : (A.labor ? 16 : (A.Na <= 1024 ? 32 : 64));
+    // states per wave: labour 16 up to Na = 512, then 32 (profiles/r05_wide_ab.txt, r05_g52:
+    // Na = 1,000 30.8 -> 21.8 us, 2,000 69.9 -> 56.4); A1 32 up to 1,024, then 64
+    const int sb = ws->wide_SB > 0 ? ws->wide_SB
+                                   : (A.labor ? (A.Na <= 512 ? 16 : 32) : (A.Na <= 1024 ? 32 : 64));
     const int nw = ws->wide_NW > 0 ? ws->wide_NW : 8;
     const int s = ws->wide_S > 0 ? ws->wide_S : 1;
     if (bell_wide_lds(A.Na, s, nw) > kWideMaxLds) return false;
