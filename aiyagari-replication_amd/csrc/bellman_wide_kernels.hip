@@ -34,10 +34,10 @@
 namespace aiy {
 
 // the previous sweep's slot set: folded into fold[0..1] (reduce_slots_kernel's rule) when asked,
-// then cleared for the sweep after this one — wave 0 of block 0, each lane its own two words
+// then cleared for the sweep after this one — one wave of block 0, each lane its own two words
 __device__ __forceinline__ void wide_fold_clear(unsigned long long* __restrict__ old,
                                                 unsigned long long* __restrict__ fold) {
-    const int l = threadIdx.x;
+    const int l = threadIdx.x & 63;
     unsigned long long m = old[2 * l];
     const unsigned long long f = old[2 * l + 1];
     if (fold) {
@@ -65,6 +65,12 @@ __global__ __launch_bounds__(64 * NW) void bell_wide_kernel(
     __shared__ double s_L[kWideMaxNl], s_dis[kWideMaxNl];  // (labour) levels and disutilities
     const int lane = threadIdx.x & 63;
     const int wave = readfirst(threadIdx.x >> 6);
+    // every kernel argument the prologue and the bar read, in one batch of scalar loads (left to
+    // itself the compiler fetches them in dependent rounds, a wait each, as each use is reached)
+    asm volatile("" ::"s"(A.a), "s"(A.P), "s"(A.v_old), "s"(A.kf), "s"(A.hint), "s"(A.s),
+                 "s"(A.w), "s"(A.beta), "s"(A.r), "s"(A.N), "s"(A.Na), "s"(A.Nl), "s"(A.sigma),
+                 "s"(A.L), "s"(A.dis), "s"(A.trace), "s"(ntile), "s"(S), "s"(lsb), "s"(flags),
+                 "s"(old_slots), "s"(A.fold));
     // (instrumentation, aiy_ws_set_timing bit 2) wave 0's phase marks, one record per block
     const bool TR = A.trace != nullptr;
     long long tr_mark[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // (constant indices only: registers)
@@ -74,7 +80,6 @@ __global__ __launch_bounds__(64 * NW) void bell_wide_kernel(
         if (TR) tr_mark[q] = (long long)__builtin_amdgcn_s_memtime();           \
     } while (0)
     AIY_WMARK(0);
-    if (blockIdx.x == 0 && wave == 0 && old_slots) wide_fold_clear(old_slots, A.fold);
     // block → (tile item, split); the S splits of an item have equal blockIdx % 8 (one XCD under
     // round-robin placement: the partials' hand-off stays in one L2 — speed only)
     const int b = blockIdx.x;
@@ -413,6 +418,10 @@ __global__ __launch_bounds__(64 * NW) void bell_wide_kernel(
     s_best[wave][lane] = best;
     s_idx[wave][lane] = idx;
     __syncthreads();
+    // the previous sweep's slot set (not the one this sweep writes): folded and cleared by wave
+    // 1 of block 0 while wave 0 writes the outputs (at the start it held block 0's table loads
+    // back by a round trip)
+    if (blockIdx.x == 0 && wave == 1 && old_slots) wide_fold_clear(old_slots, A.fold);
     if (wave != 0) return;
     AIY_WMARK(5);  // [5] every wave's screen (barrier)
 #pragma unroll
