@@ -187,6 +187,9 @@ __global__ __launch_bounds__(1024) void dist_push_kernel(DistArgs A) {
     extern __shared__ double s_src[];  // [N][stage] λ, then [N][stage] weights (LOT)
     const int lane = threadIdx.x & 63;
     const int i = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // blockDim = 64·N
+    // every kernel argument in one batch of scalar loads (otherwise fetched in dependent rounds)
+    asm volatile("" ::"s"(A.N), "s"(A.Na), "s"(A.P), "s"(A.lam), "s"(A.off), "s"(A.wr),
+                 "s"(A.out), "s"(A.diff), "s"(A.stage), "s"(A.diff_clear), "s"(A.trace));
     const int N = A.N, Na = A.Na;
     const int k0 = blockIdx.x * 64, k = k0 + lane;
     double pm[kDistPushMaxN];  // column m = i of P (the projection's weights), loads first
