@@ -70,7 +70,8 @@ __global__ __launch_bounds__(64 * NW) void bell_wide_kernel(
     asm volatile("" ::"s"(A.a), "s"(A.P), "s"(A.v_old), "s"(A.kf), "s"(A.hint), "s"(A.s),
                  "s"(A.w), "s"(A.beta), "s"(A.r), "s"(A.N), "s"(A.Na), "s"(A.Nl), "s"(A.sigma),
                  "s"(A.L), "s"(A.dis), "s"(A.trace), "s"(ntile), "s"(S), "s"(lsb), "s"(flags),
-                 "s"(old_slots), "s"(A.fold));
+                 "s"(old_slots), "s"(A.fold), "s"(A.idx), "s"(A.pk), "s"(A.pc), "s"(A.v_new),
+                 "s"(A.diff));
     // (instrumentation, aiy_ws_set_timing bit 2) wave 0's phase marks, one record per block
     const bool TR = A.trace != nullptr;
     long long tr_mark[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // (constant indices only: registers)
