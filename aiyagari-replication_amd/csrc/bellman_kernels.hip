@@ -737,7 +737,9 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
     // compiler fetches them in dependent rounds as the control flow reaches each use)
     asm volatile("" ::"s"(A0.a), "s"(A0.Dt), "s"(A0.EV), "s"(A0.kf), "s"(A0.hint), "s"(A0.v_old),
                  "s"(A0.Dm512), "s"(A0.s), "s"(A0.r), "s"(A0.w), "s"(A0.N), "s"(A0.Na),
-                 "s"(A0.variant), "s"(A0.C), "s"(A0.nb512), "s"(A0.sigma), "s"(A0.trace));
+                 "s"(A0.variant), "s"(A0.C), "s"(A0.nb512), "s"(A0.sigma), "s"(A0.trace),
+                 "s"(A0.best0), "s"(A0.idx0), "s"(A0.tw), "s"(ntile), "s"(nblocks), "s"(A0.mom),
+                 "s"(A0.idx), "s"(A0.pk), "s"(A0.pc), "s"(A0.v_new), "s"(A0.diff));
     const long long t_boot = (INS && A0.trace) ? (long long)wall_clock64() : 0;  // (instrumentation)
     const long long c_boot = (INS && A0.trace) ? (long long)__builtin_amdgcn_s_memtime() : 0;
     int item = A0.perm ? A0.perm[block_id]
