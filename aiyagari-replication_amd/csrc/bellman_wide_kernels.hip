@@ -448,15 +448,21 @@ __global__ __launch_bounds__(64 * NW) void bell_wide_kernel(
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(pp + 2 * 64 * sp + 1, (unsigned long long)(long long)idx,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every partial store drained
+        // the partials are published by a release RMW on the tile's counter (the
+        // fence orders every lane's stores before lane 0's add) and the last arriver acquires
+        // before it reads them back — the memory model's order, not the hardware's
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         unsigned prev = 0;
-        if (lane == 0) prev = atomicAdd(cnt + item, 1u);
+        if (lane == 0)
+            prev = __hip_atomic_fetch_add(cnt + item, 1u, __ATOMIC_RELEASE,
+                                          __HIP_MEMORY_SCOPE_AGENT);
         prev = (unsigned)readlane_i((int)prev, 0);
         AIY_WMARK(6);  // [6] partials published
         if (prev != (unsigned)(S - 1)) {  // not the last split of this tile
             trace_out(0);
             return;
         }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every split's partial visible
         if (lane == 0)  // re-armed for the next sweep (read after this launch's boundary)
             __hip_atomic_store(cnt + item, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // every split's partial (own included: a repeat merges as a no-op), all loads in

@@ -1,7 +1,8 @@
 // One process per GPU, device memory and hand-off flags shared between the ranks of a node
 // (the KS direct schedule under torch.distributed, ks_dist.DirectPeers): IPC handles of the
-// ranks' column buffers, a host page mapped into every rank for the sweep counters, and the
-// stream-ordered wait / publish launches (ipc_kernels.hip).
+// ranks' column buffers, a host page mapped into every rank for the sweep counters, the
+// stream-ordered wait / publish launches (ipc_kernels.hip) and the staged sweeps, whose waits
+// and publishes run inside the sweep launch itself (ks_staged_sweep_kernel).
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -79,61 +80,35 @@ int aiy_flag_set(void* flags, int32_t slot, uint64_t value, void* stream) {
 }  // extern "C"
 
 extern "C" {
-// nsweeps Jacobi Howard sweeps of the direct schedule in one call (ks_dist.DirectPeers.sweeps):
-// sweep i reads parity p = parity ^ (i & 1) and writes parity p ^ 1, after the neighbours in
-// `mask` have published n0 + i, and publishes n0 + i + 1 in `slot`.  Staged: the forecast columns
-// peers own are read from a local halo, refreshed every sweep from the owners' buffers (device
-// pointer arrays src_p[q] -> dst[q], `col_bytes` each, q < ncopy; system-scope loads) by extra
-// block rows of the interior launch, so the copies run beside the interior columns; the
-// boundary columns sweep in the next launch.  The publish follows a
-// system-scope release of the sweep's writes (an event recorded with hipEventReleaseToSystem), so
-// a peer's copy after its wait reads this sweep's values from HBM, not from this device's L2.
-int ks_dev_direct_sweeps(ks_dev* h, const void* const* tab0, const void* const* tab1,
-                         double* V0, double* V1, double* dV0, double* dV1, double* kopt,
-                         int32_t parity, int64_t nsweeps, const void* const* src0,
-                         const void* const* src1, void* const* dst, int32_t ncopy,
-                         int64_t col_bytes, void* flags, int32_t slot, uint64_t mask, uint64_t n0,
-                         double timeout_s, void* err, void* stream, void* copy_stream) {
-    if (!h || !tab0 || !tab1 || !V0 || !V1 || !dV0 || !dV1 || !kopt || !flags || !err ||
-        nsweeps < 0 || (parity & ~1) || ncopy < 0 || (ncopy && (!src0 || !src1 || !dst)) ||
-        (ncopy && (!copy_stream || col_bytes <= 0 || col_bytes % 8)))
+// nsweeps Jacobi Howard sweeps of the direct schedule in one call (ks_dist.DirectPeers.sweeps),
+// ONE launch per sweep (ks_dev_staged_sweep) on three buffers per rank: version v lives in
+// buffer (v - 1) mod 3, so sweep i reads version n0 + i in buffer b = (cur + i) mod 3 (column
+// table tabs[b]) and writes buffer (b + 1) mod 3, which its neighbours last read at version
+// n0 + i - 2.  The launch publishes n0 + i (its predecessor's version) first,
+// copies the peers' forecast columns of version n0 + i (srcs[b][q] -> dst[q], device pointer
+// arrays) once the neighbours in `mask` have published it, sweeps the interior columns without
+// waiting and the boundary columns after the copies; a last one-wave launch publishes
+// n0 + nsweeps.  tabs, V, dV and srcs are host arrays of three device pointers.
+int ks_dev_direct_sweeps(ks_dev* h, void* const* tabs, double* const* V, double* const* dV,
+                         double* kopt, int32_t cur, int64_t nsweeps, void* const* srcs,
+                         void* const* dst, int32_t ncopy, int64_t col_bytes, void* flags,
+                         int32_t slot, uint64_t mask, uint64_t n0, double timeout_s, void* err,
+                         void* stream) {
+    if (!h || !tabs || !V || !dV || !kopt || !flags || !err || nsweeps < 0 || cur < 0 || cur > 2 ||
+        ncopy < 0 || (ncopy && (!srcs || !dst || col_bytes <= 0 || col_bytes % 8)))
         return fail(AIY_BAD_ARG, "bad argument");
-    const void* const* tab[2] = {tab0, tab1};
-    const void* const* src[2] = {src0, src1};
-    double* V[2] = {V0, V1};
-    double* dV[2] = {dV0, dV1};
-    hipStream_t st = (hipStream_t)stream;
-    (void)copy_stream;  // (the copies now run inside the interior launch)
-    hipEvent_t ev_rel = nullptr;
-    int rc = AIY_OK;
-    auto done = [&](int r) {
-        if (ev_rel) (void)hipEventDestroy(ev_rel);
-        return r;
-    };
-#define DS_TRY(x)                   \
-    do {                            \
-        rc = (x);                   \
-        if (rc != AIY_OK) return done(rc); \
-    } while (0)
-    {
-        const hipError_t e = hipEventCreateWithFlags(&ev_rel, hipEventDisableTiming | hipEventReleaseToSystem);
-        if (e != hipSuccess) return fail(AIY_HIP_ERROR, "hipEventCreateWithFlags: %s", hipGetErrorString(e));
-    }
+    for (int b = 0; b < 3; ++b)
+        if (!tabs[b] || !V[b] || !dV[b] || (ncopy && !srcs[b])) return fail(AIY_BAD_ARG, "NULL buffer");
     for (int64_t i = 0; i < nsweeps; ++i) {
-        const int p = parity ^ (int)(i & 1);
-        DS_TRY(aiy_flags_wait(flags, mask, n0 + (uint64_t)i, timeout_s, err, stream));
-        DS_TRY(ks_dev_set_columns(h, tab[p]));
-        // interior columns + the halo copy rows in one launch, then the boundary columns
-        DS_TRY(ks_dev_howard_fused_part_halo(h, 0, V[p], dV[p], kopt, V[p ^ 1], dV[p ^ 1],
-                                             ncopy ? src[p] : nullptr, ncopy ? dst : nullptr,
-                                             ncopy, stream));
-        DS_TRY(ks_dev_howard_fused_part(h, 1, V[p], dV[p], kopt, V[p ^ 1], dV[p ^ 1], stream));
-        const hipError_t e = hipEventRecord(ev_rel, st);  // system-scope release before the publish
-        if (e != hipSuccess) return done(fail(AIY_HIP_ERROR, "hipEventRecord: %s", hipGetErrorString(e)));
-        DS_TRY(aiy_flag_set(flags, slot, n0 + (uint64_t)i + 1, stream));
+        const int b = (int)((cur + i) % 3), bo = (b + 1) % 3;
+        const uint64_t v = n0 + (uint64_t)i;
+        AIY_TRY(ks_dev_set_columns(h, reinterpret_cast<const void* const*>(tabs[b])));
+        AIY_TRY(ks_dev_staged_sweep(h, V[b], dV[b], kopt, V[bo], dV[bo],
+                                    ncopy ? reinterpret_cast<const void* const*>(srcs[b]) : nullptr,
+                                    ncopy ? dst : nullptr, ncopy, flags, mask, v, slot, v,
+                                    timeout_s, err, stream));
     }
-#undef DS_TRY
-    return done(AIY_OK);
+    return aiy_flag_set(flags, slot, n0 + (uint64_t)nsweeps, stream);
 }
 
 // the halo refresh alone (before an improvement): the same copies, stream-ordered

@@ -6,39 +6,17 @@
 #include <hip/hip_runtime.h>
 
 #include "aiy_common.hpp"
+#include "ipc_dev.hpp"
 
 namespace aiy {
-constexpr int kFlagStride = 16;  // slots 128 B apart (one cache line each)
 
-// lanes q with bit q of `mask` set poll slot q until it reaches v; a wave that sees no progress
-// for `timeout_ticks` of the 100 MHz wall clock sets *err and leaves (a dead neighbour must not
-// hang the device: the host checks err and aborts the solve)
+// lanes q with bit q of `mask` set poll slot q until it reaches v (wave_wait_flags)
 __global__ __launch_bounds__(64) void flags_wait_kernel(const unsigned long long* flags,
                                                         unsigned long long mask,
                                                         unsigned long long v,
                                                         long long timeout_ticks,
                                                         unsigned long long* err) {
-    const int q = threadIdx.x;
-    // an earlier wait of this rank already timed out: the schedule is void, do not wait again
-    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0ull) return;
-    const bool mine = (mask >> q) & 1ull;
-    const long long t0 = (long long)wall_clock64();
-    bool ok = !mine;
-    while (!__all(ok)) {
-        if (!ok) {
-            const unsigned long long f = __hip_atomic_load(flags + (size_t)q * kFlagStride,
-                                                           __ATOMIC_ACQUIRE,
-                                                           __HIP_MEMORY_SCOPE_SYSTEM);
-            ok = f >= v;
-        }
-        if ((long long)wall_clock64() - t0 > timeout_ticks) {
-            if (!ok)
-                __hip_atomic_store(err, 1ull + (unsigned long long)q, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
-            break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-    }
+    wave_wait_flags(flags, mask, v, timeout_ticks, err);
 }
 
 // slot `q` := v once every earlier operation on the stream has completed (the stream order puts

@@ -30,15 +30,39 @@ struct KsArgs {
     // the launch's own V / dV arrays
     const double* const* colV;
     const double* const* coldV;
-    // staged direct schedule: the fused Howard launch runs the columns col_list[0 .. n_list)
-    // (interior or boundary subset of the shard's own columns) instead of the node range
+    // staged direct schedule, ONE launch per sweep (ks_dev_staged_sweep): block
+    // rows [0, n_copy_rows) copy halo column q from halo_src[q] (a peer's buffer: system-scope
+    // loads, after the wait below) to halo_dst[q] (n_copy_rows = n_halo; one wait-only row when
+    // n_halo == 0 but wait_mask != 0); then the interior columns col_list[0 .. n_list); then the
+    // boundary columns bnd_list[0 .. n_bnd), which wait in-kernel for every copy block
     const int* col_list;
     int n_list;
-    // ... and, in the same launch, n_halo extra block rows copy halo column q from halo_src[q]
-    // (a peer's buffer: system-scope loads) to halo_dst[q]
+    const int* bnd_list;
+    int n_bnd;
     const double* const* halo_src;
     double* const* halo_dst;
     int n_halo;
+    int n_copy_rows;
+    int copy_x;  // working copy blocks per copy row (the rest of the row returns at once)
+    // copy rows wait until every slot q in wait_mask holds >= wait_v (host page, system scope;
+    // timeout -> *err = 1 + q); null wait_flags: no wait
+    const unsigned long long* wait_flags;
+    unsigned long long wait_mask, wait_v;
+    long long timeout_ticks;
+    unsigned long long* err;
+    // each working copy block adds 1 (agent scope, after its stores); boundary blocks start once
+    // *copy_cnt >= copy_target (monotonic across launches; the host keeps the running total)
+    unsigned long long* copy_cnt;
+    unsigned long long copy_target;
+    // block (0, 0) stores go_token (a per-handle launch sequence number, strictly increasing)
+    // here once the neighbours' slots allow it; the other copy blocks poll it (one poller of the
+    // host page per launch)
+    unsigned long long* go;
+    unsigned long long go_token;
+    // the launch's first block stores pub_v into *pub_flag (system-scope release) before anything
+    // else: the PREVIOUS launch on the stream (the sweep that produced version pub_v) is complete
+    unsigned long long* pub_flag;
+    unsigned long long pub_v;
 };
 struct KsParams {  // the 13-double parameter block, in order
     double beta, alpha, delta, k_min, k_max, ug, ub, l_bar, mu, z1, z2, e1, e2;
@@ -65,6 +89,11 @@ int launch_ks_halo_copy(const double* const* src, double* const* dst, int ncols,
                         hipStream_t st);
 int launch_ks_howard_slopes(const KsArgs& A, const double* V, const double* dV,
                             const double* kopt, double* Vn, double* dVn, hipStream_t st);
+// the staged direct schedule's one launch per sweep (ks_staged_sweep_kernel); the working copy
+// blocks per copy row (what each copy row adds to copy_cnt)
+int launch_ks_staged_sweep(const KsArgs& A, const double* V, const double* dV,
+                           const double* kopt, double* Vn, double* dVn, hipStream_t st);
+int ks_staged_copy_blocks(int nk);
 int launch_ks_hints(const KsArgs& A, const double* kopt, hipStream_t st);
 int launch_ks_reldiff(const KsArgs& A, const double* V, const double* Vold,
                       unsigned long long* slots, hipStream_t st);

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -42,6 +43,11 @@ struct ks_dev {
     int* cols_int = nullptr;
     int* cols_bnd = nullptr;
     int n_int = 0, n_bnd = 0;
+    // staged sweeps: the copy blocks' arrival counter (device; [1]: the launch's go word) and
+    // its running total (host)
+    unsigned long long* copy_cnt = nullptr;
+    unsigned long long copy_total = 0;
+    unsigned long long launches = 0;  // staged launches so far (the go word's tokens)
 };
 
 namespace aiy {
@@ -78,7 +84,7 @@ int ks_dev_destroy(ks_dev* h) {
                     "destroy them first", h->sharers);
     if (h->seg_owner) h->seg_owner->sharers--;
     void* ps[] = {h->kg, h->P, h->sl, h->dV, h->cols, h->own_cols, h->slots,
-                  h->seg_owner ? nullptr : h->seg, h->cols_int, h->cols_bnd};
+                  h->seg_owner ? nullptr : h->seg, h->cols_int, h->cols_bnd, h->copy_cnt};
     for (void* q : ps)
         if (q) (void)hipFree(q);
     delete h;
@@ -139,6 +145,8 @@ int ks_dev_create_slice(const double* k_grid, const double* K_grid, const double
     if (e == hipSuccess) e = hipMalloc((void**)&h->slots, 2 * kDiffSlots * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMalloc((void**)&h->seg, n * sizeof(int));
     if (e == hipSuccess) e = hipMemset(h->seg, 0, n * sizeof(int));
+    if (e == hipSuccess) e = hipMalloc((void**)&h->copy_cnt, 2 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(h->copy_cnt, 0, 2 * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemcpy(h->kg, k_grid, nk * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->P, Pr, sizeof Pr, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->sl, sl.data(), sl.size() * sizeof(KsSlice), hipMemcpyHostToDevice);
@@ -238,32 +246,68 @@ int ks_dev_set_split(ks_dev* h, const int32_t* interior, int32_t n_int, const in
 // the fused Howard sweep over one subset of the own columns (0 = interior, 1 = boundary)
 int ks_dev_howard_fused_part(ks_dev* h, int part, const double* V, const double* dV,
                              const double* kopt, double* Vout, double* dVout, void* stream) {
-    return ks_dev_howard_fused_part_halo(h, part, V, dV, kopt, Vout, dVout, nullptr, nullptr, 0,
-                                         stream);
-}
-// ... with `n_halo` halo columns copied (src[q] -> dst[q], device pointer arrays, system-scope
-// loads) by extra block rows of the same launch
-int ks_dev_howard_fused_part_halo(ks_dev* h, int part, const double* V, const double* dV,
-                                  const double* kopt, double* Vout, double* dVout,
-                                  const void* const* src, void* const* dst, int32_t n_halo,
-                                  void* stream) {
-    if (!h || !V || !dV || !kopt || !Vout || !dVout || (part & ~1) || n_halo < 0 ||
-        (n_halo && (!src || !dst)))
+    if (!h || !V || !dV || !kopt || !Vout || !dVout || (part & ~1))
         return fail(AIY_BAD_ARG, "bad argument");
-    if (h->n_int + h->n_bnd == 0) {  // no split set: part 0 is the whole shard, part 1 nothing
-        if (n_halo) return fail(AIY_BAD_ARG, "halo copies need ks_dev_set_split");
+    if (V == Vout || dV == dVout)
+        return fail(AIY_BAD_ARG, "Howard sweeps are Jacobi: V/Vout and dV/dVout must differ");
+    if (h->n_int + h->n_bnd == 0)  // no split set: part 0 is the whole shard, part 1 nothing
         return part ? AIY_OK : ks_dev_howard_fused(h, V, dV, kopt, Vout, dVout, stream);
-    }
     KsArgs A = shard_args(h);
     A.col_list = part ? h->cols_bnd : h->cols_int;
     A.n_list = part ? h->n_bnd : h->n_int;
-    // an empty list stays in list mode (the launch may be copy rows only): any non-null pointer
-    if (!A.col_list) A.col_list = h->own_cols;
+    return launch_ks_staged_sweep(A, V, dV, kopt, Vout, dVout, (hipStream_t)stream);
+}
+
+// The staged direct schedule's whole sweep in ONE launch (ks_staged_sweep_kernel): publish
+// pub_v in slot `slot` of `flags` first (the previous launch on the stream produced it), copy
+// the n_halo peer columns src[q] -> dst[q] (device pointer arrays) once the slots in `mask` hold
+// >= wait_v, sweep the interior columns meanwhile and the boundary columns after the copies.
+// flags = NULL: no publish and no wait (one process; the tests' single-launch checks).
+int ks_dev_staged_sweep(ks_dev* h, const double* V, const double* dV, const double* kopt,
+                        double* Vout, double* dVout, const void* const* src, void* const* dst,
+                        int32_t n_halo, void* flags, uint64_t mask, uint64_t wait_v, int32_t slot,
+                        uint64_t pub_v, double timeout_s, void* err, void* stream) {
+    if (!h || !V || !dV || !kopt || !Vout || !dVout || n_halo < 0 || (n_halo && (!src || !dst)) ||
+        (flags && (!err || !(timeout_s > 0) || slot < 0 || slot >= 64)))
+        return fail(AIY_BAD_ARG, "bad argument");
+    if (V == Vout || dV == dVout)
+        return fail(AIY_BAD_ARG, "Howard sweeps are Jacobi: V/Vout and dV/dVout must differ");
+    if (h->n_int + h->n_bnd == 0) return fail(AIY_BAD_ARG, "staged sweeps need ks_dev_set_split");
+    if (n_halo && !h->n_bnd)
+        return fail(AIY_BAD_ARG, "halo columns without boundary columns (ks_dev_set_split)");
+    KsArgs A = shard_args(h);
+    // empty lists are fine here (the rows are counted, not inferred from a null pointer): a
+    // shard with no interior column is all copy and boundary rows (the r05 g37 case)
+    A.col_list = h->cols_int;
+    A.n_list = h->n_int;
+    A.bnd_list = h->cols_bnd;
+    A.n_bnd = h->n_bnd;
     A.halo_src = reinterpret_cast<const double* const*>(src);
     A.halo_dst = reinterpret_cast<double* const*>(dst);
     A.n_halo = n_halo;
-    if (!A.n_list && !n_halo) return AIY_OK;
-    return launch_ks_howard_slopes(A, V, dV, kopt, Vout, dVout, (hipStream_t)stream);
+    const bool waits = flags && mask;
+    A.n_copy_rows = n_halo ? n_halo : (waits ? 1 : 0);
+    A.copy_x = n_halo ? ks_staged_copy_blocks(h->nk) : 1;
+    if (waits) {
+        A.wait_flags = (const unsigned long long*)flags;
+        A.wait_mask = mask;
+        A.wait_v = wait_v;
+        A.timeout_ticks = (long long)(timeout_s * 1e8);
+        A.err = (unsigned long long*)err;
+    }
+    if (flags) {
+        A.pub_flag = (unsigned long long*)flags + (size_t)slot * 16;
+        A.pub_v = pub_v;
+    }
+    A.copy_cnt = h->copy_cnt;
+    A.go = h->copy_cnt + 1;
+    A.go_token = h->launches + 1;
+    const unsigned long long add = (unsigned long long)n_halo * (unsigned long long)A.copy_x;
+    A.copy_target = h->copy_total + add;
+    AIY_TRY(launch_ks_staged_sweep(A, V, dV, kopt, Vout, dVout, (hipStream_t)stream));
+    h->copy_total += add;
+    h->launches += 1;
+    return AIY_OK;
 }
 
 // the slopes of the shard's own columns of V into dV (the start of a direct schedule)

@@ -22,6 +22,7 @@
 
 #include "aiy_common.hpp"
 #include "ks.hpp"
+#include "ipc_dev.hpp"
 #include "pchip_dev.hpp"
 
 namespace aiy {
@@ -45,6 +46,7 @@ __device__ __forceinline__ int seg_hinted_dev(const double* __restrict__ x, int 
     return seg_of_dev(x, n, q);
 }
 
+template <bool SC1 = false>
 __device__ __forceinline__ double ks_bellman_dev(const KsArgs& A, const KsView& W,
                                                  const KsSlice& sl, int si, double k, double kp,
                                                  int hint = -1) {
@@ -58,7 +60,7 @@ __device__ __forceinline__ double ks_bellman_dev(const KsArgs& A, const KsView& 
         const size_t col = (size_t)c * nk;
         const double* Vc = A.colV ? A.colV[c] : W.V + col;
         const double* dVc = A.colV ? A.coldV[c] : W.dV + col;
-        expec = expec + A.P[si * 4 + sn] * pchip_at(W.kg, Vc, dVc, seg, kq);
+        expec = expec + A.P[si * 4 + sn] * pchip_at<SC1>(W.kg, Vc, dVc, seg, kq);
     }
     double c = (sl.a1 * k + sl.a2) - kp;
     c = fmax(c, 1e-10);
@@ -222,6 +224,35 @@ __global__ void ks_howard_kernel(KsArgs A, const double* __restrict__ V,
     }
 }
 
+// Copy of one halo column share: elements i0, i0 + step, ... < n from a peer's buffer (system-
+// scope loads: served by the owner's memory) to this device.  Eight loads per thread in flight
+// before the stores (global_ address space, so no flat instructions).
+template <bool SC1 = false>
+__device__ __forceinline__ void halo_copy_share(const double* src, double* dst, int i0, int step,
+                                                int n) {
+    using gu64 = __attribute__((address_space(1))) unsigned long long;
+    const gu64* s = (const gu64*)(const void*)src;
+    gu64* d = (gu64*)(void*)dst;
+    for (int b = i0; b < n; b += 8 * step) {
+        unsigned long long u[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int i = b + j * step;
+            u[j] = i < n ? __hip_atomic_load(s + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int i = b + j * step;
+            if (i < n) {
+                if constexpr (SC1)  // write-through: the in-kernel consumer reads it sc1
+                    __hip_atomic_store(d + i, u[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else
+                    d[i] = u[j];
+            }
+        }
+    }
+}
+
 // Howard sweep + the NEXT sweep's pchip slopes in one launch (the .Values refresh of
 // :186-191 fused into the sweep that produces the values).  A block owns O consecutive k
 // nodes of a column and evaluates the sweep on [q0 − 2, q0 + O + 2) (the neighbours the
@@ -230,15 +261,11 @@ __global__ void ks_howard_kernel(KsArgs A, const double* __restrict__ V,
 // ks_howard_kernel + ks_slopes_kernel, so bit for bit the two-launch sweep.  Columns of
 // length <= blockDim are one block each (O = nk: nothing evaluated twice); longer columns
 // evaluate 4 of every 256 nodes twice.
-// LIST: the staged direct schedule's launches (a column list, halo copy rows, write-through
-// stores); the node-range instantiation is the plain sweep.
-template <bool LIST>
-__global__ __launch_bounds__(256) void ks_howard_slopes_kernel(KsArgs A, const double* __restrict__ V,
-                                                               const double* __restrict__ dV,
-                                                               const double* __restrict__ k_opt,
-                                                               double* __restrict__ Vn,
-                                                               double* __restrict__ dVn, int O) {
-    __shared__ double s_v[256];
+template <bool WT, bool SC1 = false>
+__device__ __forceinline__ void howard_slopes_col(const KsArgs& A, const KsView& W, int col,
+                                                  const double* __restrict__ k_opt,
+                                                  double* __restrict__ Vn,
+                                                  double* __restrict__ dVn, double* s_v, int O) {
     const int nk = A.nk;
     const int q0 = blockIdx.x * O;
     const int lo = q0 >= 2 ? q0 - 2 : 0;
@@ -246,52 +273,127 @@ __global__ __launch_bounds__(256) void ks_howard_slopes_kernel(KsArgs A, const d
     const int hi = min(nk, q0 + O + 2);
     const int q = lo + (int)threadIdx.x;
     const bool comp = q < hi, mine = q >= q0 && q < own_hi;
-    if (LIST && (int)blockIdx.y >= A.n_list) {  // a halo copy row (staged schedule)
-        const int hq = (int)blockIdx.y - A.n_list;
-        const double* src = A.halo_src[hq];
-        double* dst = A.halo_dst[hq];
-        for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nk; i += gridDim.x * blockDim.x) {
-            const unsigned long long u = __hip_atomic_load(
-                reinterpret_cast<const unsigned long long*>(src + i), __ATOMIC_RELAXED,
-                __HIP_MEMORY_SCOPE_SYSTEM);
-            dst[i] = __builtin_bit_cast(double, u);
-        }
-        return;  // (block-uniform: no barrier below is skipped by part of a block)
-    }
-    const int col0 = A.node0 / nk + (int)blockIdx.z * (A.sstride / nk);  // block-uniform
-    const int ncl = LIST ? A.n_list : A.n_local / nk;
-    KsView W{A.k_grid, V, dV};
     const double k = comp ? W.kg[q] : 0.0;
     const LdsCol yl{s_v, lo};
-    for (int y = blockIdx.y; y < ncl; y += gridDim.y) {  // block-uniform trip count
-        const int col = LIST ? A.col_list[y] : col0 + y;
-        const int si = col / A.nK;
-        const size_t n = (size_t)col * nk + q;
-        double v = 0.0;
-        if (comp) {
-            const KsSlice sl = A.slice[col];
-            v = ks_bellman_dev(A, W, sl, si, k, k_opt[n], A.seg_hint ? A.seg_hint[n] : -1);
+    const int si = col / A.nK;
+    const size_t n = (size_t)col * nk + q;
+    double v = 0.0;
+    if (comp) {
+        const KsSlice sl = A.slice[col];
+        v = ks_bellman_dev<SC1>(A, W, sl, si, k, k_opt[n], A.seg_hint ? A.seg_hint[n] : -1);
+    }
+    s_v[threadIdx.x] = v;
+    __syncthreads();
+    if (mine) {
+        const double d = pchip_slope_t(A.k_grid, yl, nk, q);
+        if (WT) {  // staged direct schedule: peers copy these columns once the next launch has
+            // published — stored write-through (system-scope vector stores), so they are in
+            // memory when this kernel ends
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(Vn + n),
+                               __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(dVn + n),
+                               __builtin_bit_cast(unsigned long long, d), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        } else {
+            Vn[n] = v;
+            dVn[n] = d;
         }
-        s_v[threadIdx.x] = v;
-        __syncthreads();
-        if (mine) {
-            const double d = pchip_slope_t(A.k_grid, yl, nk, q);
-            if (LIST) {  // staged direct schedule: peers copy these columns after the
-                // publish — write them through to memory (system-scope vector stores), so the
-                // system-scope release before the publish has little left to flush
-                __hip_atomic_store(reinterpret_cast<unsigned long long*>(Vn + n),
-                                   __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
-                __hip_atomic_store(reinterpret_cast<unsigned long long*>(dVn + n),
-                                   __builtin_bit_cast(unsigned long long, d), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
-            } else {
-                Vn[n] = v;
-                dVn[n] = d;
+    }
+    __syncthreads();
+}
+
+// the node-range sweep (x: k tile, y: column of an s block, grid-stride; z: s block)
+__global__ __launch_bounds__(256) void ks_howard_slopes_kernel(KsArgs A, const double* __restrict__ V,
+                                                               const double* __restrict__ dV,
+                                                               const double* __restrict__ k_opt,
+                                                               double* __restrict__ Vn,
+                                                               double* __restrict__ dVn, int O) {
+    __shared__ double s_v[256];
+    const int col0 = A.node0 / A.nk + (int)blockIdx.z * (A.sstride / A.nk);  // block-uniform
+    const int ncl = A.n_local / A.nk;
+    const KsView W{A.k_grid, V, dV};
+    for (int y = blockIdx.y; y < ncl; y += gridDim.y)  // block-uniform trip count
+        howard_slopes_col<false>(A, W, col0 + y, k_opt, Vn, dVn, s_v, O);
+}
+
+// The staged direct schedule's sweep: ONE launch per sweep.
+// Block rows, in dispatch order:
+//   copy rows      [0, n_copy_rows): block (0, 0) waits (one wave) for the neighbours' slots
+//                  >= wait_v in the host page — the versions this sweep reads — and passes that
+//                  on through a device word (`go`); the other copy blocks poll the device word.
+//                  Then each copies its share of halo column q from the owner's buffer (system-
+//                  scope loads) with sc1 stores and adds 1 to copy_cnt (the guide's first-row
+//                  hand-off: every storing wave waits for its stores, a barrier, one lane's
+//                  agent-scope add).  With no halo but neighbours: one wait-only row.
+//   interior rows  col_list: columns whose four forecast columns are all own — no wait at all.
+//   boundary rows  bnd_list: thread 0 polls copy_cnt (sc1 loads) up to copy_target, a barrier,
+//                  then the sweep reads every column with sc1 loads (no L1 line from an older
+//                  halo can serve them).
+// Block (0, 0) first publishes pub_v (the previous launch on the stream, which produced version
+// pub_v, has completed; its write-through stores are in memory) with a system-scope release.
+// Copy rows come first so that the copies start with the launch; boundary rows last, so a
+// spinning boundary block never holds back the dispatch of a block it waits for (blocks of one
+// XCD are dispatched in order; copy blocks wait only on other ranks) — and measured: boundary
+// rows right after the copy rows spin while the copies run and hold slots the interior needs
+// (one-GPU model, worst shard: 54.8 vs 30.9 us per sweep, profiles/r06_g03_ks_staged_probe.txt).  Write-after-read on the
+// three buffers (ks_dev_direct_sweeps): a launch writes the buffer its neighbours read two
+// versions ago, and they published that they had finished with it before this launch's
+// predecessor's copy rows could pass their wait — so the interior rows need no wait.
+constexpr int kCopyX = 16;  // working copy blocks per copy row (strided copy)
+__global__ __launch_bounds__(256) void ks_staged_sweep_kernel(KsArgs A, const double* __restrict__ V,
+                                                              const double* __restrict__ dV,
+                                                              const double* __restrict__ k_opt,
+                                                              double* __restrict__ Vn,
+                                                              double* __restrict__ dVn, int O) {
+    __shared__ double s_v[256];
+    const int tid = threadIdx.x;
+    const bool first = blockIdx.x == 0 && blockIdx.y == 0;
+    if (A.pub_flag && first && tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(A.pub_flag, A.pub_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    int y = blockIdx.y;
+    if (y < A.n_copy_rows) {  // a copy (or wait-only) row: block-uniform branch
+        if ((int)blockIdx.x >= A.copy_x) return;
+        if (A.wait_flags) {
+            if (first) {  // the one poller of the host page
+                if (tid < 64) {
+                    wave_wait_flags(A.wait_flags, A.wait_mask, A.wait_v, A.timeout_ticks, A.err);
+                    if (tid == 0)
+                        __hip_atomic_store(A.go, A.go_token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            } else if (A.n_halo > 0 && tid == 0) {
+                while (__hip_atomic_load(A.go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < A.go_token)
+                    __builtin_amdgcn_s_sleep(4);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: peers' data
             }
+            __syncthreads();
         }
+        if (A.n_halo == 0) return;
+        halo_copy_share<true>(A.halo_src[y], A.halo_dst[y], blockIdx.x * blockDim.x + tid,
+                              A.copy_x * (int)blockDim.x, A.nk);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its stores done
+        __syncthreads();
+        if (tid == 0)
+            __hip_atomic_fetch_add(A.copy_cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    y -= A.n_copy_rows;
+    const KsView W{A.k_grid, V, dV};
+    if (y < A.n_list) {
+        howard_slopes_col<true, false>(A, W, A.col_list[y], k_opt, Vn, dVn, s_v, O);
+        return;
+    }
+    if (A.n_halo > 0) {  // wait for every copy block of this launch
+        if (tid == 0)
+            while (__hip_atomic_load(A.copy_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                   A.copy_target)
+                __builtin_amdgcn_s_sleep(8);
         __syncthreads();
     }
+    howard_slopes_col<true, true>(A, W, A.bnd_list[y - A.n_list], k_opt, Vn, dVn, s_v, O);
 }
 
 // The staged direct schedule's halo refresh: column q (nk doubles) from src[q] (a peer's buffer,
@@ -301,14 +403,8 @@ __global__ __launch_bounds__(256) void ks_howard_slopes_kernel(KsArgs A, const d
 __global__ __launch_bounds__(256) void ks_halo_copy_kernel(const double* const* __restrict__ src,
                                                            double* const* __restrict__ dst,
                                                            int nk) {
-    const double* s = src[blockIdx.y];
-    double* d = dst[blockIdx.y];
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < nk; i += gridDim.x * 256) {
-        const unsigned long long u = __hip_atomic_load(
-            reinterpret_cast<const unsigned long long*>(s + i), __ATOMIC_RELAXED,
-            __HIP_MEMORY_SCOPE_SYSTEM);
-        d[i] = __builtin_bit_cast(double, u);
-    }
+    halo_copy_share(src[blockIdx.y], dst[blockIdx.y], blockIdx.x * 256 + threadIdx.x,
+                    gridDim.x * 256, nk);
 }
 int launch_ks_halo_copy(const double* const* src, double* const* dst, int ncols, int nk,
                         hipStream_t st) {
@@ -502,20 +598,39 @@ int launch_ks_howard(const KsArgs& A, const double* V, const double* dV, const d
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }
+static int ks_fused_geometry(int nk, int* B) {
+    *B = (int)ks_col_block(nk).x;  // 64 .. 256
+    return nk <= *B ? nk : *B - 4;
+}
 int launch_ks_howard_slopes(const KsArgs& A, const double* V, const double* dV,
                             const double* kopt, double* Vn, double* dVn, hipStream_t st) {
     if (A.node0 % A.nk || A.n_local % A.nk || (A.ns > 1 && A.sstride % A.nk))
         return fail(AIY_BAD_SHAPE, "Howard launch: node range must be whole columns");
-    const int B = (int)ks_col_block(A.nk).x;  // 64 .. 256
-    const int O = A.nk <= B ? A.nk : B - 4;
-    if (A.col_list && A.n_list + A.n_halo > 65535)
-        return fail(AIY_BAD_SHAPE, "Howard launch: at most 65,535 listed + halo columns");
-    const dim3 g(cdiv(A.nk, O),
-                 (unsigned)std::max(1, A.col_list ? A.n_list + A.n_halo
-                                                  : std::min(A.n_local / A.nk, 65535)),
-                 A.col_list ? 1 : std::max(A.ns, 1));
-    if (A.col_list) ks_howard_slopes_kernel<true><<<g, B, 0, st>>>(A, V, dV, kopt, Vn, dVn, O);
-    else ks_howard_slopes_kernel<false><<<g, B, 0, st>>>(A, V, dV, kopt, Vn, dVn, O);
+    int B;
+    const int O = ks_fused_geometry(A.nk, &B);
+    const dim3 g(cdiv(A.nk, O), (unsigned)std::max(1, std::min(A.n_local / A.nk, 65535)),
+                 std::max(A.ns, 1));
+    ks_howard_slopes_kernel<<<g, B, 0, st>>>(A, V, dV, kopt, Vn, dVn, O);
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
+}
+int ks_staged_copy_blocks(int nk) {
+    int B;
+    const int O = ks_fused_geometry(nk, &B);
+    return std::min(cdiv(nk, O), kCopyX);
+}
+int launch_ks_staged_sweep(const KsArgs& A, const double* V, const double* dV,
+                           const double* kopt, double* Vn, double* dVn, hipStream_t st) {
+    int B;
+    const int O = ks_fused_geometry(A.nk, &B);
+    const long long rows = (long long)A.n_copy_rows + A.n_list + A.n_bnd;
+    if (rows > 65535) return fail(AIY_BAD_SHAPE, "staged sweep: at most 65,535 block rows");
+    if (rows == 0) return AIY_OK;
+    if ((A.n_list && !A.col_list) || (A.n_bnd && !A.bnd_list) ||
+        (A.n_halo && (!A.halo_src || !A.halo_dst || !A.copy_cnt)))
+        return fail(AIY_BAD_ARG, "staged sweep: missing list or halo pointers");
+    ks_staged_sweep_kernel<<<dim3(cdiv(A.nk, O), (unsigned)rows), B, 0, st>>>(A, V, dV, kopt, Vn,
+                                                                           dVn, O);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }

@@ -54,21 +54,37 @@ struct LdsCol {
     __device__ double operator[](int i) const { return p[i - lo]; }
 };
 
+// a column element: plain load, or (SC1) an L1-bypassing agent-scope load — the consumer side
+// of an in-kernel hand-off whose producer stored the bytes sc1 (MI355X_MICROARCH.md, the
+// inter-workgroup visibility table's first row)
+template <bool SC1>
+__device__ __forceinline__ double col_ld(const double* p) {
+    if constexpr (SC1)
+        return __builtin_bit_cast(double, __hip_atomic_load(
+            reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT));
+    else
+        return *p;
+}
+
 // pwch coefficients + ppval Horner on segment i
+template <bool SC1 = false>
 __device__ __forceinline__ double pchip_at(const double* __restrict__ x,
                                            const double* __restrict__ y,
                                            const double* __restrict__ d, int i, double xq) {
+    const double y0 = col_ld<SC1>(y + i), y1 = col_ld<SC1>(y + i + 1);
+    const double d0 = col_ld<SC1>(d + i), d1 = col_ld<SC1>(d + i + 1);
     double h = x[i + 1] - x[i];
-    double dl = (y[i + 1] - y[i]) / h;
-    double dzzdx = (dl - d[i]) / h;
-    double dzdxdx = (d[i + 1] - dl) / h;
+    double dl = (y1 - y0) / h;
+    double dzzdx = (dl - d0) / h;
+    double dzdxdx = (d1 - dl) / h;
     double c3 = (dzdxdx - dzzdx) / h;
     double c2 = 2 * dzzdx - dzdxdx;
     double sx = xq - x[i];
     double v = c3;
     v = sx * v + c2;
-    v = sx * v + d[i];
-    v = sx * v + y[i];
+    v = sx * v + d0;
+    v = sx * v + y0;
     return v;
 }
 

@@ -21,6 +21,10 @@ struct SimArgs {
     // reads pol + c·pcs and U + c·ucs and writes out[c], status[c] (no paths)
     int C;
     size_t pcs, ucs;
+    // reserve whole CUs (>= kSimExclusiveLds of LDS per chain workgroup) so no solve block
+    // shares the chain's CU — opt-in (aiy_ws_set_cu_exclusive on the chain's workspace; the GE
+    // driver sets it), ADVICE r5
+    bool exclusive;
 };
 int launch_sim_capital(const SimArgs& A, hipStream_t st);
 }  // namespace aiy

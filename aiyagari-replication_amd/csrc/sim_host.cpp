@@ -14,7 +14,8 @@ namespace aiy {
 
 int sim_capital_dev(const double* pol, size_t zs, size_t as, const double* a, const double* P,
                     int64_t N, int64_t Na, int64_t z1, double k1, int64_t T, const double* U,
-                    double* out, double* sim_k, int* sim_z, int* status, hipStream_t st) {
+                    double* out, double* sim_k, int* sim_z, int* status, hipStream_t st,
+                    bool exclusive = false) {
     if (!pol || !a || !P || !out || !status || (T > 1 && !U))
         return fail(AIY_BAD_ARG, "NULL argument");
     if (T < 1 || T > (1ll << 31) - 1) return fail(AIY_BAD_SHAPE, "T must be in [1, 2^31)");
@@ -23,6 +24,7 @@ int sim_capital_dev(const double* pol, size_t zs, size_t as, const double* a, co
     A.N = (int)N; A.Na = (int)Na; A.T = (int)T; A.z1 = (int)z1; A.k1 = k1;
     A.pol = pol; A.zs = zs; A.as = as; A.a = a; A.P = P; A.U = U;
     A.out = out; A.sim_k = sim_k; A.sim_z = sim_z; A.status = status;
+    A.exclusive = exclusive;
     return launch_sim_capital(A, st);
 }
 
@@ -88,7 +90,8 @@ int aiy_sim_capital_dev(aiy_ws* ws, const double* policy_rows, const double* a_g
                         int32_t* sim_z, int32_t* status, void* stream) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
     return sim_capital_dev(policy_rows, (size_t)ws->Na, 1, a_grid, P, ws->N, ws->Na, z1, k1, T,
-                           uniforms, k_supply, sim_k, sim_z, status, (hipStream_t)stream);
+                           uniforms, k_supply, sim_k, sim_z, status, (hipStream_t)stream,
+                           ws->cu_exclusive);
 }
 
 }  // extern "C"

@@ -9,6 +9,7 @@
 // a_grid and the policy rows are staged in LDS when they fit (Na·(N+1) <= 18432 doubles),
 // otherwise read through L1/L2.
 // Uniform draws come from the host (MATLAB's rand stream), so the chain is reproducible.
+#include <atomic>
 #include <algorithm>
 
 #include "aiy_common.hpp"
@@ -513,14 +514,21 @@ int launch_sim_chain_pipe(const SimArgs& A, hipStream_t st) {
     const int S = A.Na + 64;
     const int SS = S <= 512 ? 512 : (S <= 1024 && A.N <= 7 ? 1024 : 0);
     if (!SS) return fail(AIY_BAD_SHAPE, "pipe chain tables exceed LDS");
-    const size_t bytes = std::max(sizeof(double) * (size_t)(2 + 2 * A.N) * SS,
-                                  (size_t)kSimExclusiveLds);
+    const size_t tables = sizeof(double) * (size_t)(2 + 2 * A.N) * SS;
+    const size_t bytes = A.exclusive ? std::max(tables, (size_t)kSimExclusiveLds) : tables;
     const int g = std::max(A.C, 1);
     const bool path = A.sim_k || A.sim_z;
+    // the dynamic-LDS limit is raised once per instantiation, to the most any call asks for
 #define AIY_PIPE(SS_, PA_)                                                                         \
     do {                                                                                           \
-        AIY_HIP(hipFuncSetAttribute((const void*)sim_chain_pipe_kernel<SS_, PA_>,                  \
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));      \
+        static std::atomic<bool> lds_set{false};                                                   \
+        if (!lds_set) {                                                                            \
+            constexpr int most = std::max((int)sizeof(double) * (2 + 2 * (SS_ == 512 ? 8 : 7)) * SS_, \
+                                          kSimExclusiveLds);                                       \
+            AIY_HIP(hipFuncSetAttribute((const void*)sim_chain_pipe_kernel<SS_, PA_>,              \
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, most));        \
+            lds_set = true;                                                                        \
+        }                                                                                          \
         sim_chain_pipe_kernel<SS_, PA_><<<g, 128, bytes, st>>>(A);                                 \
     } while (0)
     if (SS == 512) {
@@ -545,10 +553,16 @@ int launch_sim_capital(const SimArgs& A, hipStream_t st) {
         const bool path = A.sim_k || A.sim_z;
         const int g = std::max(A.C, 1);
         if (need_pad <= kSimChainLdsMax) {
-            const size_t bytes = std::max(sizeof(double) * (size_t)need_pad, (size_t)kSimExclusiveLds);
-            const void* fn = path ? (const void*)sim_chain_kernel<true, true>
-                                  : (const void*)sim_chain_kernel<true, false>;
-            AIY_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+            const size_t tables = sizeof(double) * (size_t)need_pad;
+            const size_t bytes = A.exclusive ? std::max(tables, (size_t)kSimExclusiveLds) : tables;
+            static std::atomic<bool> lds_set[2] = {false, false};
+            if (!lds_set[path]) {  // once per instantiation, to the most any call asks for
+                const void* fn = path ? (const void*)sim_chain_kernel<true, true>
+                                      : (const void*)sim_chain_kernel<true, false>;
+                const int most = std::max((int)sizeof(double) * kSimChainLdsMax, kSimExclusiveLds);
+                AIY_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, most));
+                lds_set[path] = true;
+            }
             if (path) sim_chain_kernel<true, true><<<g, 256, bytes, st>>>(A);
             else sim_chain_kernel<true, false><<<g, 256, bytes, st>>>(A);
         } else {

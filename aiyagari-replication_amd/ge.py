@@ -263,6 +263,7 @@ def aiyagari_vfi_overlapped(Na=400, rho=0.75, sigma_e=0.75, shocks="tauchen", T=
             #                         its chain, its children's solves reading its v_old)
             self.alive = True
             self.chained = False
+            self.err = None         # a solve's or chain's exception
 
     # solve slots and chain resources persist across calls (per device and grid): a new
     # workspace allocates its scratch with hipMalloc / hipMemset on first use, which would
@@ -284,12 +285,47 @@ def aiyagari_vfi_overlapped(Na=400, rho=0.75, sigma_e=0.75, shocks="tauchen", T=
         streams.put(x)
 
     def get(free, pool_all, make):
-        x = free.pop() if free else make()
+        if free:
+            x = free.pop()
+            # a pooled workspace caches its feasible prefixes keyed on (r, w) and the
+            # raw addresses of a and s, not their contents; a later call with another
+            # calibration at the same Na can get a_t / s_t at the same addresses and repeat an
+            # r, so every reuse drops the cache (host-side flags only, no device work)
+            x.ws.invalidate()
+        else:
+            x = make()
         pool_all.append(x)
         return x
 
     out = dict(r_history=[], k_supply=[], k_demand=[], iters=[])
     fut = {}
+    try:
+        _run_tree(locals())
+    finally:
+        # every slot and chain resource goes back to the pools, also on an error
+        free_slots[:] = list({id(x): x for x in free_slots + all_slots}.values())
+        free_sims[:] = list({id(x): x for x in free_sims + all_sims}.values())
+    out["r"] = out["r_history"][-1]
+    out["iters"] = [out.pop("it0")] + out["iters"]
+    out["wall_s"] = time.perf_counter() - t0
+    out["cal"] = cal
+    out["lookahead"] = lookahead
+    out["solves"] = len(all_slots)
+    out["timeline"] = sorted(timeline, key=lambda e: e[3])
+    return out
+
+
+def _run_tree(env):
+    """The speculative tree of aiyagari_vfi_overlapped (its closure state passed in `env`)."""
+    import concurrent.futures as cf
+    solve, chain, get = env["solve"], env["chain"], env["get"]
+    _Node, cal, dev = env["_Node"], env["cal"], env["dev"]
+    N, Na, r0 = env["N"], env["Na"], env["r0"]
+    free_slots, all_slots = env["free_slots"], env["all_slots"]
+    free_sims, all_sims = env["free_sims"], env["all_sims"]
+    out, fut = env["out"], env["fut"]
+    max_r_iter, r_tol, lookahead = env["max_r_iter"], env["r_tol"], env["lookahead"]
+    import torch
     with cf.ThreadPoolExecutor(max_workers=16) as pool:
         root = get(free_slots, all_slots, lambda: _GESlot(N, Na, dev))
         it0 = solve(root, torch.zeros((N, Na), dtype=torch.float64, device=dev), r0)
@@ -340,54 +376,60 @@ def aiyagari_vfi_overlapped(Na=400, rho=0.75, sigma_e=0.75, shocks="tauchen", T=
         cur = _Node(1, r_low, r_high, None)
         submit_solve(cur, root.v_old)
         done = False
-        while fut and not done:
-            finished, _ = cf.wait(list(fut), return_when=cf.FIRST_COMPLETED)
-            for f in finished:
-                kind, node, sim = fut.pop(f)
-                res = f.result()
-                if sim is not None:
-                    free_sims.append(sim)
-                if kind == "chain0":
-                    continue
-                if kind == "solve":
-                    node.it = res
-                    node.refs -= 1
-                    if node.parent is not None:
-                        node.parent.refs -= 1
-                        release(node.parent)
-                    if not node.alive:
-                        release(node)
+        try:
+            while fut and not done:
+                finished, _ = cf.wait(list(fut), return_when=cf.FIRST_COMPLETED)
+                for f in finished:
+                    kind, node, sim = fut.pop(f)
+                    try:
+                        res, err = f.result(), None
+                    except Exception as e:  # kept on the node: raised only if the path needs it
+                        res, err = None, e
+                    if sim is not None:
+                        free_sims.append(sim)
+                    if kind == "chain0":
+                        if err is not None:  # the sequential script runs this chain too
+                            raise err
                         continue
-                    advance(node)
-                    continue
-                node.Ks = res  # a chain
-                node.refs -= 1
-                release(node)
-            # decisions: the current step's chain, then (already chained) the steps after it
-            while not done and cur.Ks is not None:
-                Kd = cb.capital_demand(cur.r, cal["labor"], cal["alpha"], cal["delta"])
-                out["r_history"].append(cur.r); out["k_supply"].append(cur.Ks)
-                out["k_demand"].append(Kd); out["iters"].append(cur.it)
-                if cur.j == max_r_iter or abs(cur.Ks - Kd) < r_tol:
-                    done = True
-                    break
-                nxt, other = (cur.kids[0], cur.kids[1]) if cur.Ks > Kd else (cur.kids[1], cur.kids[0])
-                kill(other)
-                prev, cur = cur, nxt
-                release(prev)
-                advance(cur)
-        for f in list(fut):  # speculative work still running: let it finish before teardown
-            f.result()
-    out["r"] = out["r_history"][-1]
-    out["iters"] = [it0] + out["iters"]
-    out["wall_s"] = time.perf_counter() - t0
-    out["cal"] = cal
-    out["lookahead"] = lookahead
-    out["solves"] = len(all_slots)
-    out["timeline"] = sorted(timeline, key=lambda e: e[3])
-    free_slots[:] = list({id(x): x for x in free_slots + all_slots}.values())  # all back
-    free_sims[:] = list({id(x): x for x in free_sims + all_sims}.values())
-    return out
+                    if kind == "solve":
+                        node.it, node.err = res, err
+                        node.refs -= 1
+                        if node.parent is not None:
+                            node.parent.refs -= 1
+                            release(node.parent)
+                        if not node.alive or err is not None:
+                            release(node)
+                            continue
+                        advance(node)
+                        continue
+                    node.Ks, node.err = res, err  # a chain
+                    node.refs -= 1
+                    release(node)
+                # decisions: the current step's chain, then (already chained) the steps after it
+                while not done and (cur.Ks is not None or cur.err is not None):
+                    if cur.err is not None:  # a failure on the sequential loop's own path
+                        raise cur.err
+                    Kd = cb.capital_demand(cur.r, cal["labor"], cal["alpha"], cal["delta"])
+                    out["r_history"].append(cur.r); out["k_supply"].append(cur.Ks)
+                    out["k_demand"].append(Kd); out["iters"].append(cur.it)
+                    if cur.j == max_r_iter or abs(cur.Ks - Kd) < r_tol:
+                        done = True
+                        break
+                    nxt, other = ((cur.kids[0], cur.kids[1]) if cur.Ks > Kd
+                                  else (cur.kids[1], cur.kids[0]))
+                    kill(other)
+                    prev, cur = cur, nxt
+                    release(prev)
+                    advance(cur)
+        finally:
+            # speculative work still running finishes before the slots go back to the pools;
+            # its results and errors (killed nodes, steps past the last) are ignored
+            for f in list(fut):
+                try:
+                    f.result()
+                except Exception:
+                    pass
+    out["it0"] = it0
 
 
 def _wait_polled(stream, nap=0.0):
@@ -428,6 +470,9 @@ class _GESim:
 
         from .vfi import Workspace
         self.ws = Workspace(N, Na)
+        # the chain's workgroup reserves its CU so no speculative solve block shares it (a
+        # co-resident block slows the serial wave; opt-in per workspace since ADVICE r5)
+        self.ws.set_cu_exclusive(True)
         self.k = torch.zeros(1, dtype=torch.float64, device=dev)
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)
         self.kh = torch.zeros(1, dtype=torch.float64).pin_memory()  # host copies (pinned)

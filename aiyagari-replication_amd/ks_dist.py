@@ -294,6 +294,23 @@ class HipShard:
     def improve_direct(self, kopt):
         check(lib().ks_dev_improve_direct(self._h, ptr(kopt), stream_handle(None)))
 
+    def set_split(self, interior, boundary):
+        """The staged schedule's split of the own columns (ks_dev_set_split)."""
+        ii = np.ascontiguousarray(interior, np.int32)
+        bb = np.ascontiguousarray(boundary, np.int32)
+        check(lib().ks_dev_set_split(self._h, ptr(ii), C.c_int32(ii.size), ptr(bb),
+                                     C.c_int32(bb.size)))
+
+    def staged_sweep(self, V, dV, kopt, Vout, dVout, src=None, dst=None, n_halo=0, flags=None,
+                     mask=0, wait_v=0, slot=0, pub_v=0, timeout_s=30.0, err=None):
+        """One staged sweep in one launch (ks_dev_staged_sweep): src / dst device int64 tensors
+        of column addresses; flags / err device addresses (ints) of a mapped host page, or None."""
+        check(lib().ks_dev_staged_sweep(
+            self._h, ptr(V), ptr(dV), ptr(kopt), ptr(Vout), ptr(dVout), ptr(src), ptr(dst),
+            C.c_int32(n_halo), C.c_void_p(flags), C.c_uint64(mask), C.c_uint64(wait_v),
+            C.c_int32(slot), C.c_uint64(pub_v), C.c_double(timeout_s), C.c_void_p(err),
+            stream_handle(None)))
+
     def reldiff(self, V, Vold):
         import torch
         out = torch.zeros(2, dtype=torch.int64, device=V.device)
@@ -330,14 +347,16 @@ def staged_plan(own, kp_idx, owner, nK: int, rank: int):
 
 class DirectPeers:
     """The direct schedule (ks_vfi_solve_sharded depth = 0) under one process per
-    GPU.  Every rank keeps its own columns of value and slopes in two parity buffers; the
-    other ranks map them through IPC handles (exchanged once), and the rank's column tables
-    point each forecast column at its owner's buffer, so a Howard sweep or an improvement reads
-    neighbours' columns in place over xGMI — no halo copies, no ghost sweeps.  The hand-off is
-    a counter per rank in a host page every rank maps (`aiy_flag_set` after each sweep,
-    `aiy_flags_wait` on the neighbours' counters before the next one): stream-ordered, the
-    host never blocks.  Neighbours = the owners of the columns this rank reads and the ranks
-    that read its columns (the latter so a buffer is not overwritten while it is read)."""
+    GPU, staged.  Every rank keeps its own columns of value and slopes in three buffers (version
+    v in buffer (v - 1) mod 3); the other ranks map them through IPC handles (exchanged once).
+    Per Howard sweep ONE launch (ks_dev_staged_sweep): it publishes the previous version in the
+    rank's counter slot of a host page every rank maps, copies the forecast columns peers own
+    into a local halo once those peers have published the version it reads (the wait runs in
+    the copy blocks), sweeps the interior columns (all forecast columns own) without waiting and
+    the boundary columns after the copies.  Stream-ordered, the host never blocks.  Neighbours =
+    the owners of the columns this rank reads and the ranks that read its columns (the latter
+    so a buffer is not overwritten while it is read: with three buffers that wait is one
+    version old and already satisfied by the previous sweep's copy rows)."""
 
     # the host page: counter slot q at byte 128·q (q < 64), rank q's timeout word at 8192 + 128·q
     PAGE = 16384
@@ -351,14 +370,16 @@ class DirectPeers:
         self.shard, self.nK, self.rank, self.world = shard, nK, rank, world
         self.nk = V.shape[-1]
         self.timeout_s = float(timeout_s)
+        # three buffers (version v in buffer (v - 1) mod 3): a sweep writes the
+        # buffer its neighbours finished reading two versions ago, so only its copy rows wait.
         # NaN outside the own columns: a read of a local copy instead of the owner's would show
-        self.V = [torch.full_like(V, math.nan) for _ in range(2)]
-        self.dV = [torch.full_like(V, math.nan) for _ in range(2)]
+        self.V = [torch.full_like(V, math.nan) for _ in range(3)]
+        self.dV = [torch.full_like(V, math.nan) for _ in range(3)]
         self.own = owned_columns(nK, rank, world, bounds)
         plan = halo_plan(shard.kp_idx, nK, world, bounds)
         self.nbr = sorted({p for p in range(world) if p != rank and (plan[rank][p] or plan[p][rank])})
         self.mask = sum(1 << p for p in self.nbr)
-        # IPC handles of the four buffers, every rank's (a failure on any rank is raised on
+        # IPC handles of the six buffers, every rank's (a failure on any rank is raised on
         # every rank, after the same collectives, so no rank is left inside one)
         mine, fail_msg = [], None
         try:
@@ -373,7 +394,7 @@ class DirectPeers:
         dist.all_gather_object(allh, (mine, fail_msg))
         self._opened = []
         self._shm = None
-        addr = []   # addr[q] = (V0, V1, dV0, dV1) device addresses of rank q's buffers
+        addr = []   # addr[q] = (V0, V1, V2, dV0, dV1, dV2) device addresses of rank q's buffers
         if not any(m for _, m in allh):
             try:
                 for q in range(world):
@@ -408,10 +429,7 @@ class DirectPeers:
         # reads a peer's memory; the own columns split into interior (every forecast column
         # owned) and boundary (at least one copied)
         self.remote, interior, boundary = staged_plan(self.own, shard.kp_idx, owner, nK, rank)
-        ii = np.ascontiguousarray(interior, np.int32)
-        bb = np.ascontiguousarray(boundary, np.int32)
-        check(lib().ks_dev_set_split(shard._h, ptr(ii), C.c_int32(ii.size), ptr(bb),
-                                     C.c_int32(bb.size)))
+        shard.set_split(interior, boundary)
         nr = len(self.remote)
         self.hV = torch.empty((max(nr, 1), self.nk), dtype=V.dtype, device=V.device)
         self.hdV = torch.empty_like(self.hV)
@@ -421,19 +439,21 @@ class DirectPeers:
         def col(c, b, slope):
             if owner[c] != rank and c in slot:
                 return (hdv if slope else hv) + cb * slot[c]
-            return addr[owner[c]][(2 if slope else 0) + b] + cb * c
+            return addr[owner[c]][(3 if slope else 0) + b] + cb * c
         self.tab = [torch.tensor([col(c, b, False) for c in range(4 * nK)] +
                                  [col(c, b, True) for c in range(4 * nK)],
-                                 dtype=torch.int64, device=V.device) for b in (0, 1)]
-        # the copies of one sweep: the owners' parity-b value then slope columns -> the halo
+                                 dtype=torch.int64, device=V.device) for b in range(3)]
+        # the copies of one sweep: the owners' buffer-b value then slope columns -> the halo
         dev_arr = lambda xs: torch.tensor(xs or [0], dtype=torch.int64, device=V.device)
         self._src = [dev_arr([addr[owner[c]][b] + cb * c for c in self.remote] +
-                             [addr[owner[c]][2 + b] + cb * c for c in self.remote])
-                     for b in (0, 1)]
+                             [addr[owner[c]][3 + b] + cb * c for c in self.remote])
+                     for b in range(3)]
         self._dst = dev_arr([hv + cb * i for i in range(nr)] + [hdv + cb * i for i in range(nr)])
         self._ncopy = 2 * nr
         self._col_bytes = cb
-        self.copy_stream = torch.cuda.Stream(device=V.device)
+        p3 = lambda ts: (C.c_void_p * 3)(*[t.data_ptr() for t in ts])  # host arrays of 3
+        self._tabs, self._Vs, self._dVs = p3(self.tab), p3(self.V), p3(self.dV)
+        self._srcs = p3(self._src)
         # the counter page: rank 0 creates it, every rank maps and registers it
         name, fail_msg = [None], None
         if rank == 0:
@@ -499,7 +519,9 @@ class DirectPeers:
 
     # the schedule (every rank calls the same sequence)
     def start(self, V):
-        """Own columns of V into parity 0, their slopes, and publish "sweep 0"."""
+        """Own columns of V into buffer 0, their slopes, and publish the next version (every
+        rank restarts its buffer cycle here, after a barrier, so the version -> buffer map is
+        the same on every rank)."""
         import torch
         import torch.distributed as dist
         torch.cuda.synchronize()
@@ -522,21 +544,20 @@ class DirectPeers:
         self.shard.improve_direct(kopt)
 
     def sweeps(self, kopt, n):
-        """n Jacobi Howard sweeps (:172-192): per sweep the hand-off wait, the halo copies on
-        the copy stream beside the interior launch, the boundary launch, a system-scope release
-        and the publish, all enqueued by one C call (ks_dev_direct_sweeps)."""
+        """n Jacobi Howard sweeps (:172-192), ONE launch each (ks_dev_direct_sweeps /
+        ks_dev_staged_sweep): publish the previous version, copy the peers' forecast columns once
+        they have published theirs, interior columns meanwhile, boundary columns after the
+        copies; then one publish of the last version."""
         if n <= 0:
             return
         check(lib().ks_dev_direct_sweeps(
-            self.shard._h, ptr(self.tab[0]), ptr(self.tab[1]), ptr(self.V[0]), ptr(self.V[1]),
-            ptr(self.dV[0]), ptr(self.dV[1]), ptr(kopt), C.c_int32(self.cur), i64(n),
-            ptr(self._src[0]), ptr(self._src[1]), ptr(self._dst), C.c_int32(self._ncopy),
-            i64(self._col_bytes),
+            self.shard._h, self._tabs, self._Vs, self._dVs, ptr(kopt), C.c_int32(self.cur),
+            i64(n), self._srcs, ptr(self._dst), C.c_int32(self._ncopy), i64(self._col_bytes),
             C.c_void_p(self._flags), C.c_int32(self.rank), C.c_uint64(self.mask),
             C.c_uint64(self.n), C.c_double(self.timeout_s), C.c_void_p(self._err),
-            stream_handle(None), stream_handle(self.copy_stream)))
+            stream_handle(None)))
         self.n += n
-        self.cur ^= n & 1
+        self.cur = (self.cur + n) % 3
 
     def current(self):
         return self.V[self.cur]

@@ -33,6 +33,7 @@ sys.path.insert(0, str(ROOT))
 # waits behind it (ge.aiyagari_vfi_overlapped; tools/ge_concurrency.py: with 4 queues two
 # solves beside two chains ran 2.6x slower).  Raised (never lowered) before the HIP runtime starts:
 # an inherited smaller value (the GPU box exports 4) would otherwise win.
+HW_QUEUES_INHERITED = os.environ.get("GPU_MAX_HW_QUEUES")  # recorded in ge_equilibrium
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:
     os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
@@ -115,7 +116,10 @@ def ge_wall(pkg, threads):
         H = no.ge_bisection_vfi(cal, solve=lambda *a: corc.vfi_solve(*a))
         cpu[th] = time.perf_counter() - t0
     cpu_s = cpu[threads]
-    return {"workload": "Aiyagari_VFI.m defaults (configs[0]): initial VFI + 10-step bisection + MC",
+    inherited = queues_probe()
+    return {"hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]),
+            "hw_queues_inherited": HW_QUEUES_INHERITED, "at_inherited_queues": inherited,
+            "wall_s_gpu_inherited_queues": inherited.get("wall_s_gpu"),"workload": "Aiyagari_VFI.m defaults (configs[0]): initial VFI + 10-step bisection + MC",
             "r_gpu": out["r"], "r_cpu": H["r_final"], "identical_trace": out["r_history"] == H["r"],
             "sweeps": int(sum(out["iters"])), "wall_s_gpu": gpu_s, "wall_s_cpu": cpu_s,
             "wall_s_gpu_runs": walls,
@@ -126,6 +130,23 @@ def ge_wall(pkg, threads):
             and seq["k_supply"] == out["k_supply"] and seq["iters"] == out["iters"],
             "cpu_cores": threads, "wall_s_cpu_1core": cpu[1],
             "cpu_kind": "port (oracle/aiy_oracle.c)"}
+
+
+def queues_probe():
+    """The same GE wall in a child process under the inherited GPU_MAX_HW_QUEUES (the value a
+    library caller or the test suite runs with; bench.py raised its own to 16) — ADVICE r5."""
+    import subprocess
+    env = dict(os.environ)
+    if HW_QUEUES_INHERITED is None:
+        env.pop("GPU_MAX_HW_QUEUES", None)
+    else:
+        env["GPU_MAX_HW_QUEUES"] = HW_QUEUES_INHERITED
+    try:
+        p = subprocess.run([sys.executable, str(ROOT / "tools" / "ge_wall_probe.py")], env=env,
+                           capture_output=True, text=True, timeout=300)
+        return json.loads(p.stdout.strip().splitlines()[-1])
+    except Exception as e:  # reported, never fatal to the bench
+        return {"error": repr(e)[:200]}
 
 
 def solve_wall(pkg, ws, cal, r, w, a_t, s_t, P_t, dev):

@@ -373,11 +373,12 @@ def direct_model(pkg, dev, world=8, nk=32768, nK=64, sweeps=24, howard=50):
         torch.cuda.synchronize()
         swp.append(e0.elapsed_time(e1) / sweeps)
     # the cross-process schedule's own cost (ks_dist.DirectPeers, staged): the slowest shard's
-    # sweeps through ks_dev_direct_sweeps — per sweep a counter wait on a mapped host page (its
-    # own slot, always satisfied), the copies of the peers' forecast columns into a local halo on
-    # a second stream beside the interior launch, the boundary launch, the system-scope release
-    # and the publish.  The copies here are device-local (the peers' buffers are on this GPU),
-    # so their time is an HBM lower bound on the xGMI copy (DESIGN.md §6 budgets the link).
+    # sweeps through ks_dev_direct_sweeps — ONE launch per sweep that publishes the previous
+    # version in its slot of a mapped host page, copies the peers' forecast columns into a local
+    # halo once the neighbours' slots allow it (its own slot here: self-satisfied), sweeps the
+    # interior columns meanwhile and the boundary columns after the copies, on three buffers.
+    # The copies here are device-local (the peers' buffers are on this GPU), so their time is an
+    # HBM lower bound on the xGMI copy (DESIGN.md §6 budgets the link).
     import ctypes as C
     import mmap
     check, lib = pkg._capi.check, pkg._capi.lib
@@ -398,18 +399,23 @@ def direct_model(pkg, dev, world=8, nk=32768, nK=64, sweeps=24, howard=50):
     hdV = torch.empty_like(hV)
     cb = 8 * nk
     slot = {c: i for i, c in enumerate(remote)}
+    # shard q's third buffer (the other shards keep two: only their buffer b of the version
+    # being read matters to q's copies and tables)
+    Vq = Vb[q] + [Vb[q][0].clone()]
+    dVq = dVb[q] + [dVb[q][0].clone()]
+    bufV = lambda o, b: Vq[b] if o == q else Vb[o][b % 2]
+    bufD = lambda o, b: dVq[b] if o == q else dVb[o][b % 2]
     stab = []
-    for b in range(2):
-        a = [(hV.data_ptr() + cb * slot[c]) if c in slot else Vb[owner[c]][b].data_ptr() + cb * c
+    for b in range(3):
+        a = [(hV.data_ptr() + cb * slot[c]) if c in slot else bufV(owner[c], b).data_ptr() + cb * c
              for c in range(4 * nK)]
-        a += [(hdV.data_ptr() + cb * slot[c]) if c in slot else dVb[owner[c]][b].data_ptr() + cb * c
+        a += [(hdV.data_ptr() + cb * slot[c]) if c in slot else bufD(owner[c], b).data_ptr() + cb * c
               for c in range(4 * nK)]
         stab.append(torch.tensor(a, dtype=torch.int64, device=dev))
     darr = lambda xs: torch.tensor(xs or [0], dtype=torch.int64, device=dev)
-    src = [darr([Vb[owner[c]][b].data_ptr() + cb * c for c in remote] +
-                [dVb[owner[c]][b].data_ptr() + cb * c for c in remote]) for b in range(2)]
+    src = [darr([bufV(owner[c], b).data_ptr() + cb * c for c in remote] +
+                [bufD(owner[c], b).data_ptr() + cb * c for c in remote]) for b in range(3)]
     dst = darr([hV.data_ptr() + cb * i for i in range(nr)] + [hdV.data_ptr() + cb * i for i in range(nr)])
-    cstream = torch.cuda.Stream(device=dev)
     page = mmap.mmap(-1, 16384)
     host = C.c_char.from_buffer(page)
     hp = C.addressof(host)
@@ -417,15 +423,17 @@ def direct_model(pkg, dev, world=8, nk=32768, nK=64, sweeps=24, howard=50):
     check(lib().aiy_host_register(C.c_void_p(hp), C.c_int64(16384), C.byref(dptr)))
     C.c_uint64.from_address(hp).value = 1
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-    P_ = lambda t: C.c_void_p(t.data_ptr())
+    p3 = lambda ts: (C.c_void_p * 3)(*[t.data_ptr() for t in ts])
+    tabs3, V3, dV3, src3 = p3(stab), p3(Vq), p3(dVq), p3(src)
+    cur = [0]
 
     def run_direct(n, n0):
         check(lib().ks_dev_direct_sweeps(
-            sh[q]._h, P_(stab[0]), P_(stab[1]), P_(Vb[q][0]), P_(Vb[q][1]), P_(dVb[q][0]),
-            P_(dVb[q][1]), P_(ko), C.c_int32(0), C.c_int64(n), P_(src[0]), P_(src[1]), P_(dst),
-            C.c_int32(2 * nr), C.c_int64(cb), dptr, C.c_int32(0), C.c_uint64(1),
-            C.c_uint64(n0), C.c_double(30.0), C.c_void_p(dptr.value + 8192), st,
-            C.c_void_p(cstream.cuda_stream)))
+            sh[q]._h, tabs3, V3, dV3, C.c_void_p(ko.data_ptr()), C.c_int32(cur[0]), C.c_int64(n),
+            src3, C.c_void_p(dst.data_ptr()), C.c_int32(2 * nr), C.c_int64(cb), dptr,
+            C.c_int32(0), C.c_uint64(1), C.c_uint64(n0), C.c_double(30.0),
+            C.c_void_p(dptr.value + 8192), st))
+        cur[0] = (cur[0] + n) % 3
     run_direct(2, 1)
     e0, e1 = ev(), ev()
     e0.record()
@@ -451,16 +459,17 @@ def direct_model(pkg, dev, world=8, nk=32768, nK=64, sweeps=24, howard=50):
                         "interior_columns": int(interior.size),
                         "boundary_columns": int(boundary.size),
                         "xgmi_us_per_sweep_at_link_rate": remote_bytes / 153e9 * 1e6,
-                        "note": "ks_dev_direct_sweeps (staged) on the slowest shard: self-satisfied "
-                                "counter wait, halo copies of the peers' columns on a second stream "
-                                "beside the interior launch, boundary launch, system-scope release, "
-                                "publish; the copies are device-local here (xGMI time at one link's "
+                        "note": "ks_dev_direct_sweeps (staged, one launch per sweep, three "
+                                "buffers) on the shard with the most peer columns: publish, "
+                                "self-satisfied counter wait and halo copies in the copy blocks, "
+                                "interior columns beside them, boundary columns after the copies; "
+                                "the copies are device-local here (xGMI time at one link's "
                                 "153 GB/s: xgmi_us_per_sweep_at_link_rate); the neighbours' skew is "
                                 "not in it"},
             "note": f"direct schedule (ks_vfi_solve_sharded depth 0) emulated on one GPU: each of "
                     f"{world} shards timed alone, reading the other shards' buffers through its "
                     f"column table; projected iteration = slowest improvement + {howard} x "
-                    f"slowest sweep; `handoff` adds the staged schedule's copies and second launch"}
+                    f"slowest sweep; `handoff` adds the staged schedule's one-launch hand-off (publish, waits, copies)"}
 
 
 def main():

@@ -91,7 +91,7 @@ def leg_summary(leg):
     for k in ("wall_s_gpu", "wall_s_cpu", "identical_trace", "r", "r_gpu", "iters", "wall_ms",
               "ms_per_sweep", "us_per_step", "us_per_push", "howard_ms_per_sweep",
               "vfi_iteration_ms", "r_equals_reference_trace", "speedup_vs_sequential_rates",
-              "bit_exact_vs_halo"):
+              "bit_exact_vs_halo", "hw_queues", "wall_s_gpu_inherited_queues"):
         if k in leg and (_num(leg[k]) is not None or isinstance(leg[k], bool)):
             s[k] = leg[k]
     return s

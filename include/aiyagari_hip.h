@@ -446,37 +446,35 @@ int aiy_host_unregister(void* p);
 int aiy_flags_wait(const void* flags, uint64_t mask, uint64_t value, double timeout_s, void* err,
                    void* stream);
 int aiy_flag_set(void* flags, int32_t slot, uint64_t value, void* stream);
-/* The staged direct schedule.  ks_dev_set_split: the shard's own columns c = s·K_size + K in
- * two host lists — `interior` columns read only forecast columns the shard owns, `boundary`
- * columns read at least one a peer owns; ks_dev_howard_fused_part sweeps one list (part 0 / 1)
- * like ks_dev_howard_fused.
- * ks_dev_direct_sweeps: nsweeps fused Howard sweeps; sweep i reads parity p = parity ^ (i & 1)
- * (V/dV p, column table tab_p) and writes parity p ^ 1, once the slots in `mask` hold >= n0 + i.
- * The forecast columns peers own are read from a local halo that the table points at: per
- * sweep, after the wait, the interior launch also copies src_p[q] -> dst[q], col_bytes each,
- * q < ncopy (DEVICE arrays of pointers; the owners' parity-p value and slope columns, read with
- * system-scope loads) in extra block rows, beside the interior columns; the boundary columns
- * sweep in the next launch; both store their values write-through (system scope).  copy_stream
- * is unused (kept for the ABI).  ks_dev_howard_fused_part_halo: the part launch with such
- * copy rows.  Then a
- * system-scope release (an event recorded with hipEventReleaseToSystem) and slot `slot` :=
- * n0 + i + 1.  ncopy = 0: every forecast column is read through the table as it is (one process,
- * or no peer columns).  ks_dev_halo_copy: the same copies once, stream-ordered (before an
- * improvement). */
+/* The staged direct schedule.  ks_dev_set_split: the shard's own columns
+ * c = s·K_size + K in two host lists — `interior` columns read only forecast columns the shard
+ * owns, `boundary` columns read at least one a peer owns; ks_dev_howard_fused_part sweeps one
+ * list (part 0 / 1) like ks_dev_howard_fused.
+ * ks_dev_staged_sweep: one whole sweep in ONE launch — first publish pub_v in slot `slot` of
+ * `flags` (the previous launch on the stream produced that version; system-scope release), then
+ * copy src[q] -> dst[q] (DEVICE arrays of column pointers, q < n_halo: the owners' value and
+ * slope columns, system-scope loads) once every slot in `mask` holds >= wait_v (timeout: *err =
+ * 1 + q, as aiy_flags_wait), sweep the interior columns without waiting and the boundary columns
+ * once every copy is in (an in-kernel agent-scope counter hand-off); own columns are stored
+ * write-through (system scope).  flags = NULL: no publish and no wait.
+ * ks_dev_direct_sweeps: nsweeps such sweeps on three buffers — version v in buffer (v - 1) mod 3:
+ * sweep i reads buffer b = (cur + i) mod 3 (V[b], dV[b], column table tabs[b], copies from
+ * srcs[b]) and writes buffer (b + 1) mod 3, waiting for / publishing n0 + i; then one launch
+ * publishes n0 + nsweeps.  tabs, V, dV, srcs: HOST arrays of three device pointers.
+ * ks_dev_halo_copy: the same copies once, stream-ordered (before an improvement). */
 int ks_dev_set_split(ks_dev* h, const int32_t* interior, int32_t n_int, const int32_t* boundary,
                      int32_t n_bnd);
 int ks_dev_howard_fused_part(ks_dev* h, int part, const double* V, const double* dV,
                              const double* kopt, double* Vout, double* dVout, void* stream);
-int ks_dev_howard_fused_part_halo(ks_dev* h, int part, const double* V, const double* dV,
-                                  const double* kopt, double* Vout, double* dVout,
-                                  const void* const* src, void* const* dst, int32_t n_halo,
-                                  void* stream);
-int ks_dev_direct_sweeps(ks_dev* h, const void* const* tab0, const void* const* tab1,
-                         double* V0, double* V1, double* dV0, double* dV1, double* kopt,
-                         int32_t parity, int64_t nsweeps, const void* const* src0,
-                         const void* const* src1, void* const* dst, int32_t ncopy,
-                         int64_t col_bytes, void* flags, int32_t slot, uint64_t mask, uint64_t n0,
-                         double timeout_s, void* err, void* stream, void* copy_stream);
+int ks_dev_staged_sweep(ks_dev* h, const double* V, const double* dV, const double* kopt,
+                        double* Vout, double* dVout, const void* const* src, void* const* dst,
+                        int32_t n_halo, void* flags, uint64_t mask, uint64_t wait_v, int32_t slot,
+                        uint64_t pub_v, double timeout_s, void* err, void* stream);
+int ks_dev_direct_sweeps(ks_dev* h, void* const* tabs, double* const* V, double* const* dV,
+                         double* kopt, int32_t cur, int64_t nsweeps, void* const* srcs,
+                         void* const* dst, int32_t ncopy, int64_t col_bytes, void* flags,
+                         int32_t slot, uint64_t mask, uint64_t n0, double timeout_s, void* err,
+                         void* stream);
 int ks_dev_halo_copy(const void* const* src, void* const* dst, int32_t ncopy, int64_t col_bytes,
                      void* stream);
 /* Ghost shards (ks_dist.py exchanges halos every m Howard sweeps and sweeps a widening

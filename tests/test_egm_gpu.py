@@ -231,3 +231,44 @@ def test_egm_chained_solve_dev(pkg, gpu, Na, N, labor):
         Ro = corc.egm_solve(pc0, a, s, P, r, w, 0.96, 5.0, cal["amin"], 1e-6, 400)
     assert i0 == Ro["iters"] and d0 == Ro["dist"]
     assert np.array_equal(c0_, Ro["policy_c"]) and np.array_equal(k0, Ro["policy_k"])
+
+
+@pytest.mark.parametrize("Na,N,labor,sigma,theta", [
+    (2, 7, False, 5.0, 1.0), (3, 7, True, 5.0, 1.0), (65, 7, False, 5.0, 1.0),
+    (400, 7, False, 5.0, 1.0), (400, 7, True, 5.0, 1.0), (400, 7, True, 2.5, 2.0),
+    (1024, 7, False, 5.0, 1.0), (700, 7, True, 5.0, 1.0), (300, 16, False, 3.0, 1.0),
+    (1000, 1, False, 5.0, 1.0)])
+def test_egm_small_grid_solve_dev(pkg, gpu, Na, N, labor, sigma, theta):
+    """Small grids (the fused one-launch step inside the speculative device-tier solve): the
+    iteration count, policy_c and policy_k equal the C loop bit for bit, for N = 1 … 16, integer
+    and non-integer sigma, theta != 1, stops on tol and at max_iter."""
+    import torch
+    dev = torch.device("cuda", 0)
+    cal = no.calib_aiyagari(Na=Na, shocks="rouwenhorst", N=N) if N not in (7, 1) else \
+        no.calib_aiyagari(Na=Na, shocks="rouwenhorst")
+    a, s, P = cal["a_grid"], cal["s"], cal["P"]
+    if N == 1:
+        s, P = np.array([1.0]), np.array([[1.0]])
+    N = P.shape[0]
+    r = 0.03
+    w = no.wage(r, 0.36, 0.08)
+    t = lambda x: torch.as_tensor(np.ascontiguousarray(x), device=dev)
+    pc0 = np.tile(((1 + r) * a + w * np.mean(s))[None, :], (N, 1))
+    for tol, max_iter in ((1e-6, 400), (1e-3, 400), (1e-6, 9)):
+        ws = pkg.Workspace(N, Na)
+        c = t(pc0)
+        pk = torch.zeros_like(c)
+        pl = torch.zeros_like(c) if labor else None
+        it, dist = pkg.egm_solve_dev(ws, c, t(a), t(s), t(P), r, w, 0.96, sigma, cal["amin"],
+                                     tol, max_iter, pk, labor=labor, phi=1.0, theta=theta,
+                                     policy_l=pl)
+        ws.close()
+        if labor:
+            Ro = corc.labor_egm_solve(pc0, a, s, P, r, w, 0.96, sigma, 1.0, theta, cal["amin"],
+                                      tol, max_iter)
+            assert np.array_equal(pl.cpu().numpy(), Ro["policy_l"])
+        else:
+            Ro = corc.egm_solve(pc0, a, s, P, r, w, 0.96, sigma, cal["amin"], tol, max_iter)
+        assert it == Ro["iters"]
+        assert np.array_equal(c.cpu().numpy(), Ro["policy_c"])
+        assert np.array_equal(pk.cpu().numpy(), Ro["policy_k"])

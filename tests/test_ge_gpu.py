@@ -130,3 +130,16 @@ def test_ge_histogram_supply_runs(pkg, gpu):
     assert -0.05 < out["r"] < 1 / 0.96 - 1
     gap = abs(out["k_supply"][-1] - out["k_demand"][-1])
     assert gap < 1.0
+
+
+def test_ge_overlapped_pool_reuse_other_calibration(pkg, gpu):
+    """the overlapped driver's pooled workspaces cache feasible prefixes keyed
+    on (r, w) and the addresses of a and s.  Two calls at the same Na with different
+    calibrations (so different a and s, possibly at reused addresses, and the same bisection
+    midpoints) must each equal the sequential driver."""
+    kw = dict(Na=300, T=3000)
+    for rho, sig in ((0.75, 0.75), (0.6, 0.2), (0.75, 0.75)):
+        seq = pkg.ge.aiyagari_vfi(rho=rho, sigma_e=sig, **kw)
+        ovl = pkg.ge.aiyagari_vfi_overlapped(rho=rho, sigma_e=sig, **kw)
+        for key in ("r_history", "k_supply", "k_demand", "iters", "r"):
+            assert ovl[key] == seq[key], (rho, sig, key)
