@@ -265,9 +265,10 @@ template <bool WT, bool SC1 = false>
 __device__ __forceinline__ void howard_slopes_col(const KsArgs& A, const KsView& W, int col,
                                                   const double* __restrict__ k_opt,
                                                   double* __restrict__ Vn,
-                                                  double* __restrict__ dVn, double* s_v, int O) {
+                                                  double* __restrict__ dVn, double* s_v, int O,
+                                                  int tile = -1) {
     const int nk = A.nk;
-    const int q0 = blockIdx.x * O;
+    const int q0 = (tile >= 0 ? tile : (int)blockIdx.x) * O;
     const int lo = q0 >= 2 ? q0 - 2 : 0;
     const int own_hi = min(nk, q0 + O);
     const int hi = min(nk, q0 + O + 2);
@@ -315,6 +316,38 @@ __global__ __launch_bounds__(256) void ks_howard_slopes_kernel(KsArgs A, const d
     const KsView W{A.k_grid, V, dV};
     for (int y = blockIdx.y; y < ncl; y += gridDim.y)  // block-uniform trip count
         howard_slopes_col<false>(A, W, col0 + y, k_opt, Vn, dVn, s_v, O);
+}
+
+// The same sweep on a 1-D grid dealt by XCD (tile-major): blocks are dealt round-robin over the
+// 8 XCDs (observed), so linear block L runs on XCD L mod 8; slot start_x + L / 8 of the
+// sequence (tile mod 8, tile, column) is what it computes.  Every column's tile t then runs on
+// the XCD that runs tile t of every other column, and the forecast segments those tiles read
+// (near the tile's k range: k' ≈ k) are fetched into that XCD's L2 once, not once per XCD.
+// Work order only: the same values.  gx tiles per column, C columns (s blocks × ncl).
+__global__ __launch_bounds__(256) void ks_howard_slopes_xcd_kernel(KsArgs A,
+                                                                   const double* __restrict__ V,
+                                                                   const double* __restrict__ dV,
+                                                                   const double* __restrict__ k_opt,
+                                                                   double* __restrict__ Vn,
+                                                                   double* __restrict__ dVn, int O,
+                                                                   int gx, int C) {
+    __shared__ double s_v[256];
+    const int total = gx * C;
+    const int L = blockIdx.x, x = L & 7, r = L >> 3;
+    int start = 0;
+    for (int q = 0; q < x; ++q) start += (total - q + 7) >> 3;
+    int slot = start + r, g = 0;
+    for (; g < 8; ++g) {  // residue group g: tiles g, g + 8, ... of every column
+        const int tg = gx > g ? (gx - g + 7) >> 3 : 0;
+        if (slot < tg * C) break;
+        slot -= tg * C;
+    }
+    const int tile = g + 8 * (slot / C), cc = slot % C;
+    const int ncl = A.n_local / A.nk;
+    const int z = cc / ncl, y = cc - z * ncl;
+    const int col = A.node0 / A.nk + z * (A.sstride / A.nk) + y;
+    const KsView W{A.k_grid, V, dV};
+    howard_slopes_col<false>(A, W, col, k_opt, Vn, dVn, s_v, O, tile);
 }
 
 // The staged direct schedule's sweep: ONE launch per sweep.
@@ -610,6 +643,15 @@ int launch_ks_howard_slopes(const KsArgs& A, const double* V, const double* dV,
     const int O = ks_fused_geometry(A.nk, &B);
     const dim3 g(cdiv(A.nk, O), (unsigned)std::max(1, std::min(A.n_local / A.nk, 65535)),
                  std::max(A.ns, 1));
+    // dealt tile-major by XCD (ks_howard_slopes_xcd_kernel): 200 -> 194 us per sweep at
+    // k = 32,768, K = 64 (profiles/r06_g07_ks_xcd_ab.txt); the 3-D grid beyond 65,535 columns
+    if ((long long)g.x * g.y * g.z < (1ll << 31) && A.n_local / A.nk <= 65535) {
+        const int C = (int)g.y * (int)g.z;
+        ks_howard_slopes_xcd_kernel<<<dim3(g.x * C), B, 0, st>>>(A, V, dV, kopt, Vn, dVn, O,
+                                                                  (int)g.x, C);
+        AIY_HIP(hipGetLastError());
+        return AIY_OK;
+    }
     ks_howard_slopes_kernel<<<g, B, 0, st>>>(A, V, dV, kopt, Vn, dVn, O);
     AIY_HIP(hipGetLastError());
     return AIY_OK;

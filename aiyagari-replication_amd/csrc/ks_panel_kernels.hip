@@ -190,21 +190,36 @@ __global__ __launch_bounds__(256) void ks_panel_step_kernel(PanelArgs A, int t) 
     const int nk = A.nk, nK = A.nK;
     const double* kg = A.k_grid;
     const double* Kg = A.K_grid;
-    if constexpr (LDS) {
-        for (int q = threadIdx.x; q < nk; q += 256) grid_lds[q] = A.k_grid[q];
-        for (int q = threadIdx.x; q < nK; q += 256) grid_lds[nk + q] = A.K_grid[q];
-        kg = grid_lds;
-        Kg = grid_lds + nk;
-    }
     const int64_t L = (int64_t)A.G * 256;
     int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    // the grids' loads and the first agent's (prefetched before the partials are folded) all in
+    // flight before any LDS write: clamped, unguarded loads (a guarded load and its write in one
+    // loop waited for each load in turn — two round trips before the agent's)
+    double gk = 0.0, gK = 0.0;
+    const bool one = LDS && nk <= 256 && nK <= 256;  // (uniform) one grid value per thread
+    if (one) {
+        const int q = (int)threadIdx.x;
+        gk = A.k_grid[min(q, nk - 1)];
+        gK = A.K_grid[min(q, nK - 1)];
+    }
     const int zt = A.zi[t];
     const int8_t* __restrict__ erow = A.eps + (int64_t)t * A.ts;
-    double k = 0.0;
-    int e = 0;
-    if (i < A.pop) {           // first agent: prefetched before the partials are folded
-        k = A.k_pop[i];
-        e = erow[i * A.is];
+    const int64_t ic = i < A.pop ? i : 0;
+    const double k0 = A.k_pop[ic];
+    const int e0 = erow[ic * A.is];
+    const double k = i < A.pop ? k0 : 0.0;
+    const int e = i < A.pop ? e0 : 0;
+    if constexpr (LDS) {
+        if (one) {
+            const int q = (int)threadIdx.x;
+            if (q < nk) grid_lds[q] = gk;
+            if (q < nK) grid_lds[nk + q] = gK;
+        } else {
+            for (int q = threadIdx.x; q < nk; q += 256) grid_lds[q] = A.k_grid[q];
+            for (int q = threadIdx.x; q < nK; q += 256) grid_lds[nk + q] = A.K_grid[q];
+        }
+        kg = grid_lds;
+        Kg = grid_lds + nk;
     }
     double v[kFoldPer];
     if (threadIdx.x < 64) fold_load(A.part + (t & 1) * A.G, A.G, v);

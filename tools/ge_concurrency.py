@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--prio", action="store_true", help="solve streams at high priority")
     ap.add_argument("--excl", action="store_true", help="CU-exclusive sweep workgroups")
     ap.add_argument("--geo", default="", help="wide geometry S,NW,SB for the solve slots")
+    ap.add_argument("--chain-shared", action="store_true",
+                    help="chains without CU exclusivity (the GE driver sets it, round 6)")
+    ap.add_argument("--chain-nap", type=float, default=2e-4, help="host poll interval of a chain")
     args = ap.parse_args()
     import os
     if args.queues:
@@ -57,6 +60,9 @@ def main():
         if args.excl:
             sl.ws.set_cu_exclusive(True)
     sims = [ge._GESim(N, Na, dev) for _ in range(4)]
+    if args.chain_shared:
+        for sm in sims:
+            sm.ws.set_cu_exclusive(False)
     lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") else (0, -1)
     streams = [torch.cuda.Stream(device=dev, priority=(-1 if args.prio and q < 8 else 0))
                for q in range(12)]
@@ -82,7 +88,7 @@ def main():
             t0 = time.perf_counter()
             pkg.sim.sim_capital_dev(sm.ws, root.pk, a_t, P_t, 2, float(cal["a_grid"][100]), U,
                                     sm.k, sm.status, stream=st)
-        ge._wait_polled(st, nap=2e-4)
+        ge._wait_polled(st, nap=args.chain_nap)
         return time.perf_counter() - t0, 0
 
     res = {}
