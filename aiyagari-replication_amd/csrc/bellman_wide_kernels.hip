@@ -313,46 +313,53 @@ __global__ __launch_bounds__(64 * NW) void bell_wide_kernel(
     const int nbl = (kmax - 8 * gw0 + 8 * gstride - 1) / (8 * gstride);  // (wave-uniform)
     constexpr int VB = 4;
     if (LAB && nbl <= 2) {
-        // few blocks per level (small labour grids): the (level, block) pairs of this lane's
-        // slice flattened — pair p = level p / nbl, the lane's n-th block n = p mod nbl — and
-        // bound-tested VB at a time (independent chains across levels; one level at a time
-        // would test one or two blocks per dependent round)
-        const int npair = nbl > 0 ? Nl * nbl : 0;
-        const int lsh = nbl == 2 ? 1 : 0;  // pair p: level p >> lsh, the lane's (p & lsh)-th block
-        for (int p0 = 0; p0 < npair; p0 += VB) {
-            double cx[VB], dd[VB], tb[VB], coh[VB], dis[VB];
-            int lv[VB], k0v[VB], kev[VB];
-            // every LDS read of the VB pairs first, at indices clamped into range (no branch
-            // around a read: one wait for all of them), then the selects
-            double Lv[VB], av[VB], dmv[VB];
+        // few blocks per level (small labour grids): the lane's one or two blocks are the same
+        // at every level, so their a_{k0} and Dmax8 are read once; per level only the cash and
+        // the bar key change (computed once per level, not per (level, block) pair), and the
+        // pairs of VL levels are bound-tested together — VL·nbl independent tests per round
+        // (round 5: four pairs per round, every operand re-read and recomputed per pair,
+        // ≈ 170 VALU per round; profiles/r05_wide_ab.txt)
+        constexpr int VL = 5;
+        double avb[2], dmb[2];
+        int k0b[2];
 #pragma unroll
-            for (int v = 0; v < VB; ++v) {
-                const int pp = min(p0 + v, npair - 1);
-                const int l = pp >> lsh;
-                lv[v] = l;
-                k0v[v] = 8 * (gw + (pp & lsh) * gstride);
-                const int kc = min(k0v[v], Na - 1);
-                kev[v] = s_kfl[l];
+        for (int q = 0; q < 2; ++q) {
+            k0b[q] = 8 * (gw + q * gstride);
+            const int kc = min(k0b[q], Na - 1);
+            avb[q] = s_tab[kc].x;
+            dmb[q] = s_dm8[kc >> 3];
+        }
+        for (int l0 = 0; l0 < Nl; l0 += VL) {
+            double Lv[VL], dsv[VL], cohv[VL], Bv[VL], tb[2 * VL], cx[2 * VL], dd[2 * VL];
+            int kev[VL];
+#pragma unroll
+            for (int v = 0; v < VL; ++v) {  // (reads first, clamped: one LDS wait)
+                const int l = min(l0 + v, Nl - 1);
                 Lv[v] = s_L[l];
-                dis[v] = s_dis[l];
-                av[v] = s_tab[kc].x;
-                dmv[v] = s_dm8[kc >> 3];
+                dsv[v] = s_dis[l];
+                kev[v] = s_kfl[l];
             }
 #pragma unroll
-            for (int v = 0; v < VB; ++v) {
-                coh[v] = okj ? cash<LAB>(x, y, Lv[v]) : 0.0;
-                const double B = okj ? screen_B(best, idx, dis[v], NP) : __builtin_nan("");
-                const bool okb = p0 + v < npair && k0v[v] < kev[v];
-                cx[v] = okb ? coh[v] - av[v] : -1.0;
-                dd[v] = okb ? dmv[v] - B : __builtin_nan("");
+            for (int v = 0; v < VL; ++v) {
+                cohv[v] = okj ? cash<LAB>(x, y, Lv[v]) : 0.0;
+                Bv[v] = okj ? screen_B(best, idx, dsv[v], NP) : __builtin_nan("");
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const bool okb = l0 + v < Nl && q < nbl && k0b[q] < kev[v];
+                    cx[2 * v + q] = okb ? cohv[v] - avb[q] : -1.0;
+                    dd[2 * v + q] = okb ? dmb[q] - Bv[v] : __builtin_nan("");
+                }
             }
             AIY_SCHED_BARRIER();
-            screen_t<NP, VB>(tb, cx, dd);
-            ntests += VB;  // (bound tests, counted per lane like the candidates)
+            screen_t<NP, 2 * VL>(tb, cx, dd);
+            ntests += 2 * VL;  // (bound tests, counted per lane like the candidates)
             if (TR) ++nrnd;
 #pragma unroll
-            for (int v = 0; v < VB; ++v)
-                if (__any(tb[v] >= kThr)) block(lv[v], k0v[v], kev[v], coh[v], dis[v]);
+            for (int v = 0; v < VL; ++v)
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+                    if (__any(tb[2 * v + q] >= kThr))
+                        block(l0 + v, k0b[q], kev[v], cohv[v], dsv[v]);
         }
     } else {
         // level by level, VB of the lane's blocks bound-tested at a time
