@@ -244,9 +244,9 @@ def aiyagari_vfi_overlapped(Na=400, rho=0.75, sigma_e=0.75, shocks="tauchen", T=
                             sim.k, sim.status, stream=stream)
             sim.kh.copy_(sim.k, non_blocking=True)
             sim.sh.copy_(sim.status, non_blocking=True)
-        # a chain runs ~2.5 ms: poll its event instead of a blocking synchronize (a thread
+        # a chain runs ~1.6 ms: poll its event instead of a blocking synchronize (a thread
         # parked in a synchronize slowed the other threads' launches 2-3x)
-        _wait_polled(stream, nap=2e-4)
+        _wait_polled(stream, nap=_CHAIN_NAP)
         streams.put(stream)
         if int(sim.sh[0]) != 0:
             raise RuntimeError("find() empty in the capital-supply chain (Aiyagari_VFI.m:106)")
@@ -480,6 +480,11 @@ class _GESim:
         torch.cuda.current_stream(dev).synchronize()
 
 
+# host poll interval of a Monte-Carlo chain's completion (seconds; AIY_GE_CHAIN_NAP for A/B):
+# 20 us, not 200 — the step after a chain waits for its K_s (GE wall 25.1 -> 22.9 ms median over
+# three alternating rounds; busy polling 23.6)
+import os as _os  # noqa: E402
+_CHAIN_NAP = float(_os.environ.get("AIY_GE_CHAIN_NAP", "2e-5"))  # profiles/r06_g15_ge_chain_nap.txt
 _GE_POOLS = {}  # (device, N, Na) -> (solve slots, chain resources) of aiyagari_vfi_overlapped
 _GE_STREAMS = {}  # device -> the driver's streams
 

@@ -28,14 +28,22 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
-# hardware queues per process (HIP's default is 4): the GE drivers run speculative solves and
-# 2.7 ms Monte-Carlo chains on their own streams, and a stream sharing a queue with a chain
-# waits behind it (ge.aiyagari_vfi_overlapped; tools/ge_concurrency.py: with 4 queues two
-# solves beside two chains ran 2.6x slower).  Raised (never lowered) before the HIP runtime starts:
-# an inherited smaller value (the GPU box exports 4) would otherwise win.
+# hardware queues per process (HIP's default is 4): the GE driver runs up to two speculative
+# solves and two Monte-Carlo chains on their own streams, and with 4 queues streams share them —
+# a solve queued behind a 1.6 ms chain waits for it (tools/ge_concurrency.py, profiles/
+# r06_g14_hw_queues.txt: 2 solves + 2 chains 3.2 ms at 4 queues, 2.9 at 16; 4 solves 2.7 vs
+# 1.8 ms).  More than ~4 busy queues degrade instead (6 solves: 5.9 ms at 16 queues, 3.1 at 4 —
+# the driver stays at lookahead 1).  Raised (never lowered) by bench.py's main only, before the
+# HIP runtime starts; the GE leg reports the wall at the inherited value too.
 HW_QUEUES_INHERITED = os.environ.get("GPU_MAX_HW_QUEUES")  # recorded in ge_equilibrium
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:
-    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+
+
+def raise_hw_queues():
+    """bench.py's own process only (called first in main, before the HIP runtime starts; an
+    import of this module changes nothing — tools/ge_wall_probe.py measures the inherited
+    value through that)."""
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:
+        os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 PEAK_FP64_TFLOPS = 78.6   # MI355X fp64 vector (= fp64 matrix) peak, datasheet
 FLOPS_PER_CANDIDATE = 8  # SURVEY §8(d) D3: sub, mul, mul, div, sub, mul, add, max
@@ -225,6 +233,7 @@ def main():
                     help="launcher/contract check without a GPU: gloo ranks, a trivial timed "
                          "CPU loop, the same barrier/max-over-ranks/contract line")
     args = ap.parse_args()
+    raise_hw_queues()
 
     import bench_launch
     # --gpus N without a launcher: start N ranks (child torch.distributed.run), exit with its rc

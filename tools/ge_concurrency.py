@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--cases", default="1:0,2:0,4:0,8:0,1:1,2:2,4:2,0:1",
                     help="solves:chains pairs")
     ap.add_argument("--specs", default="16,64")
-    ap.add_argument("--queues", type=int, default=0, help="GPU_MAX_HW_QUEUES (0: bench's)")
+    ap.add_argument("--queues", type=int, default=0, help="GPU_MAX_HW_QUEUES (0: inherited)")
     ap.add_argument("--prio", action="store_true", help="solve streams at high priority")
     ap.add_argument("--excl", action="store_true", help="CU-exclusive sweep workgroups")
     ap.add_argument("--geo", default="", help="wide geometry S,NW,SB for the solve slots")
