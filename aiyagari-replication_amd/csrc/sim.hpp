@@ -25,6 +25,10 @@ struct SimArgs {
     // shares the chain's CU — opt-in (aiy_ws_set_cu_exclusive on the chain's workspace; the GE
     // driver sets it), ADVICE r5
     bool exclusive;
+    // the speculative-segment chain (sim_chain_par_kernel): the k path's scratch, T doubles per
+    // chain (null: the serial kernels); par: -1 by size, 0 never, 1 whenever it applies
+    double* kscr;
+    int par;
 };
 int launch_sim_capital(const SimArgs& A, hipStream_t st);
 }  // namespace aiy

@@ -15,7 +15,7 @@ namespace aiy {
 int sim_capital_dev(const double* pol, size_t zs, size_t as, const double* a, const double* P,
                     int64_t N, int64_t Na, int64_t z1, double k1, int64_t T, const double* U,
                     double* out, double* sim_k, int* sim_z, int* status, hipStream_t st,
-                    bool exclusive = false) {
+                    bool exclusive = false, double* kscr = nullptr, int par = -1) {
     if (!pol || !a || !P || !out || !status || (T > 1 && !U))
         return fail(AIY_BAD_ARG, "NULL argument");
     if (T < 1 || T > (1ll << 31) - 1) return fail(AIY_BAD_SHAPE, "T must be in [1, 2^31)");
@@ -25,6 +25,8 @@ int sim_capital_dev(const double* pol, size_t zs, size_t as, const double* a, co
     A.pol = pol; A.zs = zs; A.as = as; A.a = a; A.P = P; A.U = U;
     A.out = out; A.sim_k = sim_k; A.sim_z = sim_z; A.status = status;
     A.exclusive = exclusive;
+    A.kscr = kscr;
+    A.par = par;
     return launch_sim_capital(A, st);
 }
 
@@ -61,8 +63,10 @@ int aiy_sim_capital(const double* policy_k, int vfi_layout, const double* a_grid
         AIY_HIP(hipMemcpyAsync(dU, uniforms, sizeof(double) * (T - 1), hipMemcpyHostToDevice, c->st));
     // MATLAB layouts: VFI policy_k is N x Na (z stride 1, a stride N); EGM is Na x N.
     size_t zs = vfi_layout ? 1 : (size_t)Na, as = vfi_layout ? (size_t)N : 1;
+    double* dks = nullptr;  // the speculative-segment chain's path scratch
+    AIY_TRY(c->buf("sim_kscr", sizeof(double) * T, (void**)&dks));
     AIY_TRY(sim_capital_dev(dpol, zs, as, da, dP, N, Na, z1 - 1, k1, T, dU, dout, dk, dz, dst,
-                            c->st));
+                            c->st, false, dks, c->ws ? c->ws->sim_par : -1));
     double out;
     int status;
     AIY_HIP(hipMemcpyAsync(&out, dout, sizeof(double), hipMemcpyDeviceToHost, c->st));
@@ -89,9 +93,24 @@ int aiy_sim_capital_dev(aiy_ws* ws, const double* policy_rows, const double* a_g
                         const double* uniforms, double* k_supply, double* sim_k,
                         int32_t* sim_z, int32_t* status, void* stream) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
+    if (T >= 2 && ws->sim_par != 0 && ws->sim_kcap < (size_t)T) {  // path scratch (per workspace)
+        if (ws->sim_kbuf) AIY_HIP(hipFree(ws->sim_kbuf));
+        ws->sim_kbuf = nullptr;
+        ws->sim_kcap = 0;
+        AIY_HIP(hipMalloc((void**)&ws->sim_kbuf, sizeof(double) * (size_t)T));
+        ws->sim_kcap = (size_t)T;
+    }
     return sim_capital_dev(policy_rows, (size_t)ws->Na, 1, a_grid, P, ws->N, ws->Na, z1, k1, T,
                            uniforms, k_supply, sim_k, sim_z, status, (hipStream_t)stream,
-                           ws->cu_exclusive);
+                           ws->cu_exclusive, ws->sim_par != 0 ? ws->sim_kbuf : nullptr,
+                           ws->sim_par);
+}
+
+int aiy_ws_set_sim(aiy_ws* ws, int mode) {
+    if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
+    if (mode < -1 || mode > 1) return fail(AIY_BAD_ARG, "mode: -1 (by size), 0 or 1");
+    ws->sim_par = mode;
+    return AIY_OK;
 }
 
 }  // extern "C"

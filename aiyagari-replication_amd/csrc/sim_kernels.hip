@@ -508,6 +508,311 @@ __global__ __launch_bounds__(128) void sim_chain_pipe_kernel(SimArgs A0) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Speculative segments (round 6).  The chain is serial, but its two recurrences forget where
+// they started: z_t = find(u_t < cumsum(P(z_{t-1},:)), 1) is a composition of maps of a set of
+// N states, and k_t = interp1(a, policy_k(z_t,:), k_{t-1}) contracts — two paths driven by the
+// same shocks become bit-identical after a few dozen steps (Aiyagari_VFI.m's policy at r = 0.04:
+// 1 to 187 steps from any start, tools/sim_coalesce.py) and stay identical.  So, in ONE
+// workgroup of 16 waves:
+//   Z. every thread builds the step maps of its share of t (3 bits per state, 7 = find() empty,
+//      absorbing), the block scans their compositions (a Hillis-Steele scan of composed maps),
+//      and each thread applies its prefix to z1 and walks its share: z_t for all t, in LDS, and
+//      the first empty find() (the chain stops there, as the serial kernel does);
+//   K. wave s runs segment s of the k chain, steps [1 + sL, 1 + (s+1)L), from k1 (s = 0) or a
+//      guess (k1), with the serial kernel's step (64-lane window, the same operations), storing
+//      the path; then repair passes: wave s restarts from the (true) last value of segment s-1
+//      and steps until its value equals the stored one bit for bit — from there the stored
+//      path is the true one — or overwrites its whole segment; a segment is true once its
+//      predecessor was true when its pass started, or became true in the same pass without
+//      changing its last value.  Passes repeat until every segment is true (at most 15; one
+//      in practice);
+//   S. wave 0 sums the path in order (the serial kernel's fp64 accumulation, bit for bit).
+// The path, hence K_s, is the serial chain's bit for bit whatever the guesses: every stored
+// value is either computed from the true predecessor or equal to such a value.
+constexpr int kParWaves = 16;
+constexpr int kParMaxT = 16384;  // z_t in LDS (one byte each)
+
+// k_t = interp1(a_grid, policy_k(z_t,:), k_{t-1}) by one wave, the window of sim_chain_pipe_kernel
+template <int SS>
+struct ParStepper {
+    const double* X0;
+    const double* H;
+    const double* Y;
+    int Na, wmax, lane, w0;
+    bool primed;
+    double x0, h, y0, dy;
+    __device__ __forceinline__ void ldwin(int w, int zo) {
+        const int p = w + lane;
+        x0 = X0[p];
+        h = H[p];
+        const double2 yy = *reinterpret_cast<const double2*>(reinterpret_cast<const char*>(Y) + zo + 16 * p);
+        y0 = yy.x;
+        dy = yy.y;
+    }
+    // zo: byte offset of row z_t in Y; zo1: of row z_{t+1} (its window is loaded under the division)
+    __device__ __forceinline__ double step(double k, int zo, int zo1) {
+        if (__builtin_expect(!primed, 0)) {
+            ldwin(w0, zo);
+            primed = true;
+        }
+        const int c = __popcll(__ballot(x0 <= k));
+        int sl = min(c - 1, Na - 2 - w0);
+        sl = sl < 0 ? 0 : sl;
+        int seg = w0 + sl;
+        const int hit = ((c > 0) | (w0 == 0)) & ((c < 64) | (w0 == wmax));
+        int w0n = seg - 31;
+        w0n = w0n < 0 ? 0 : (w0n > wmax ? wmax : w0n);
+        const double d = k - x0;
+        const double ch = h, cy0 = y0, cdy = dy;
+        ldwin(w0n, zo1);
+        __builtin_amdgcn_sched_barrier(0);
+        const double kn = cy0 + (d / ch) * cdy;
+        double kw = readlane_d(kn, sl);
+        if (__builtin_expect(!hit, 0)) {  // the window missed k: 64-ary search
+            int lo = 0, hi = Na;
+            while (hi - lo > 64) {
+                int stp = (hi - lo + 63) / 64;
+                int pp = lo + lane * stp;
+                bool le = pp < hi && X0[pp] <= k;
+                int cc = __popcll(__ballot(le));
+                if (cc == 0) {
+                    hi = lo;
+                    break;
+                }
+                lo = lo + (cc - 1) * stp;
+                hi = min(lo + stp, hi);
+            }
+            int pp = lo + lane;
+            int cc = __popcll(__ballot(pp < hi && X0[pp] <= k));
+            seg = lo + cc - 1;
+            seg = seg < 0 ? 0 : (seg > Na - 2 ? Na - 2 : seg);
+            w0n = seg - 31;
+            w0n = w0n < 0 ? 0 : (w0n > wmax ? wmax : w0n);
+            primed = false;
+            const double T0 = (k - X0[seg]) / H[seg];
+            const double* Yz = reinterpret_cast<const double*>(reinterpret_cast<const char*>(Y) + zo) + 2 * seg;
+            kw = Yz[0] + T0 * Yz[1];
+        }
+        w0 = w0n;
+        return kw;
+    }
+};
+
+__device__ __forceinline__ unsigned zmap_compose(unsigned A, unsigned B) {  // A, then B
+    unsigned R = 0;
+#pragma unroll
+    for (int z = 0; z < 8; ++z) R |= ((B >> (3 * ((A >> (3 * z)) & 7u))) & 7u) << (3 * z);
+    return R;
+}
+
+template <int SS, bool PATH>
+__global__ __launch_bounds__(1024) void sim_chain_par_kernel(SimArgs A0) {
+    SimArgs A = A0;
+    double* kp = A0.kscr;
+    if (A0.C > 1) {
+        A.pol += blockIdx.x * A0.pcs;
+        A.U += blockIdx.x * A0.ucs;
+        A.out += blockIdx.x;
+        A.status += blockIdx.x;
+        kp += (size_t)blockIdx.x * A0.T;
+    }
+    if (PATH && A.sim_k) kp = A.sim_k;  // the path is the output itself
+    extern __shared__ double lds[];  // X0[SS] | H[SS] | Y[N][SS][2] = {y_i, y_{i+1} - y_i}
+    __shared__ unsigned char zp[kParMaxT];
+    __shared__ unsigned s_map[1024];
+    __shared__ double s_cs[64];
+    __shared__ int s_stop, s_go;
+    __shared__ int s_res[kParWaves], s_chg[kParWaves];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int N = A.N, Na = A.Na, T = A.T;
+    double* X0 = lds;
+    double* H = lds + SS;
+    double* Y = lds + 2 * SS;
+    for (int i = tid; i < SS; i += 1024) {
+        const double x0 = A.a[min(i, Na - 1)], x1 = A.a[min(i + 1, Na - 1)];
+        X0[i] = x0;
+        H[i] = x1 - x0;
+    }
+    for (int q = tid; q < N * SS; q += 1024) {
+        const int zz = q / SS, i = q - zz * SS;
+        const double* row = A.pol + (size_t)zz * A.zs;
+        const double y0 = i < Na ? row[(size_t)i * A.as] : 0.0;
+        const double y1 = i + 1 < Na ? row[(size_t)(i + 1) * A.as] : 0.0;
+        Y[2 * (size_t)q] = y0;
+        Y[2 * (size_t)q + 1] = y1 - y0;
+    }
+    if (tid < 64) {  // cumsum(P(z,:))(m) in order (as cumsum), lanes 8z + m
+        const int zz = tid >> 3, m = tid & 7;
+        double acc = 0.0;
+        if (zz < N && m < N)
+            for (int q = 0; q <= m; ++q) acc = acc + A.P[zz * N + q];
+        s_cs[tid] = acc;
+    }
+    if (tid == 0) s_stop = T;
+    __syncthreads();
+
+    // Z. the state path
+    const int nst = T - 1;                             // steps 1 .. T-1 use u[t - 1]
+    const int ch = (nst + 1023) / 1024;                // steps per thread
+    const int t0 = 1 + tid * ch, t1 = min(T, t0 + ch);
+    auto zmap = [&](int t) __attribute__((always_inline)) -> unsigned {
+        const double u = A.U[t - 1];
+        unsigned M = 7u << 21;  // entry 7 -> 7 (absorbing "find() empty")
+#pragma unroll
+        for (int z = 0; z < 7; ++z) {
+            int e = 7;
+#pragma unroll
+            for (int m = 7; m >= 0; --m)
+                if (z < N && m < N && u < s_cs[8 * z + m]) e = m;  // the first m with u < cumsum
+            M |= (unsigned)e << (3 * z);
+        }
+        return M;
+    };
+    unsigned agg = 0;
+#pragma unroll
+    for (int z = 0; z < 8; ++z) agg |= (unsigned)z << (3 * z);  // identity
+    const unsigned ident = agg;
+    for (int t = t0; t < t1; ++t) agg = zmap_compose(agg, zmap(t));
+    s_map[tid] = agg;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {  // inclusive scan of the compositions
+        const unsigned prev = tid >= off ? s_map[tid - off] : ident;
+        __syncthreads();
+        if (tid >= off) s_map[tid] = zmap_compose(prev, s_map[tid]);
+        __syncthreads();
+    }
+    {
+        const unsigned pre = tid > 0 ? s_map[tid - 1] : ident;
+        int z = (int)((pre >> (3 * A.z1)) & 7u);
+        int first_bad = T;
+        for (int t = t0; t < t1; ++t) {
+            z = (int)((zmap(t) >> (3 * z)) & 7u);
+            zp[t] = (unsigned char)z;
+            if (z == 7 && first_bad == T) first_bad = t;
+        }
+        if (first_bad < T) atomicMin(&s_stop, first_bad);
+        if (tid == 0) zp[0] = (unsigned char)A.z1;
+    }
+    __syncthreads();
+    const int Te = s_stop;  // steps 1 .. Te-1 run (Te < T: find() empty at step Te)
+    const int zrow = SS * 16;
+    auto zo_of = [&](int t) __attribute__((always_inline)) {
+        return t < Te ? (int)zp[t] * zrow : 0;
+    };
+
+    // K. segments, then repairs
+    const int L = (Te - 1 + kParWaves - 1) / kParWaves;  // >= 0
+    const int Ts = 1 + wave * L, Tn = min(Te, Ts + L);
+    ParStepper<SS> ps{X0, H, Y, Na, Na - 64, lane, 0, false, 0.0, 0.0, 0.0, 0.0};
+    if (Ts < Tn) {
+        double k = A.k1;
+        for (int t = Ts; t < Tn; ++t) {
+            k = ps.step(k, zo_of(t), zo_of(t + 1));
+            if (lane == 0) kp[t] = k;
+        }
+    }
+    if (tid == 0) kp[0] = A.k1;
+    if (lane == 0) {
+        s_res[wave] = wave == 0 ? 1 : (Ts < Tn ? 0 : 1);  // (empty segments are trivially true)
+        s_chg[wave] = 0;
+    }
+    __syncthreads();
+    for (;;) {
+        if (tid == 0) {
+            int go = 0;
+            for (int q = 0; q < kParWaves; ++q) go |= !s_res[q];
+            s_go = go;
+        }
+        __syncthreads();
+        if (!s_go) break;
+        const bool mine = !s_res[wave];
+        double k = mine ? kp[Ts - 1] : 0.0;  // every start read before any repair writes
+        __syncthreads();
+        int chg = 0;
+        if (mine) {
+            ps.primed = false;
+            for (int t = Ts; t < Tn; ++t) {
+                k = ps.step(k, zo_of(t), zo_of(t + 1));
+                const unsigned long long kb = __builtin_bit_cast(unsigned long long, k);
+                const unsigned long long sb = __builtin_bit_cast(unsigned long long, kp[t]);
+                if (kb == sb) break;  // the stored path is the true one from here
+                if (lane == 0) kp[t] = k;
+                if (t == Tn - 1) chg = 1;
+            }
+        }
+        if (lane == 0) s_chg[wave] = chg;
+        __syncthreads();
+        if (tid == 0) {
+            int prev_old = s_res[0], prev_new = 1;
+            for (int q = 1; q < kParWaves; ++q) {
+                const int old = s_res[q];
+                const int nw = old || prev_old || (prev_new && !s_chg[q - 1]);
+                prev_old = old;
+                prev_new = nw;
+                s_res[q] = nw;
+            }
+        }
+        __syncthreads();
+    }
+    // S. the mean (sequential fp64 sum, k_0 .. k_{Te-1}) and the outputs
+    if (wave == 0) {
+        double v = lane < Te ? kp[lane] : 0.0;
+        double sum = readlane_d(v, 0);  // sum = k_1 (the serial kernel's start), then in order
+        for (int c0 = 0; c0 < Te; c0 += 64) {
+            const double vn = c0 + 64 + lane < Te ? kp[c0 + 64 + lane] : 0.0;
+            const int n = min(64, Te - c0);
+            if (n == 64 && c0 > 0) {
+#pragma unroll
+                for (int j = 0; j < 64; ++j) sum = sum + readlane_d(v, j);
+            } else {
+                for (int j = c0 == 0 ? 1 : 0; j < n; ++j) sum = sum + readlane_d(v, j);
+            }
+            v = vn;
+        }
+        if (lane == 0) {
+            A.out[0] = sum / (double)A.T;
+            A.status[0] = Te < T ? 1 : 0;
+        }
+    }
+    if (PATH && A.sim_z)
+        for (int t = tid; t < Te; t += 1024) A.sim_z[t] = zp[t];
+}
+
+// the speculative-segment chain; AIY_BAD_SHAPE when it does not apply
+int launch_sim_chain_par(const SimArgs& A, hipStream_t st) {
+    if (A.N < 1 || A.N > 7 || A.Na < 64 || A.T < 2 || A.T > kParMaxT || !A.kscr)
+        return fail(AIY_BAD_SHAPE, "speculative chain: N <= 7, Na >= 64, 2 <= T <= 16384, scratch");
+    const int S = A.Na + 64;
+    const int SS = S <= 512 ? 512 : (S <= 1024 ? 1024 : 0);
+    if (!SS) return fail(AIY_BAD_SHAPE, "speculative chain tables exceed LDS");
+    const size_t bytes = sizeof(double) * (size_t)(2 + 2 * A.N) * SS;
+    const int g = std::max(A.C, 1);
+    const bool path = A.sim_k || A.sim_z;
+#define AIY_PAR(SS_, PA_)                                                                          \
+    do {                                                                                           \
+        static std::atomic<bool> lds_set{false};                                                   \
+        if (!lds_set) {                                                                            \
+            AIY_HIP(hipFuncSetAttribute((const void*)sim_chain_par_kernel<SS_, PA_>,               \
+                                        hipFuncAttributeMaxDynamicSharedMemorySize,                \
+                                        (int)sizeof(double) * (2 + 2 * 7) * SS_));                 \
+            lds_set = true;                                                                        \
+        }                                                                                          \
+        sim_chain_par_kernel<SS_, PA_><<<g, 1024, bytes, st>>>(A);                                 \
+    } while (0)
+    if (SS == 512) {
+        if (path) AIY_PAR(512, true);
+        else AIY_PAR(512, false);
+    } else {
+        if (path) AIY_PAR(1024, true);
+        else AIY_PAR(1024, false);
+    }
+#undef AIY_PAR
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
+}
+
 // the two-wave chain; AIY_BAD_SHAPE when it does not apply (N > 8, Na < 64, tables past LDS)
 int launch_sim_chain_pipe(const SimArgs& A, hipStream_t st) {
     if (A.N < 1 || A.N > 8 || A.Na < 64) return fail(AIY_BAD_SHAPE, "pipe chain: N <= 8, Na >= 64");
@@ -546,6 +851,10 @@ int launch_sim_chain_pipe(const SimArgs& A, hipStream_t st) {
 int launch_sim_capital(const SimArgs& A, hipStream_t st) {
     if (A.N > 16 || A.N < 1) return fail(AIY_BAD_SHAPE, "simulation supports 1 <= N <= 16");
     const long long need = (long long)A.Na * (A.N + 1);
+    // the speculative-segment chain for the GE loop's long chains (T = 10,000: 1.6 ms serial)
+    const bool par_ok = A.kscr && A.N <= 7 && A.Na >= 64 && A.Na + 64 <= 1024 && A.T >= 2 &&
+                        A.T <= kParMaxT;
+    if (par_ok && (A.par > 0 || (A.par < 0 && A.T >= 2048))) return launch_sim_chain_par(A, st);
     if (A.N <= 8 && A.Na >= 64 && (A.Na + 64 <= 512 || (A.Na + 64 <= 1024 && A.N <= 7)))
         return launch_sim_chain_pipe(A, st);
     if (A.N <= 15) {

@@ -50,6 +50,11 @@ struct aiy_ws {
     // Na <= wide_max (-1: the default bound) with `wide_S` splits of `wide_NW` waves (0: by size)
     int wide_max = -1, wide_S = 0, wide_NW = 0, wide_SB = 0;
     bool cu_exclusive = false;  // aiy_ws_set_cu_exclusive
+    // A9 chains (aiy_ws_set_sim): -1 by size, 0 the serial kernels, 1 the speculative-segment
+    // kernel whenever it applies; its k-path scratch
+    int sim_par = -1;
+    double* sim_kbuf = nullptr;
+    size_t sim_kcap = 0;
     unsigned long long* wdiff = nullptr;  // device [2][2*kDiffSlots]: the set not current is zero
     int wcur = 0;                         // the set the last wide sweep wrote
     unsigned* wcnt = nullptr;             // device [N·ntile] per-tile arrival counters (zero)
@@ -180,7 +185,7 @@ struct aiy_ws {
     void free_all() {
         void* ps[] = {EV, T, T32, Dm, Dm8, Dt, Dm512, touched, best0, idx0, mom, dis, kf, partial, diff, hitcount, trace, g0, g1, g2, gi,
                       d_key, d_off, d_wr, d_mass, d_part, egm_x2, egm_y2, egm_seg, tree_perm,
-                      kf_last, wdiff, wcnt, wpart};
+                      kf_last, wdiff, wcnt, wpart, sim_kbuf};
         for (void* p : ps)
             if (p) (void)hipFree(p);
         free_spec();
@@ -197,6 +202,7 @@ struct aiy_ws {
         tree_perm = nullptr; perm_cap = 0; perm_ok = false;
         kf_last = nullptr; kf_last_cap = 0;
         wdiff = nullptr; wcnt = nullptr; wcnt_cap = 0; wpart = nullptr; wpart_cap = 0; wcur = 0;
+        sim_kbuf = nullptr; sim_kcap = 0;
         last_wide = false; vdiff = nullptr; dis_ok = false;
         d_key = d_off = nullptr; d_wr = d_mass = d_part = nullptr;
         partial_cap = 0;

@@ -140,6 +140,12 @@ class Workspace:
         running concurrently on other streams.  Results do not depend on it."""
         check(lib().aiy_ws_set_cu_exclusive(self._h, ip(int(bool(on)))))
 
+    def set_sim(self, mode: int = -1):
+        """A9 chains on this workspace (aiy_ws_set_sim): -1 by size (the speculative-segment
+        chain for long chains), 0 the serial kernels, 1 the speculative chain wherever it
+        applies.  Results do not depend on it."""
+        check(lib().aiy_ws_set_sim(self._h, ip(int(mode))))
+
     def set_search(self, coarse_stride=0, k_chunk=1024):
         check(lib().aiy_ws_set_search(self._h, ip(coarse_stride), ip(k_chunk)))
 

@@ -266,6 +266,13 @@ int aiy_ws_set_wide(aiy_ws* ws, int max_na, int splits, int waves, int states);
  * sharing its CU with another solve's becomes the straggler of its sweep.  Default 0.  Results do
  * not depend on it. */
 int aiy_ws_set_cu_exclusive(aiy_ws* ws, int on);
+/* The A9 chain (aiy_sim_capital_dev) on this workspace: mode -1 (default) runs the speculative-
+ * segment chain (16 waves each run a segment of the k recurrence from a guess, then repair it
+ * from its predecessor's true end until the stored path matches bit for bit; the state path by a
+ * parallel scan of composed transition maps) for 2,048 <= T <= 16,384, N <= 7, 64 <= Na <= 960,
+ * the serial kernels otherwise; 0: always the serial kernels; 1: the speculative chain wherever
+ * it applies.  Results (K_s, the paths, find() errors) are identical for every mode. */
+int aiy_ws_set_sim(aiy_ws* ws, int mode);
 /* kernel shapes and A/B knobs (tuning only; results are identical for every value in
  * [-1, 2^26)).  VFI, bit 3 clear (default): the bound tree screen, bit 0 = 2 states per lane
  * (else 1), bits 1-2 = 1, 2, 4 or 8 cooperating waves per tile, bit 4 = XCD-aware tile order,

@@ -14,13 +14,16 @@ import bench  # noqa: E402
 pkg = bench.load_pkg()
 dev = torch.device("cuda:0")
 t = lambda x: torch.as_tensor(np.ascontiguousarray(x), device=dev)
-for Na in (400, 1900, 20000):
+import os
+modes = [int(x) for x in os.environ.get("SIM_MODES", "-1,0").split(",")]
+for Na, mode in [(n, m) for n in (400, 900, 1900, 20000) for m in modes]:
     cal = pkg.calibration.aiyagari(Na=Na)
     r = 0.04
     w = pkg.calibration.wage(r, cal["alpha"], cal["delta"])
     R = pkg.vfi_solve(np.zeros((cal["N"], Na)), cal["a_grid"], cal["s"], cal["P"], r, w,
                       cal["beta"], cal["sigma"], 1e-5, 1000)
     ws = pkg.Workspace(cal["N"], Na)
+    ws.set_sim(mode)
     U = t(np.random.default_rng(0).random(9999))
     pol, a_t, P_t = t(R["policy_k"]), t(cal["a_grid"]), t(cal["P"])
     ks = torch.zeros(1, dtype=torch.float64, device=dev)
@@ -34,6 +37,6 @@ for Na in (400, 1900, 20000):
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 20
-    print(json.dumps({"Na": Na, "T": 10000, "ms_per_chain": ms, "ns_per_step": ms * 1e6 / 1e4,
+    print(json.dumps({"Na": Na, "sim_mode": mode, "T": 10000, "ms_per_chain": ms, "ns_per_step": ms * 1e6 / 1e4,
                       "K_s": float(ks[0]), "status": int(st[0])}))
     ws.close()
