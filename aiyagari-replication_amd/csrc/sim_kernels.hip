@@ -513,7 +513,7 @@ __global__ __launch_bounds__(128) void sim_chain_pipe_kernel(SimArgs A0) {
 // they started: z_t = find(u_t < cumsum(P(z_{t-1},:)), 1) is a composition of maps of a set of
 // N states, and k_t = interp1(a, policy_k(z_t,:), k_{t-1}) contracts — two paths driven by the
 // same shocks become bit-identical after a few dozen steps (Aiyagari_VFI.m's policy at r = 0.04:
-// 1 to 187 steps from any start, tools/sim_coalesce.py) and stay identical.  So, in ONE
+// at most ~210 steps from any start, tools/sim_coalesce.py) and stay identical.  So, in ONE
 // workgroup of 16 waves:
 //   Z. every thread builds the step maps of its share of t (3 bits per state, 7 = find() empty,
 //      absorbing), the block scans their compositions (a Hillis-Steele scan of composed maps),
