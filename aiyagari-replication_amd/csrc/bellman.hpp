@@ -26,6 +26,7 @@ struct BellArgs {
     int* mom;           // nullable [N][Na]: the argmax's shift in k over the last hinted sweep
     const int* perm;    // nullable [N·ntile]: tree dispatch order (block b → item perm[b]); see
                         // ws_tree_perm — work order only
+    int perm_slots;     // entries of perm (the hybrid launch runs perm_slots / 2 workgroups)
     int tw;             // tree tile width (states per one-wave tile, R = 1); 0 = 64
                         // (tree kernel: read for an extrapolated start, rewritten; heuristic
                         // only — any start is a valid screening bar)
@@ -82,9 +83,18 @@ inline int bell_tile_width(const BellArgs& A, int R) { return (R == 1 && A.tw > 
 // permutation (A.perm, which then holds -1 in the last workgroup's unused slots); instantiated
 // for A1 at sigma = 5 (np = 4), one state per lane, one wave per tile
 inline int bell_tree_pack(const BellArgs& A) {
-    return (A.np == 4 && !A.labor && A.tree && (A.variant & (1 | 2 | 4 | 8)) == 0)
-               ? 1 << ((A.variant >> 16) & 3)
-               : 1;
+    if (!(A.np == 4 && !A.labor && A.tree && (A.variant & (1 | 2 | 4 | 8)) == 0)) return 1;
+    return (A.variant & (1 << 26)) ? 2 : 1 << ((A.variant >> 16) & 3);
+}
+// variant bit 26 (with a permutation): the hybrid launch, two-wave workgroups that run either
+// two one-wave tiles or one heavy tile on both waves; bits 27-29: cooperative tiles per XCD
+// range, 8 << value (7: none)
+inline bool bell_tree_hybrid(const BellArgs& A) {
+    return (A.variant & (1 << 26)) && bell_tree_pack(A) == 2;
+}
+inline int bell_tree_coop_per_xcd(const BellArgs& A) {
+    const int v = (A.variant >> 27) & 7;
+    return v == 7 ? 0 : 8 << v;  // (7: none — the hybrid launch's own cost, for A/B)
 }
 // The small-grid sweep (bellman_wide_kernels.hip): ONE launch per sweep, a workgroup of NW
 // waves per (64-state tile, split of the candidate range), S splits per tile.  Every workgroup

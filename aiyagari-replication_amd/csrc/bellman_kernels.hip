@@ -726,9 +726,13 @@ __global__ __launch_bounds__(256, MINW) void bell_screen_kernel(BellArgs A, int 
 // The body of one work item (tile of row i); block_id / nblocks are the launch coordinates.
 // PK > 1 (W = 1, variant bits 16-17): PK independent one-wave tiles share a workgroup (fewer
 // dispatches); each wave is its own item, `lw` its LDS slice, and no workgroup barrier runs.
-template <int NP, bool LAB, int R, int LB, int W, bool INS, int PK>
+// HY (bell_tree_hybrid_kernel, variant bit 26): a two-wave workgroup runs either two one-wave
+// tiles (PK = 2) or one heavy tile with both waves (W = 2, with the one-wave pipelines: the
+// launch keeps the W = 1 register budget); s_cand / s_pass are the kernel's LDS, shared by both.
+template <int NP, bool LAB, int R, int LB, int W, bool INS, int PK, bool HY = false>
 __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, int block_id,
-                                               int nblocks) {
+                                               int nblocks, double2 (*s_cand)[512],
+                                               unsigned long long* s_pass) {
     static_assert(PK == 1 || W == 1, "packed workgroups hold one-wave tiles");
     const int lane = threadIdx.x & 63;
     const int lw = readfirst(threadIdx.x >> 6);  // this wave's LDS slice
@@ -763,12 +767,12 @@ __device__ __forceinline__ void bell_tree_item(const BellArgs& A0, int ntile, in
     // states per tile: 64·R, or A.tw (< 64, R = 1: lanes tw..63 idle) — see bell_tile_width
     const int TW = (R == 1 && A0.tw > 0) ? A0.tw : 64 * R;
     const int jbase = tile * TW;
-    __shared__ double2 s_cand[W * PK][512];  // each wave's current superblock: (a_k, D_k)
-    __shared__ unsigned long long s_pass[W];  // (first superblock, bit 12) per-wave pass masks
+    // s_cand[W·PK][512]: each wave's current superblock (a_k, D_k); s_pass[W]: (first
+    // superblock, bit 12) per-wave pass masks
     // W >= 2 (cooperating waves): registers were budgeted for 5 waves per SIMD, so the staging
     // and fine-screen software pipelines (two register sets each) are off and the screen
     // stages four chains at a time; the best exchange reuses each wave's idle s_cand slice
-    constexpr bool LEAN = W >= 2 || LAB;  // (labour: keeps 3 waves per SIMD)
+    constexpr bool LEAN = (W >= 2 && !HY) || LAB;  // (labour: keeps 3 waves per SIMD)
 
     // loads that do not depend on the start-up below, issued first so that their latency
     // overlaps it: the level-0 bounds of the first 64 superblocks (first labour group) and v_old
@@ -1434,9 +1438,31 @@ template <int NP, bool LAB, int R, int LB, int W, bool INS, int PK>
 // cooperative tiles (W >= 2) serve small grids and labour, where a few hundred waves run and
 // latency, not occupancy, bounds them — a budget of 5 (and of 4) made those builds spill
 __global__ __launch_bounds__(64 * W * PK, 3) void bell_tree_kernel(BellArgs A0, int ntile) {
+    __shared__ double2 s_cand[W * PK][512];
+    __shared__ unsigned long long s_pass[W];
     const int lw = PK > 1 ? readfirst(threadIdx.x >> 6) : 0;
     bell_tree_item<NP, LAB, R, LB, W, INS, PK>(A0, ntile, (int)blockIdx.x * PK + lw,
-                                               (int)gridDim.x * PK);
+                                               (int)gridDim.x * PK, s_cand, s_pass);
+}
+
+// Heavy tiles on two waves (variant bit 26, A1 with a dispatch permutation): workgroup b holds
+// perm[2b], perm[2b + 1]; perm[2b + 1] == -2 marks a cooperative tile (both waves on perm[2b]),
+// otherwise the two slots are one-wave tiles as in the packed launch (PK = 2).  ws_tree_perm
+// picks the heaviest tiles of each XCD's range for the cooperative workgroups and deals them
+// first.  Work split only: the (max value, first index) merge makes the result identical.
+template <int NP, bool INS>
+__global__ __launch_bounds__(128, 3) void bell_tree_hybrid_kernel(BellArgs A0, int ntile) {
+    __shared__ double2 s_cand[2][512];
+    __shared__ unsigned long long s_pass[2];
+    const int b = (int)blockIdx.x;
+    if (A0.perm[2 * b + 1] == -2) {
+        bell_tree_item<NP, false, 1, 1, 2, INS, 1, true>(A0, ntile, 2 * b, 2 * (int)gridDim.x,
+                                                        s_cand, s_pass);
+    } else {
+        const int lw = readfirst(threadIdx.x >> 6);
+        bell_tree_item<NP, false, 1, 1, 1, INS, 2, true>(A0, ntile, 2 * b + lw,
+                                                        2 * (int)gridDim.x, s_cand, s_pass);
+    }
 }
 
 // ------------------------------------------------------------------------------ 4. merge
@@ -1694,6 +1720,17 @@ static void tree_w(const BellArgs& A, hipStream_t st) {
         case 3: tree_geo<NP, LAB, R, 8>(A, st); break;
         default:
             if constexpr (!LAB && R == 1) {
+                if (A.perm && bell_tree_hybrid(A)) {
+                    const int ntile = cdiv(A.Na, bell_tile_width(A, 1));
+                    const int grid = A.perm_slots / 2;
+                    if (A.trace || A.hitcount)
+                        launch_dispatch_timed(bell_tree_hybrid_kernel<NP, true>, dim3(grid),
+                                              dim3(128), 0, st, A, ntile);
+                    else
+                        launch_dispatch_timed(bell_tree_hybrid_kernel<NP, false>, dim3(grid),
+                                              dim3(128), 0, st, A, ntile);
+                    return;
+                }
                 switch (A.perm ? bell_tree_pack(A) : 1) {
                     case 2: tree_geo<NP, LAB, R, 1, 2>(A, st); return;
                     case 4: tree_geo<NP, LAB, R, 1, 4>(A, st); return;

@@ -272,13 +272,16 @@ static int bell_args(aiy_ws* ws, const BellCall& c, BellArgs& A, hipStream_t st)
         ws->perm_ok = false;
     }
     A.perm = nullptr;
+    A.perm_slots = 0;
     if (tree_perm_eligible(A)) {
-        const int key = A.tw * (1 << 18) + (A.variant & (64 | 2048 | (3 << 16)));
+        const long long key = (long long)A.tw * (1ll << 31) +
+                              (A.variant & (64 | 2048 | (3 << 16) | (15 << 26)));
         if (!ws->perm_ok || ws->perm_key != key) {
             AIY_TRY(ws_tree_perm(ws, A, st));
             ws->perm_key = key;
         }
         A.perm = ws->tree_perm;
+        A.perm_slots = ws->perm_slots;
     }
     return AIY_OK;
 }
@@ -294,6 +297,8 @@ bool tree_perm_eligible(const BellArgs& A) {
            (A.variant & (1 | 2 | 4 | 8)) == 0;
 }
 constexpr int kSimdsPerXcd = 128;  // MI355X: 32 CUs x 4 SIMDs per XCD
+static int ws_tree_perm_hybrid(aiy_ws* ws, const BellArgs& A, const std::vector<int>& kl,
+                               int ntile, hipStream_t st);
 int ws_tree_perm(aiy_ws* ws, const BellArgs& A, hipStream_t st) {
     const int N = A.N, Na = A.Na, TW = bell_tile_width(A, 1), ntile = (Na + TW - 1) / TW;
     const int G = N * ntile;
@@ -314,6 +319,7 @@ int ws_tree_perm(aiy_ws* ws, const BellArgs& A, hipStream_t st) {
     AIY_HIP(hipMemcpyAsync(kl.data(), ws->kf_last, kl.size() * sizeof(int),
                            hipMemcpyDeviceToHost, st));
     AIY_HIP(hipStreamSynchronize(st));
+    if (bell_tree_hybrid(A)) return ws_tree_perm_hybrid(ws, A, kl, ntile, st);
     std::vector<int> perm(slots, -1);
     int start = 0;
     for (int x = 0; x < 8; ++x) {
@@ -356,6 +362,79 @@ int ws_tree_perm(aiy_ws* ws, const BellArgs& A, hipStream_t st) {
                            hipMemcpyHostToDevice, st));
     AIY_HIP(hipStreamSynchronize(st));
     ws->perm_ok = true;
+    ws->perm_slots = slots;
+    return AIY_OK;
+}
+
+// The hybrid launch's order (variant bit 26): each XCD keeps its contiguous row-major range as
+// above; its H heaviest tiles (bits 27-29) become cooperative workgroups (slots {item, -2}),
+// dealt first, heaviest first; the rest are packed two per workgroup in row-major order with
+// the range's cheapest tiles last (the third waves on a SIMD).  Workgroup b runs on XCD b mod 8.
+static int ws_tree_perm_hybrid(aiy_ws* ws, const BellArgs& A, const std::vector<int>& kl,
+                               int ntile, hipStream_t st) {
+    const int N = A.N, G = N * ntile;
+    auto cost = [&](int it) {
+        const int i = it / ntile, t = it % ntile;
+        long long c = 0;
+        for (int l = 0; l < A.Nl; ++l) c += kl[((size_t)l * N + i) * ntile + t];
+        return c;
+    };
+    // split the items into 8 contiguous ranges, then each range into workgroups
+    std::vector<std::vector<int>> wg[8];  // per XCD: its workgroups' slot pairs, in order
+    int start = 0;
+    for (int x = 0; x < 8; ++x) {
+        const int size = G / 8 + (x < G % 8 ? 1 : 0);
+        std::vector<int> items(size);
+        for (int u = 0; u < size; ++u) items[u] = start + u;
+        start += size;
+        std::vector<int> by(items);
+        std::stable_sort(by.begin(), by.end(), [&](int a, int b) { return cost(a) > cost(b); });
+        const int H = std::min(size, bell_tree_coop_per_xcd(A));
+        std::vector<char> coop(G, 0);
+        for (int u = 0; u < H; ++u) {
+            coop[by[u]] = 1;
+            wg[x].push_back({by[u], -2});
+        }
+        std::vector<int> rest;
+        for (int it : items)
+            if (!coop[it]) rest.push_back(it);
+        // the cheapest (size - H) - 2·128 one-wave tiles last, cheapest at the very end
+        const int R = (int)rest.size();
+        const int tail = std::max(0, R - 2 * kSimdsPerXcd);
+        std::vector<int> rb(rest);
+        std::stable_sort(rb.begin(), rb.end(), [&](int a, int b) { return cost(a) < cost(b); });
+        std::vector<char> last(G, 0);
+        for (int u = 0; u < tail; ++u) last[rb[u]] = 1;
+        std::vector<int> out;
+        for (int it : rest)
+            if (!last[it]) out.push_back(it);
+        for (int u = tail - 1; u >= 0; --u) out.push_back(rb[u]);
+        for (size_t u = 0; u < out.size(); u += 2)
+            wg[x].push_back({out[u], u + 1 < out.size() ? out[u + 1] : -1});
+    }
+    // interleave: workgroup b = 8q + x is XCD x's q-th; XCDs with fewer workgroups get empty
+    // ({-1, -1}) ones so that b mod 8 still names the XCD
+    size_t nq = 0;
+    for (int x = 0; x < 8; ++x) nq = std::max(nq, wg[x].size());
+    const int slots = (int)(8 * nq * 2);
+    std::vector<int> perm(slots, -1);
+    for (size_t q = 0; q < nq; ++q)
+        for (int x = 0; x < 8; ++x)
+            if (q < wg[x].size()) {
+                perm[(8 * q + x) * 2] = wg[x][q][0];
+                perm[(8 * q + x) * 2 + 1] = wg[x][q][1];
+            }
+    if (!ws->tree_perm || ws->perm_cap < slots) {
+        if (ws->tree_perm) (void)hipFree(ws->tree_perm);
+        ws->tree_perm = nullptr;
+        AIY_HIP(hipMalloc((void**)&ws->tree_perm, (size_t)slots * sizeof(int)));
+        ws->perm_cap = slots;
+    }
+    AIY_HIP(hipMemcpyAsync(ws->tree_perm, perm.data(), (size_t)slots * sizeof(int),
+                           hipMemcpyHostToDevice, st));
+    AIY_HIP(hipStreamSynchronize(st));
+    ws->perm_ok = true;
+    ws->perm_slots = slots;
     return AIY_OK;
 }
 
@@ -909,7 +988,7 @@ int aiy_ws_invalidate(aiy_ws* ws) {
 
 int aiy_ws_set_variant(aiy_ws* ws, int variant) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
-    if (variant < -1 || variant >= (1 << 26)) return fail(AIY_BAD_ARG, "variant in [-1, 2^26)");
+    if (variant < -1 || variant >= (1 << 30)) return fail(AIY_BAD_ARG, "variant in [-1, 2^30)");
     ws->variant = variant;
     return AIY_OK;
 }

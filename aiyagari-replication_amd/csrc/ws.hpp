@@ -38,7 +38,8 @@ struct aiy_ws {
     int64_t kf_Nl = 0;
     bool kf_lab = false;
     int* tree_perm = nullptr;  // tree dispatch order for the cached kf (ws_tree_perm)
-    int perm_cap = 0, perm_key = 0;
+    int perm_cap = 0, perm_slots = 0;
+    long long perm_key = 0;
     int* kf_last = nullptr;    // [Nl][N][ntile] kf of each tile's last state (ws_tree_perm)
     int kf_last_cap = 0;
     // disutility per labour level, cached with the key below (aiy_ws_invalidate resets)

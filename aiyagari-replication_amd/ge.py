@@ -184,7 +184,7 @@ def aiyagari_labor_egm(Na=400, T=10000, tol=1e-5, max_iter=1000, supply="mc", ph
 
 
 def aiyagari_vfi_overlapped(Na=400, rho=0.75, sigma_e=0.75, shocks="tauchen", T=10000, tol=1e-5,
-                            max_iter=1000, r0=0.04, max_r_iter=10, r_tol=1e-5, lookahead=1):
+                            max_iter=1000, r0=0.04, max_r_iter=10, r_tol=1e-5, lookahead=2):
     """Aiyagari_VFI.m's computation (as `aiyagari_vfi`, supply = MC) with the bisection run
     speculatively ahead of its serial Monte-Carlo chains.  Step j needs K_s(r_j) only to pick
     the next midpoint, and both candidates warm-start from the same v_old(r_j): so every solve
@@ -193,11 +193,12 @@ def aiyagari_vfi_overlapped(Na=400, rho=0.75, sigma_e=0.75, shocks="tauchen", T=
     chain (each on its own stream and workspace, one host thread per call; ctypes drops the
     GIL); a chain's K_s selects one subtree and the other is discarded.  Every solve and chain
     is the one the sequential loop runs, on the same inputs and uniform block, so r_history /
-    k_supply / iters are identical (tests/test_ge_gpu.py).  Default lookahead = 1 (the chain
-    of step j beside both solves of step j+1): with the two-wave chain (~1.6 ms per 10^4 steps)
-    and a warm small-grid solve (~1.5 ms) about equal, one level keeps the critical path at one
-    of them per step, and deeper trees run 4+ solves at once, which this runtime serves slower
-    than 2 (tools/ge_concurrency.py, profiles/r05_g32_ge_lookahead.txt)."""
+    k_supply / iters are identical (tests/test_ge_gpu.py).  Default lookahead = 2: with the
+    speculative-segment chain (~0.66 ms per 10^4 steps) shorter than a warm small-grid solve
+    (~0.7-1.5 ms), the second level keeps the next solves running while the chosen solve's
+    chain runs (16.4-17.5 vs 16.9-19.7 ms, profiles/r06_g20_ge_lookahead.txt); deeper trees
+    keep more than ~4 streams busy, which this runtime serves slower (profiles/
+    r06_g14_hw_queues.txt; round 5, with 1.6 ms chains, lookahead 1 won: r05_g32)."""
     import concurrent.futures as cf
 
     import torch

@@ -33,7 +33,7 @@ sys.path.insert(0, str(ROOT))
 # a solve queued behind a 1.6 ms chain waits for it (tools/ge_concurrency.py, profiles/
 # r06_g14_hw_queues.txt: 2 solves + 2 chains 3.2 ms at 4 queues, 2.9 at 16; 4 solves 2.7 vs
 # 1.8 ms).  More than ~4 busy queues degrade instead (6 solves: 5.9 ms at 16 queues, 3.1 at 4 —
-# the driver stays at lookahead 1).  Raised (never lowered) by bench.py's main only, before the
+# the driver's lookahead 2 keeps 4 solves + 1 chain).  Raised (never lowered) by bench.py's main only, before the
 # HIP runtime starts; the GE leg reports the wall at the inherited value too.
 HW_QUEUES_INHERITED = os.environ.get("GPU_MAX_HW_QUEUES")  # recorded in ge_equilibrium
 

@@ -274,7 +274,7 @@ int aiy_ws_set_cu_exclusive(aiy_ws* ws, int on);
  * it applies.  Results (K_s, the paths, find() errors) are identical for every mode. */
 int aiy_ws_set_sim(aiy_ws* ws, int mode);
 /* kernel shapes and A/B knobs (tuning only; results are identical for every value in
- * [-1, 2^26)).  VFI, bit 3 clear (default): the bound tree screen, bit 0 = 2 states per lane
+ * [-1, 2^30)).  VFI, bit 3 clear (default): the bound tree screen, bit 0 = 2 states per lane
  * (else 1), bits 1-2 = 1, 2, 4 or 8 cooperating waves per tile, bit 4 = XCD-aware tile order,
  * bit 6 / bit 11 = one-wave tiles dispatched from a per-workspace permutation that keeps each
  * XCD's tile range and deals it heaviest first / row-major with its cheapest tiles last, bit 13 =
@@ -293,7 +293,10 @@ int aiy_ws_set_sim(aiy_ws* ws, int mode);
  * variant never changes the EGM path): bit 18 = two launches per step even when Na <= 1024
  * (default there: one fused launch); bit 19 = no chaining in the solve loops (two launches per
  * step); bit 20 = no interp1 segment windows.  Bit 25: the small-grid one-launch sweep
- * (aiy_ws_set_wide) even with an explicit variant.  -1 (default): chosen by size — Na <= 4096:
+ * (aiy_ws_set_wide) even with an explicit variant.  Bit 26 (with bit 6 or 11, A1 at sigma = 5):
+ * the hybrid tree launch — two-wave workgroups that run two one-wave tiles, or one of each XCD
+ * range's heaviest tiles on both waves; bits 27-29: those cooperative tiles per XCD range,
+ * 8 << value.  -1 (default): chosen by size — Na <= 4096:
  * 2 cooperating waves per tile (A1), 4 with bit 12 (labour); else 16 | 2048 | 1 << 16 |
  * 1 << 21 | 1 << 23 | 1 << 24 (A1), 16 | 1 << 21 (labour) and 16 | 1 << 21 (the batched
  * multi-rate solve). */

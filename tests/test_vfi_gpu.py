@@ -173,17 +173,22 @@ def test_screen_stress_noisy_value(pkg, gpu, variant):
             assert np.array_equal(pks, pko) and np.array_equal(pcs, pco)
 
 
+_HY = 16 | 2048 | 1 << 16 | 1 << 21 | 1 << 23 | 1 << 24 | 1 << 26  # the hybrid tree launch
+
+
 @pytest.mark.parametrize("variant", [16, 80, 2064, 8208, 8272, 10256, 2064 | 1 << 16,
                                      2064 | 2 << 16, 2064 | 3 << 16, 80 | 2 << 16,
                                      10256 | 2 << 16, 16 | 2048 | 1 << 16 | 1 << 21,
                                      16 | 2048 | 1 << 16 | 1 << 21 | 1 << 23,
-                                     16 | 2048 | 1 << 16 | 1 << 21 | 3 << 23])
+                                     16 | 2048 | 1 << 16 | 1 << 21 | 3 << 23,
+                                     _HY, _HY | 2 << 27, _HY | 5 << 27])
 def test_full_size_dispatch_orders_and_tile_widths(pkg, gpu, variant):
     """Na = 20,000 (configs[1]): the tree's dispatch orders (bit 6: each XCD's range heaviest
     first; bit 11: its cheapest tiles last), the narrow one-wave tiles (bit 13: 46 states per
     tile, three tiles per SIMD) and packed workgroups (bits 16-17: 2, 4 or 8 one-wave tiles per
-    workgroup) change only the work split — a hinted warm sweep is bit-exact against the C
-    oracle for each."""
+    workgroup), and the hybrid launch (bit 26: the 8, 32 or 256 heaviest tiles of each XCD range
+    on two cooperating waves, the rest packed two per workgroup) change only the work split — a
+    hinted warm sweep is bit-exact against the C oracle for each."""
     import torch
     cal = no.calib_aiyagari(Na=20000, shocks="rouwenhorst")
     a, s, P = cal["a_grid"], cal["s"], cal["P"]
@@ -201,7 +206,9 @@ def test_full_size_dispatch_orders_and_tile_widths(pkg, gpu, variant):
 
 
 @pytest.mark.parametrize("Na,variant", [(1100, 2048 | 2 << 16), (1100, 64 | 3 << 16),
-                                        (333, 2048 | 1 << 16), (4100, 8192 | 2048 | 2 << 16)])
+                                        (333, 2048 | 1 << 16), (4100, 8192 | 2048 | 2 << 16),
+                                        (333, 2048 | 1 << 26 | 1 << 27), (1100, 2048 | 1 << 26),
+                                        (4100, 8192 | 2048 | 1 << 26 | 2 << 27)])
 def test_packed_workgroups_ragged(pkg, gpu, Na, variant):
     """Packed workgroups whose last one is partly empty (7 rows x 18 tiles = 126 one-wave
     items in 4-wave workgroups: 2 unused slots; 7 x 6 = 42 in 2-wave ones at Na = 333; the

@@ -18,16 +18,17 @@ def main():
     pkg = bench.load_pkg()
     import torch
     torch.cuda.set_device(0)
-    pkg.ge.aiyagari_vfi_overlapped(max_iter=5)
-    pkg.ge.aiyagari_vfi_overlapped(max_iter=5)
+    kw = {"lookahead": int(sys.argv[1])} if len(sys.argv) > 1 else {}  # (A/B: default otherwise)
+    pkg.ge.aiyagari_vfi_overlapped(max_iter=5, **kw)
+    pkg.ge.aiyagari_vfi_overlapped(max_iter=5, **kw)
     walls, out = [], None
     for _ in range(5):
         t0 = time.perf_counter()
-        out = pkg.ge.aiyagari_vfi_overlapped()
+        out = pkg.ge.aiyagari_vfi_overlapped(**kw)
         walls.append(time.perf_counter() - t0)
     print(json.dumps({"hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "runtime default"),
                       "wall_s_gpu": sorted(walls)[2], "wall_s_gpu_runs": walls,
-                      "r": out["r"]}), flush=True)
+                      "lookahead": out["lookahead"], "r": out["r"]}), flush=True)
 
 
 if __name__ == "__main__":
