@@ -182,7 +182,7 @@ def _json_profile(name):
     return json.loads(f.read_text()) if f.exists() else None
 
 
-PMC_ROUNDS = ("r05", "r04", "r03")  # newest first: counter passes of the kernels at HEAD
+PMC_ROUNDS = ("r06", "r05", "r04", "r03")  # newest first: counter passes of the kernels at HEAD
 
 
 def _counters(name, traffic_name=None):
@@ -398,7 +398,7 @@ def main():
         # result is bit-identical to -- the rate an exhaustive kernel would need to match it
         effective = FLOPS_PER_CANDIDATE * evals_per_sweep / (kern_avg_ms * 1e-3) / 1e12
         # PMC / HBM-traffic passes over the same sweeps 6..25 on the current kernels
-        # (tools/exp/r05_pmc.sh: tools/pmc.sh + pmc_summary / pmc_traffic, skip 5 take 20)
+        # (tools/exp/r06_pmc.sh: tools/pmc.sh + pmc_summary / pmc_traffic, skip 5 take 20)
         pmc_d, traffic, pmc_src = _counters("tree", "vfi_tree")
         step_ms = sorted(blocks)
         out = {
@@ -478,7 +478,7 @@ def main():
             out["dist"] = BL.dist_leg(pkg, dev, cpu_threads=threads)
             progress("dist done")
             # counter passes of the kernels these legs time (tools/pmc_workloads_r05.py under
-            # tools/pmc.sh, one workload per pass set: tools/exp/r05_pmc.sh)
+            # tools/pmc.sh, one workload per pass set: tools/exp/r06_pmc.sh)
             def attach(leg, name, kernel):
                 pmc_d, tf, src = _counters(name)
                 leg["roofline"].update(pmc={kernel: pmc_d}, traffic=tf, pmc_source=src)

@@ -101,7 +101,7 @@ def ks_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, exchange="halo", r
             "value": nodes * howard / th, "unit": "evals/s", "n_gpus": world,
             "roofline": {"bound": "valu", "achieved": tfs, "peak": 78.6, "unit": "TFLOP/s",
                          "frac": tfs / 78.6,
-                         "traffic": (pmc or {}).get("ks_howard_slopes_kernel", {}).get(
+                         "traffic": next(iter((pmc or {None: {}}).values())).get(
                              "hbm_bytes_per_launch"),
                          "basis": f"{fpn} fp64 flops per node per Howard sweep (4 pchip "
                                   f"evaluations 66, expectation 8, budget 3, aiy_log 28, "
@@ -223,11 +223,12 @@ def ks_direct_leg(pkg, world, rank, dev, nk=32768, nK=64, howard=50, reps=3, che
 
 
 def _ks_pmc():
-    """Counter summary of the kernel this leg times — ks_howard_slopes_kernel, one launch per
-    Howard sweep at k = 32,768, K = 64 (rocprofv3 --pmc passes over tools/pmc_workloads_r05.py
-    ks, tools/exp/r05_pmc.sh) — from the newest round's files committed under profiles/."""
-    name = "ks_howard_slopes_kernel"
-    for rnd in ("r05", "r04"):
+    """Counter summary of the kernel this leg times — one launch per Howard sweep at k = 32,768,
+    K = 64 (rocprofv3 --pmc passes over tools/pmc_workloads_r05.py ks, tools/exp/r06_pmc.sh):
+    ks_howard_slopes_xcd_kernel from round 6, ks_howard_slopes_kernel before — from the newest
+    round's files committed under profiles/."""
+    for rnd in ("r06", "r05", "r04"):
+        name = "ks_howard_slopes_xcd_kernel" if rnd >= "r06" else "ks_howard_slopes_kernel"
         p = ROOT / "profiles" / f"{rnd}_pmc_ks_howard_slopes.json"
         q = ROOT / "profiles" / f"{rnd}_traffic_ks_howard_slopes.json"
         if not p.exists():

@@ -14,6 +14,9 @@ launches of the kernel it is about (VERDICT r4 "do this" 1):
   egm       egm_chain_kernel  — A4 then A5 solve loops at Na = 20,000, 200 chained steps each:
                                 take 200 / skip 200 take 200
   dist      dist_push_kernel  — 64 pushes on the r = 0.04 policy at Na = 20,000 (bench `dist`)
+  sim       sim_chain_par_kernel — (round 6) 20 capital-supply chains of T = 10,000 on the
+                                Na = 400 policy at r = 0.04 (the GE loop's chain), K_s only
+(round 6: the same workloads, tools/exp/r06_pmc.sh; `ks` now times ks_howard_slopes_xcd_kernel)
 """
 import sys
 from pathlib import Path
@@ -111,6 +114,21 @@ elif which == "dist":
     out = torch.empty_like(lam0)
     pkg.dist_stationary_dev(pkg.Workspace(N, Na), lam0, a_t, P_t, out, policy_idx=idx, tol=0.0,
                             max_iter=64)
+elif which == "sim":
+    cal, w, a_t, s_t, P_t = a1_setup(400)
+    N, Na = cal["N"], 400
+    vws = pkg.Workspace(N, Na)
+    va = torch.zeros((N, Na), dtype=torch.float64, device=dev)
+    vb = torch.zeros_like(va)
+    idx = torch.zeros((N, Na), dtype=torch.int32, device=dev)
+    pk = torch.zeros_like(va)
+    vws.vfi_solve(va, vb, a_t, s_t, P_t, r, w, cal["beta"], cal["sigma"], 1e-5, 1000, idx,
+                  policy_k=pk)
+    U = t(np.random.default_rng(0).random(9999))
+    ks = torch.zeros(1, dtype=torch.float64, device=dev)
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    for _ in range(20):
+        pkg.sim_capital_dev(vws, pk, a_t, P_t, 3, float(cal["a_grid"][200]), U, ks, st)
 else:
     raise SystemExit(f"unknown workload {which!r}")
 torch.cuda.synchronize()
