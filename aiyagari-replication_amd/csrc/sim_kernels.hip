@@ -530,6 +530,11 @@ __global__ __launch_bounds__(128) void sim_chain_pipe_kernel(SimArgs A0) {
 //   S. wave 0 sums the path in order (the serial kernel's fp64 accumulation, bit for bit).
 // The path, hence K_s, is the serial chain's bit for bit whatever the guesses: every stored
 // value is either computed from the true predecessor or equal to such a value.
+// (timing probes, results wrong: AIY_PAR_PROBE 1 = no in-order sum, 2 = no repair passes,
+// 3 = neither and no segment phase; built only into experiment libraries, never the default)
+#ifndef AIY_PAR_PROBE
+#define AIY_PAR_PROBE 0
+#endif
 constexpr int kParWaves = 16;
 constexpr int kParMaxT = 16384;  // z_t in LDS (one byte each)
 
@@ -706,7 +711,7 @@ __global__ __launch_bounds__(1024) void sim_chain_par_kernel(SimArgs A0) {
     const int L = (Te - 1 + kParWaves - 1) / kParWaves;  // >= 0
     const int Ts = 1 + wave * L, Tn = min(Te, Ts + L);
     ParStepper<SS> ps{X0, H, Y, Na, Na - 64, lane, 0, false, 0.0, 0.0, 0.0, 0.0};
-    if (Ts < Tn) {
+    if (Ts < Tn && AIY_PAR_PROBE != 3) {
         double k = A.k1;
         for (int t = Ts; t < Tn; ++t) {
             k = ps.step(k, zo_of(t), zo_of(t + 1));
@@ -715,7 +720,7 @@ __global__ __launch_bounds__(1024) void sim_chain_par_kernel(SimArgs A0) {
     }
     if (tid == 0) kp[0] = A.k1;
     if (lane == 0) {
-        s_res[wave] = wave == 0 ? 1 : (Ts < Tn ? 0 : 1);  // (empty segments are trivially true)
+        s_res[wave] = wave == 0 || AIY_PAR_PROBE >= 2 ? 1 : (Ts < Tn ? 0 : 1);  // (empty: true)
         s_chg[wave] = 0;
     }
     __syncthreads();
@@ -733,10 +738,21 @@ __global__ __launch_bounds__(1024) void sim_chain_par_kernel(SimArgs A0) {
         int chg = 0;
         if (mine) {
             ps.primed = false;
+            // the stored values in chunks of 64 (one per lane, the next chunk in flight), read
+            // back with v_readlane: no dependent global load per step
+            int cb = Ts;
+            double sv = Ts + lane < Tn ? kp[Ts + lane] : 0.0;
+            double sn = Ts + 64 + lane < Tn ? kp[Ts + 64 + lane] : 0.0;
             for (int t = Ts; t < Tn; ++t) {
+                if (t - cb == 64) {
+                    cb = t;
+                    sv = sn;
+                    sn = cb + 64 + lane < Tn ? kp[cb + 64 + lane] : 0.0;
+                }
                 k = ps.step(k, zo_of(t), zo_of(t + 1));
                 const unsigned long long kb = __builtin_bit_cast(unsigned long long, k);
-                const unsigned long long sb = __builtin_bit_cast(unsigned long long, kp[t]);
+                const unsigned long long sb =
+                    __builtin_bit_cast(unsigned long long, readlane_d(sv, t - cb));
                 if (kb == sb) break;  // the stored path is the true one from here
                 if (lane == 0) kp[t] = k;
                 if (t == Tn - 1) chg = 1;
@@ -757,7 +773,7 @@ __global__ __launch_bounds__(1024) void sim_chain_par_kernel(SimArgs A0) {
         __syncthreads();
     }
     // S. the mean (sequential fp64 sum, k_0 .. k_{Te-1}) and the outputs
-    if (wave == 0) {
+    if (wave == 0 && (AIY_PAR_PROBE == 0 || AIY_PAR_PROBE == 2)) {
         double v = lane < Te ? kp[lane] : 0.0;
         double sum = readlane_d(v, 0);  // sum = k_1 (the serial kernel's start), then in order
         for (int c0 = 0; c0 < Te; c0 += 64) {
