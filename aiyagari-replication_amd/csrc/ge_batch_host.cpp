@@ -69,8 +69,8 @@ static int ge_share(GeShare& sh, const double* r, const double* v_rows, const do
     S.out = dout; S.status = dst;
     S.C = (int)C; S.pcs = n; S.ucs = (size_t)std::max<int64_t>(T - 1, 0);
     S.par = c->ws->sim_par;
-    if (S.par != 0)  // the speculative-segment chains' path scratch, T doubles per candidate
-        AIY_TRY(c->buf("ge_kscr", sizeof(double) * (size_t)T * C, (void**)&S.kscr));
+    if (S.par != 0)  // the speculative-segment chains' scratch (paths, state paths, flags)
+        AIY_TRY(c->buf("ge_kscr", sim_par_scratch_bytes(T, C), (void**)&S.kscr));
     AIY_TRY(launch_sim_capital(S, c->st));
     std::vector<int> status(C);
     AIY_HIP(hipMemcpyAsync(k_supply + sh.c0, dout, sizeof(double) * C, hipMemcpyDeviceToHost, c->st));

@@ -25,10 +25,17 @@ struct SimArgs {
     // shares the chain's CU — opt-in (aiy_ws_set_cu_exclusive on the chain's workspace; the GE
     // driver sets it), ADVICE r5
     bool exclusive;
-    // the speculative-segment chain (sim_chain_par_kernel): the k path's scratch, T doubles per
-    // chain (null: the serial kernels); par: -1 by size, 0 never, 1 whenever it applies
+    // the speculative-segment chain (sim_kernels.hip): its scratch, sim_par_scratch_bytes(T, C)
+    // (null: the serial kernels); par: -1 by size, 0 never, 1 whenever it applies (one
+    // workgroup per chain), 2 whenever it applies (the spread four-launch variant)
     double* kscr;
     int par;
 };
+// the speculative chain's scratch: the k paths (T doubles per chain), the state paths (T bytes
+// per chain) and per chain {Te, 16 repair flags} (ints)
+inline size_t sim_par_scratch_bytes(long long T, long long C) {
+    if (C < 1) C = 1;
+    return (size_t)(8 * T * C) + (((size_t)(T * C) + 7) & ~(size_t)7) + (size_t)(4 * 17 * C);
+}
 int launch_sim_capital(const SimArgs& A, hipStream_t st);
 }  // namespace aiy

@@ -64,7 +64,7 @@ int aiy_sim_capital(const double* policy_k, int vfi_layout, const double* a_grid
     // MATLAB layouts: VFI policy_k is N x Na (z stride 1, a stride N); EGM is Na x N.
     size_t zs = vfi_layout ? 1 : (size_t)Na, as = vfi_layout ? (size_t)N : 1;
     double* dks = nullptr;  // the speculative-segment chain's path scratch
-    AIY_TRY(c->buf("sim_kscr", sizeof(double) * T, (void**)&dks));
+    AIY_TRY(c->buf("sim_kscr", sim_par_scratch_bytes(T, 1), (void**)&dks));
     AIY_TRY(sim_capital_dev(dpol, zs, as, da, dP, N, Na, z1 - 1, k1, T, dU, dout, dk, dz, dst,
                             c->st, false, dks, c->ws ? c->ws->sim_par : -1));
     double out;
@@ -93,12 +93,13 @@ int aiy_sim_capital_dev(aiy_ws* ws, const double* policy_rows, const double* a_g
                         const double* uniforms, double* k_supply, double* sim_k,
                         int32_t* sim_z, int32_t* status, void* stream) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
-    if (T >= 2 && ws->sim_par != 0 && ws->sim_kcap < (size_t)T) {  // path scratch (per workspace)
+    const size_t kb = sim_par_scratch_bytes(T, 1);
+    if (T >= 2 && ws->sim_par != 0 && ws->sim_kcap < kb) {  // the chain's scratch (per workspace)
         if (ws->sim_kbuf) AIY_HIP(hipFree(ws->sim_kbuf));
         ws->sim_kbuf = nullptr;
         ws->sim_kcap = 0;
-        AIY_HIP(hipMalloc((void**)&ws->sim_kbuf, sizeof(double) * (size_t)T));
-        ws->sim_kcap = (size_t)T;
+        AIY_HIP(hipMalloc((void**)&ws->sim_kbuf, kb));
+        ws->sim_kcap = kb;
     }
     return sim_capital_dev(policy_rows, (size_t)ws->Na, 1, a_grid, P, ws->N, ws->Na, z1, k1, T,
                            uniforms, k_supply, sim_k, sim_z, status, (hipStream_t)stream,
@@ -108,7 +109,7 @@ int aiy_sim_capital_dev(aiy_ws* ws, const double* policy_rows, const double* a_g
 
 int aiy_ws_set_sim(aiy_ws* ws, int mode) {
     if (!ws) return fail(AIY_BAD_ARG, "NULL workspace");
-    if (mode < -1 || mode > 1) return fail(AIY_BAD_ARG, "mode: -1 (by size), 0 or 1");
+    if (mode < -1 || mode > 2) return fail(AIY_BAD_ARG, "mode: -1 (by size), 0, 1 or 2");
     ws->sim_par = mode;
     return AIY_OK;
 }

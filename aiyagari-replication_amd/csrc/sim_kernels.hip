@@ -611,36 +611,19 @@ __device__ __forceinline__ unsigned zmap_compose(unsigned A, unsigned B) {  // A
     return R;
 }
 
-template <int SS, bool PATH>
-__global__ __launch_bounds__(1024) void sim_chain_par_kernel(SimArgs A0) {
-    SimArgs A = A0;
-    double* kp = A0.kscr;
-    if (A0.C > 1) {
-        A.pol += blockIdx.x * A0.pcs;
-        A.U += blockIdx.x * A0.ucs;
-        A.out += blockIdx.x;
-        A.status += blockIdx.x;
-        kp += (size_t)blockIdx.x * A0.T;
-    }
-    if (PATH && A.sim_k) kp = A.sim_k;  // the path is the output itself
-    extern __shared__ double lds[];  // X0[SS] | H[SS] | Y[N][SS][2] = {y_i, y_{i+1} - y_i}
-    __shared__ unsigned char zp[kParMaxT];
-    __shared__ unsigned s_map[1024];
-    __shared__ double s_cs[64];
-    __shared__ int s_stop, s_go;
-    __shared__ int s_res[kParWaves], s_chg[kParWaves];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int N = A.N, Na = A.Na, T = A.T;
+// the chain's LDS tables (X0[SS] | H[SS] | Y[N][SS][2] = {y_i, y_{i+1} - y_i}), by nthr threads
+template <int SS>
+__device__ __forceinline__ void par_tables(const SimArgs& A, double* lds, int tid, int nthr) {
     double* X0 = lds;
     double* H = lds + SS;
     double* Y = lds + 2 * SS;
-    for (int i = tid; i < SS; i += 1024) {
+    const int Na = A.Na;
+    for (int i = tid; i < SS; i += nthr) {
         const double x0 = A.a[min(i, Na - 1)], x1 = A.a[min(i + 1, Na - 1)];
         X0[i] = x0;
         H[i] = x1 - x0;
     }
-    for (int q = tid; q < N * SS; q += 1024) {
+    for (int q = tid; q < A.N * SS; q += nthr) {
         const int zz = q / SS, i = q - zz * SS;
         const double* row = A.pol + (size_t)zz * A.zs;
         const double y0 = i < Na ? row[(size_t)i * A.as] : 0.0;
@@ -648,6 +631,13 @@ __global__ __launch_bounds__(1024) void sim_chain_par_kernel(SimArgs A0) {
         Y[2 * (size_t)q] = y0;
         Y[2 * (size_t)q + 1] = y1 - y0;
     }
+}
+
+// Z: the state path of one chain by 1,024 threads into zp[0 .. T) (LDS); returns the stop index
+// Te (steps 1 .. Te-1 run; Te < T: find() empty at step Te).  Ends with a barrier.
+__device__ __forceinline__ int par_zpath(const SimArgs& A, unsigned char* zp, unsigned* s_map,
+                                         double* s_cs, int* s_stop) {
+    const int tid = threadIdx.x, N = A.N, T = A.T;
     if (tid < 64) {  // cumsum(P(z,:))(m) in order (as cumsum), lanes 8z + m
         const int zz = tid >> 3, m = tid & 7;
         double acc = 0.0;
@@ -655,12 +645,10 @@ __global__ __launch_bounds__(1024) void sim_chain_par_kernel(SimArgs A0) {
             for (int q = 0; q <= m; ++q) acc = acc + A.P[zz * N + q];
         s_cs[tid] = acc;
     }
-    if (tid == 0) s_stop = T;
+    if (tid == 0) *s_stop = T;
     __syncthreads();
-
-    // Z. the state path
-    const int nst = T - 1;                             // steps 1 .. T-1 use u[t - 1]
-    const int ch = (nst + 1023) / 1024;                // steps per thread
+    const int nst = T - 1;               // steps 1 .. T-1 use u[t - 1]
+    const int ch = (nst + 1023) / 1024;  // steps per thread
     const int t0 = 1 + tid * ch, t1 = min(T, t0 + ch);
     auto zmap = [&](int t) __attribute__((always_inline)) -> unsigned {
         const double u = A.U[t - 1];
@@ -688,91 +676,108 @@ __global__ __launch_bounds__(1024) void sim_chain_par_kernel(SimArgs A0) {
         if (tid >= off) s_map[tid] = zmap_compose(prev, s_map[tid]);
         __syncthreads();
     }
-    {
-        const unsigned pre = tid > 0 ? s_map[tid - 1] : ident;
-        int z = (int)((pre >> (3 * A.z1)) & 7u);
-        int first_bad = T;
-        for (int t = t0; t < t1; ++t) {
-            z = (int)((zmap(t) >> (3 * z)) & 7u);
-            zp[t] = (unsigned char)z;
-            if (z == 7 && first_bad == T) first_bad = t;
-        }
-        if (first_bad < T) atomicMin(&s_stop, first_bad);
-        if (tid == 0) zp[0] = (unsigned char)A.z1;
+    const unsigned pre = tid > 0 ? s_map[tid - 1] : ident;
+    int z = (int)((pre >> (3 * A.z1)) & 7u);
+    int first_bad = T;
+    for (int t = t0; t < t1; ++t) {
+        z = (int)((zmap(t) >> (3 * z)) & 7u);
+        zp[t] = (unsigned char)z;
+        if (z == 7 && first_bad == T) first_bad = t;
     }
+    if (first_bad < T) atomicMin(s_stop, first_bad);
+    if (tid == 0) zp[0] = (unsigned char)A.z1;
     __syncthreads();
-    const int Te = s_stop;  // steps 1 .. Te-1 run (Te < T: find() empty at step Te)
-    const int zrow = SS * 16;
-    auto zo_of = [&](int t) __attribute__((always_inline)) {
-        return t < Te ? (int)zp[t] * zrow : 0;
-    };
+    return *s_stop;
+}
 
-    // K. segments, then repairs
-    const int L = (Te - 1 + kParWaves - 1) / kParWaves;  // >= 0
-    const int Ts = 1 + wave * L, Tn = min(Te, Ts + L);
-    ParStepper<SS> ps{X0, H, Y, Na, Na - 64, lane, 0, false, 0.0, 0.0, 0.0, 0.0};
-    if (Ts < Tn && AIY_PAR_PROBE != 3) {
-        double k = A.k1;
-        for (int t = Ts; t < Tn; ++t) {
-            k = ps.step(k, zo_of(t), zo_of(t + 1));
-            if (lane == 0) kp[t] = k;
+// one wave: segment [Ts, Tn) of the k recurrence from k, stored (lane 0) into kp
+template <int SS, class ZO>
+__device__ __forceinline__ void par_segment(ParStepper<SS>& ps, double k, int Ts, int Tn,
+                                            const ZO& zo_of, double* kp, int lane) {
+    if (AIY_PAR_PROBE == 3) return;
+    for (int t = Ts; t < Tn; ++t) {
+        k = ps.step(k, zo_of(t), zo_of(t + 1));
+        if (lane == 0) kp[t] = k;
+    }
+}
+
+// one wave: repair segment [Ts, Tn) from k (its predecessor's end): step until the value equals
+// the stored one bit for bit (from there the stored path is the true one) or overwrite the whole
+// segment; returns 1 when the segment's last value changed.  The stored values are read in
+// chunks of 64 (one per lane, the next chunk in flight) and read back with v_readlane: no
+// dependent global load per step.
+template <int SS, class ZO>
+__device__ __forceinline__ int par_repair(ParStepper<SS>& ps, double k, int Ts, int Tn,
+                                          const ZO& zo_of, double* kp, int lane) {
+    ps.primed = false;
+    int cb = Ts, chg = 0;
+    double sv = Ts + lane < Tn ? kp[Ts + lane] : 0.0;
+    double sn = Ts + 64 + lane < Tn ? kp[Ts + 64 + lane] : 0.0;
+    for (int t = Ts; t < Tn; ++t) {
+        if (t - cb == 64) {
+            cb = t;
+            sv = sn;
+            sn = cb + 64 + lane < Tn ? kp[cb + 64 + lane] : 0.0;
         }
+        k = ps.step(k, zo_of(t), zo_of(t + 1));
+        const unsigned long long kb = __builtin_bit_cast(unsigned long long, k);
+        const unsigned long long sb =
+            __builtin_bit_cast(unsigned long long, readlane_d(sv, t - cb));
+        if (kb == sb) break;  // the stored path is the true one from here
+        if (lane == 0) kp[t] = k;
+        if (t == Tn - 1) chg = 1;
     }
-    if (tid == 0) kp[0] = A.k1;
-    if (lane == 0) {
-        s_res[wave] = wave == 0 || AIY_PAR_PROBE >= 2 ? 1 : (Ts < Tn ? 0 : 1);  // (empty: true)
-        s_chg[wave] = 0;
+    return chg;
+}
+
+// segment s of a chain stopping at Te: steps [Ts, Tn)
+__device__ __forceinline__ void par_seg_range(int Te, int s, int& Ts, int& Tn) {
+    const int L = (Te - 1 + kParWaves - 1) / kParWaves;  // >= 0
+    Ts = 1 + s * L;
+    Tn = min(Te, Ts + L);
+}
+
+// a segment is true once its predecessor was true when the pass started, or became true in the
+// same pass without changing its last value (one thread)
+__device__ __forceinline__ void par_resolve(int* res, const int* chg) {
+    int prev_old = res[0], prev_new = 1;
+    for (int q = 1; q < kParWaves; ++q) {
+        const int old = res[q];
+        const int nw = old || prev_old || (prev_new && !chg[q - 1]);
+        prev_old = old;
+        prev_new = nw;
+        res[q] = nw;
     }
-    __syncthreads();
+}
+
+// repair passes until every segment is true (16 waves, zp and the tables in LDS), then the mean
+// (wave 0: the sequential fp64 sum k_0 .. k_{Te-1}) and the outputs.  s_res holds the segments'
+// state on entry.
+template <int SS, class ZO>
+__device__ __forceinline__ void par_passes_sum(const SimArgs& A, ParStepper<SS>& ps,
+                                               const ZO& zo_of, double* kp, int Te, int* s_res,
+                                               int* s_chg, int* s_go) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int Ts, Tn;
+    par_seg_range(Te, wave, Ts, Tn);
     for (;;) {
         if (tid == 0) {
             int go = 0;
             for (int q = 0; q < kParWaves; ++q) go |= !s_res[q];
-            s_go = go;
+            *s_go = go;
         }
         __syncthreads();
-        if (!s_go) break;
+        if (!*s_go) break;
         const bool mine = !s_res[wave];
-        double k = mine ? kp[Ts - 1] : 0.0;  // every start read before any repair writes
+        const double k = mine ? kp[Ts - 1] : 0.0;  // every start read before any repair writes
         __syncthreads();
-        int chg = 0;
-        if (mine) {
-            ps.primed = false;
-            // the stored values in chunks of 64 (one per lane, the next chunk in flight), read
-            // back with v_readlane: no dependent global load per step
-            int cb = Ts;
-            double sv = Ts + lane < Tn ? kp[Ts + lane] : 0.0;
-            double sn = Ts + 64 + lane < Tn ? kp[Ts + 64 + lane] : 0.0;
-            for (int t = Ts; t < Tn; ++t) {
-                if (t - cb == 64) {
-                    cb = t;
-                    sv = sn;
-                    sn = cb + 64 + lane < Tn ? kp[cb + 64 + lane] : 0.0;
-                }
-                k = ps.step(k, zo_of(t), zo_of(t + 1));
-                const unsigned long long kb = __builtin_bit_cast(unsigned long long, k);
-                const unsigned long long sb =
-                    __builtin_bit_cast(unsigned long long, readlane_d(sv, t - cb));
-                if (kb == sb) break;  // the stored path is the true one from here
-                if (lane == 0) kp[t] = k;
-                if (t == Tn - 1) chg = 1;
-            }
-        }
+        const int chg = mine ? par_repair(ps, k, Ts, Tn, zo_of, kp, lane) : 0;
         if (lane == 0) s_chg[wave] = chg;
         __syncthreads();
-        if (tid == 0) {
-            int prev_old = s_res[0], prev_new = 1;
-            for (int q = 1; q < kParWaves; ++q) {
-                const int old = s_res[q];
-                const int nw = old || prev_old || (prev_new && !s_chg[q - 1]);
-                prev_old = old;
-                prev_new = nw;
-                s_res[q] = nw;
-            }
-        }
+        if (tid == 0) par_resolve(s_res, s_chg);
         __syncthreads();
     }
-    // S. the mean (sequential fp64 sum, k_0 .. k_{Te-1}) and the outputs
     if (wave == 0 && (AIY_PAR_PROBE == 0 || AIY_PAR_PROBE == 2)) {
         double v = lane < Te ? kp[lane] : 0.0;
         double sum = readlane_d(v, 0);  // sum = k_1 (the serial kernel's start), then in order
@@ -789,15 +794,175 @@ __global__ __launch_bounds__(1024) void sim_chain_par_kernel(SimArgs A0) {
         }
         if (lane == 0) {
             A.out[0] = sum / (double)A.T;
-            A.status[0] = Te < T ? 1 : 0;
+            A.status[0] = Te < A.T ? 1 : 0;
         }
+    }
+}
+
+// chain blockIdx.x / per of a batch: its policy, uniforms, outputs and path scratch
+__device__ __forceinline__ SimArgs par_chain(const SimArgs& A0, int c, double** kp) {
+    SimArgs A = A0;
+    *kp = A0.kscr;
+    if (A0.C > 1) {
+        A.pol += c * A0.pcs;
+        A.U += c * A0.ucs;
+        A.out += c;
+        A.status += c;
+        *kp += (size_t)c * A0.T;
+    }
+    if (A.sim_k) *kp = A.sim_k;  // the path is the output itself (C = 1)
+    return A;
+}
+// the spread variant's scratch after the k paths: state paths [C][T] bytes, then per chain
+// {Te, chg[kParWaves]} ints
+__device__ __forceinline__ unsigned char* par_zg(const SimArgs& A0, int c) {
+    return reinterpret_cast<unsigned char*>(A0.kscr + (size_t)max(A0.C, 1) * A0.T) + (size_t)c * A0.T;
+}
+__device__ __forceinline__ int* par_ig(const SimArgs& A0, int c) {
+    const size_t zb = ((size_t)max(A0.C, 1) * A0.T + 7) & ~(size_t)7;
+    return reinterpret_cast<int*>(reinterpret_cast<unsigned char*>(A0.kscr + (size_t)max(A0.C, 1) * A0.T) + zb) +
+           (size_t)c * (1 + kParWaves);
+}
+
+template <int SS, bool PATH>
+__global__ __launch_bounds__(1024) void sim_chain_par_kernel(SimArgs A0) {
+    double* kp;
+    const SimArgs A = par_chain(A0, blockIdx.x, &kp);
+    extern __shared__ double lds[];
+    __shared__ unsigned char zp[kParMaxT];
+    __shared__ unsigned s_map[1024];
+    __shared__ double s_cs[64];
+    __shared__ int s_stop, s_go;
+    __shared__ int s_res[kParWaves], s_chg[kParWaves];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    par_tables<SS>(A, lds, tid, 1024);
+    const int Te = par_zpath(A, zp, s_map, s_cs, &s_stop);  // (its barriers cover the tables)
+    const int zrow = SS * 16;
+    auto zo_of = [&](int t) __attribute__((always_inline)) { return t < Te ? (int)zp[t] * zrow : 0; };
+    int Ts, Tn;
+    par_seg_range(Te, wave, Ts, Tn);
+    ParStepper<SS> ps{lds, lds + SS, lds + 2 * SS, A.Na, A.Na - 64, lane, 0, false, 0.0, 0.0, 0.0, 0.0};
+    if (Ts < Tn) par_segment(ps, A.k1, Ts, Tn, zo_of, kp, lane);
+    if (tid == 0) kp[0] = A.k1;
+    if (lane == 0) {
+        s_res[wave] = wave == 0 || AIY_PAR_PROBE >= 2 ? 1 : (Ts < Tn ? 0 : 1);  // (empty: true)
+        s_chg[wave] = 0;
+    }
+    __syncthreads();
+    par_passes_sum(A, ps, zo_of, kp, Te, s_res, s_chg, &s_go);
+    if (PATH && A.sim_z)
+        for (int t = tid; t < Te; t += 1024) A.sim_z[t] = zp[t];
+}
+
+// The spread variant (round 6): the same computation in four launches, so that the 16 segments
+// run on 16 CUs (one wave per SIMD) instead of sharing one CU's four SIMDs (four waves each:
+// 571 vs 158 ns per step, profiles/r06_g23_sim_par_phases.txt).  Launch 1 (one 1,024-thread
+// workgroup per chain): the state path and Te into the scratch.  Launch 2 (16 one-wave
+// workgroups per chain): each its segment from the guess.  Launch 3 (same): repair pass 1 of
+// every segment s >= 1 from its predecessor's stored end — that end may be rewritten by the
+// predecessor's own repair meanwhile, but a start is then only trusted when the predecessor's
+// end did not change (par_resolve), so either value read is safe.  Launch 4 (one workgroup per
+// chain): the segments' state after pass 1, further passes in one CU if any is still untrusted
+// (rare), then the in-order sum.  Same values as sim_chain_par_kernel bit for bit.
+template <bool PATH>
+__global__ __launch_bounds__(1024) void sim_par_z_kernel(SimArgs A0) {
+    double* kp;
+    const SimArgs A = par_chain(A0, blockIdx.x, &kp);
+    __shared__ unsigned char zp[kParMaxT];
+    __shared__ unsigned s_map[1024];
+    __shared__ double s_cs[64];
+    __shared__ int s_stop;
+    const int tid = threadIdx.x;
+    const int Te = par_zpath(A, zp, s_map, s_cs, &s_stop);
+    unsigned char* zg = par_zg(A0, blockIdx.x);
+    for (int t = tid; t < A.T; t += 1024) zg[t] = zp[t];
+    if (tid == 0) {
+        par_ig(A0, blockIdx.x)[0] = Te;
+        kp[0] = A.k1;
     }
     if (PATH && A.sim_z)
         for (int t = tid; t < Te; t += 1024) A.sim_z[t] = zp[t];
 }
 
-// the speculative-segment chain; AIY_BAD_SHAPE when it does not apply
-int launch_sim_chain_par(const SimArgs& A, hipStream_t st) {
+constexpr int kParSlice = kParMaxT / kParWaves + 2;  // a segment's states [Ts, Tn]
+template <int SS, bool FIX>
+__global__ __launch_bounds__(64) void sim_par_seg_kernel(SimArgs A0) {
+    const int c = blockIdx.x / kParWaves, s = blockIdx.x % kParWaves, lane = threadIdx.x;
+    double* kp;
+    const SimArgs A = par_chain(A0, c, &kp);
+    int* ig = par_ig(A0, c);
+    if (FIX && s == 0) {
+        if (lane == 0) ig[1] = 0;
+        return;
+    }
+    const int Te = ig[0];
+    int Ts, Tn;
+    par_seg_range(Te, s, Ts, Tn);
+    if (Ts >= Tn) {
+        if (FIX && lane == 0) ig[1 + s] = 0;
+        return;
+    }
+    extern __shared__ double lds[];
+    __shared__ unsigned char zs[kParSlice];
+    const unsigned char* zg = par_zg(A0, c);
+    for (int t = Ts + lane; t <= Tn; t += 64) zs[t - Ts] = t < Te ? zg[t] : 0;
+    par_tables<SS>(A, lds, lane, 64);
+    __syncthreads();
+    const int zrow = SS * 16;
+    auto zo_of = [&](int t) __attribute__((always_inline)) { return t < Te ? (int)zs[t - Ts] * zrow : 0; };
+    ParStepper<SS> ps{lds, lds + SS, lds + 2 * SS, A.Na, A.Na - 64, lane, 0, false, 0.0, 0.0, 0.0, 0.0};
+    if (!FIX) {
+        par_segment(ps, A.k1, Ts, Tn, zo_of, kp, lane);
+    } else {
+        const double k = kp[Ts - 1];
+        const int chg = AIY_PAR_PROBE >= 2 ? 0 : par_repair(ps, k, Ts, Tn, zo_of, kp, lane);
+        if (lane == 0) ig[1 + s] = chg;
+    }
+}
+
+template <int SS>
+__global__ __launch_bounds__(1024) void sim_par_sum_kernel(SimArgs A0) {
+    double* kp;
+    const SimArgs A = par_chain(A0, blockIdx.x, &kp);
+    const int* ig = par_ig(A0, blockIdx.x);
+    extern __shared__ double lds[];
+    __shared__ unsigned char zp[kParMaxT];
+    __shared__ int s_go, s_all;
+    __shared__ int s_res[kParWaves], s_chg[kParWaves];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int Te = ig[0];
+    if (tid < kParWaves) {
+        int Ts, Tn;
+        par_seg_range(Te, tid, Ts, Tn);
+        s_res[tid] = tid == 0 || Ts >= Tn ? 1 : 0;  // before pass 1 (launch 3)
+        s_chg[tid] = ig[1 + tid];
+    }
+    __syncthreads();
+    if (tid == 0) {
+        par_resolve(s_res, s_chg);
+        int all = 1;
+        for (int q = 0; q < kParWaves; ++q) all &= s_res[q];
+        s_all = all;
+    }
+    __syncthreads();
+    const int zrow = SS * 16;
+    auto zo_of = [&](int t) __attribute__((always_inline)) { return t < Te ? (int)zp[t] * zrow : 0; };
+    ParStepper<SS> ps{lds, lds + SS, lds + 2 * SS, A.Na, A.Na - 64, lane, 0, false, 0.0, 0.0, 0.0, 0.0};
+    if (!s_all) {  // (rare) more passes, on this CU: the tables and the state path into LDS
+        par_tables<SS>(A, lds, tid, 1024);
+        const unsigned char* zg = par_zg(A0, blockIdx.x);
+        for (int t = tid; t < A.T; t += 1024) zp[t] = zg[t];
+        __syncthreads();
+    }
+    (void)wave;
+    par_passes_sum(A, ps, zo_of, kp, Te, s_res, s_chg, &s_go);
+}
+
+// the speculative-segment chain; AIY_BAD_SHAPE when it does not apply.  spread: the four-launch
+// variant (16 CUs per chain), else one workgroup per chain
+int launch_sim_chain_par(const SimArgs& A, hipStream_t st, bool spread) {
     if (A.N < 1 || A.N > 7 || A.Na < 64 || A.T < 2 || A.T > kParMaxT || !A.kscr)
         return fail(AIY_BAD_SHAPE, "speculative chain: N <= 7, Na >= 64, 2 <= T <= 16384, scratch");
     const int S = A.Na + 64;
@@ -806,16 +971,30 @@ int launch_sim_chain_par(const SimArgs& A, hipStream_t st) {
     const size_t bytes = sizeof(double) * (size_t)(2 + 2 * A.N) * SS;
     const int g = std::max(A.C, 1);
     const bool path = A.sim_k || A.sim_z;
-#define AIY_PAR(SS_, PA_)                                                                          \
+    // the dynamic-LDS limit is raised once per instantiation, to the most any call asks for
+#define AIY_LDS_ONCE(K_, SS_)                                                                      \
     do {                                                                                           \
         static std::atomic<bool> lds_set{false};                                                   \
         if (!lds_set) {                                                                            \
-            AIY_HIP(hipFuncSetAttribute((const void*)sim_chain_par_kernel<SS_, PA_>,               \
-                                        hipFuncAttributeMaxDynamicSharedMemorySize,                \
+            AIY_HIP(hipFuncSetAttribute((const void*)K_, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                         (int)sizeof(double) * (2 + 2 * 7) * SS_));                 \
             lds_set = true;                                                                        \
         }                                                                                          \
-        sim_chain_par_kernel<SS_, PA_><<<g, 1024, bytes, st>>>(A);                                 \
+    } while (0)
+#define AIY_PAR(SS_, PA_)                                                                          \
+    do {                                                                                           \
+        if (spread) {                                                                              \
+            AIY_LDS_ONCE((sim_par_seg_kernel<SS_, false>), SS_);                                   \
+            AIY_LDS_ONCE((sim_par_seg_kernel<SS_, true>), SS_);                                    \
+            AIY_LDS_ONCE((sim_par_sum_kernel<SS_>), SS_);                                          \
+            sim_par_z_kernel<PA_><<<g, 1024, 0, st>>>(A);                                          \
+            sim_par_seg_kernel<SS_, false><<<g * kParWaves, 64, bytes, st>>>(A);                   \
+            sim_par_seg_kernel<SS_, true><<<g * kParWaves, 64, bytes, st>>>(A);                    \
+            sim_par_sum_kernel<SS_><<<g, 1024, bytes, st>>>(A);                                    \
+        } else {                                                                                   \
+            AIY_LDS_ONCE((sim_chain_par_kernel<SS_, PA_>), SS_);                                   \
+            sim_chain_par_kernel<SS_, PA_><<<g, 1024, bytes, st>>>(A);                             \
+        }                                                                                          \
     } while (0)
     if (SS == 512) {
         if (path) AIY_PAR(512, true);
@@ -825,6 +1004,7 @@ int launch_sim_chain_par(const SimArgs& A, hipStream_t st) {
         else AIY_PAR(1024, false);
     }
 #undef AIY_PAR
+#undef AIY_LDS_ONCE
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }
@@ -870,7 +1050,9 @@ int launch_sim_capital(const SimArgs& A, hipStream_t st) {
     // the speculative-segment chain for the GE loop's long chains (T = 10,000: 1.6 ms serial)
     const bool par_ok = A.kscr && A.N <= 7 && A.Na >= 64 && A.Na + 64 <= 1024 && A.T >= 2 &&
                         A.T <= kParMaxT;
-    if (par_ok && (A.par > 0 || (A.par < 0 && A.T >= 2048))) return launch_sim_chain_par(A, st);
+    // (par: -1 by size — the spread variant; 1 one workgroup per chain; 2 the spread variant)
+    if (par_ok && (A.par > 0 || (A.par < 0 && A.T >= 2048)))
+        return launch_sim_chain_par(A, st, A.par != 1);
     if (A.N <= 8 && A.Na >= 64 && (A.Na + 64 <= 512 || (A.Na + 64 <= 1024 && A.N <= 7)))
         return launch_sim_chain_pipe(A, st);
     if (A.N <= 15) {

@@ -51,8 +51,8 @@ struct aiy_ws {
     // Na <= wide_max (-1: the default bound) with `wide_S` splits of `wide_NW` waves (0: by size)
     int wide_max = -1, wide_S = 0, wide_NW = 0, wide_SB = 0;
     bool cu_exclusive = false;  // aiy_ws_set_cu_exclusive
-    // A9 chains (aiy_ws_set_sim): -1 by size, 0 the serial kernels, 1 the speculative-segment
-    // kernel whenever it applies; its k-path scratch
+    // A9 chains (aiy_ws_set_sim): -1 by size, 0 the serial kernels, 1 / 2 the speculative-
+    // segment chain (one workgroup / spread over 16) whenever it applies; its scratch (bytes)
     int sim_par = -1;
     double* sim_kbuf = nullptr;
     size_t sim_kcap = 0;

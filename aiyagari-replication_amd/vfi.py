@@ -142,7 +142,8 @@ class Workspace:
 
     def set_sim(self, mode: int = -1):
         """A9 chains on this workspace (aiy_ws_set_sim): -1 by size (the speculative-segment
-        chain for long chains), 0 the serial kernels, 1 the speculative chain wherever it
+        chain, spread over 16 workgroups, for long chains), 0 the serial kernels, 1 the
+        speculative chain in one workgroup wherever it applies, 2 the spread variant wherever it
         applies.  Results do not depend on it."""
         check(lib().aiy_ws_set_sim(self._h, ip(int(mode))))
 

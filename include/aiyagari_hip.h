@@ -270,8 +270,11 @@ int aiy_ws_set_cu_exclusive(aiy_ws* ws, int on);
  * segment chain (16 waves each run a segment of the k recurrence from a guess, then repair it
  * from its predecessor's true end until the stored path matches bit for bit; the state path by a
  * parallel scan of composed transition maps) for 2,048 <= T <= 16,384, N <= 7, 64 <= Na <= 960,
- * the serial kernels otherwise; 0: always the serial kernels; 1: the speculative chain wherever
- * it applies.  Results (K_s, the paths, find() errors) are identical for every mode. */
+ * the serial kernels otherwise — spread over 16 workgroups (four launches: the state path; the
+ * segments; the first repair pass; further passes if any and the in-order sum); 0: always the
+ * serial kernels; 1: the speculative chain in one workgroup per chain wherever it applies; 2: the
+ * spread variant wherever it applies.  Results (K_s, the paths, find() errors) are identical for
+ * every mode. */
 int aiy_ws_set_sim(aiy_ws* ws, int mode);
 /* kernel shapes and A/B knobs (tuning only; results are identical for every value in
  * [-1, 2^30)).  VFI, bit 3 clear (default): the bound tree screen, bit 0 = 2 states per lane

@@ -1,7 +1,8 @@
 """GPU: the speculative-segment A9 chain (sim_chain_par_kernel) against the
 serial chain kernels and the C restatement, bit for bit (Aiyagari_VFI.m:104-129).  Device tier,
-the mode forced per workspace (aiy_ws_set_sim: 1 speculative wherever it applies, 0 serial), so
-the short chains the size rule would send to the serial kernels run through the segments too.
+the mode forced per workspace (aiy_ws_set_sim: 1 speculative in one workgroup, 2 the spread
+four-launch variant, 0 serial), so the short chains the size rule would send to the serial
+kernels run through the segments too.
 The adversarial case is a policy whose paths never coalesce (k' = k + 0.5 everywhere, linear
 extrapolation): every speculative start is wrong, each repair pass makes exactly one more
 segment true, and the chain needs all 15 passes with every segment overwritten whole."""
@@ -46,7 +47,8 @@ def _run(pkg, ws, mode, pol, a, P, z1, k1, U, path=True):
                                     (7, 400, 100), (7, 64, 2049), (1, 200, 500), (7, 960, 4200),
                                     (3, 500, 10000), (7, 400, 16384)])
 @pytest.mark.parametrize("kind", ["smooth", "jumpy", "drift"])
-def test_par_chain_equals_serial_and_oracle(pkg, gpu, N, Na, T, kind):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_par_chain_equals_serial_and_oracle(pkg, gpu, N, Na, T, kind, mode):
     """Every segment count edge (T - 1 below, at and above 16 steps; empty segments), the
     smallest grid (Na = 64) and the largest LDS table (Na = 960), N = 1, T at the LDS bound."""
     rng = np.random.default_rng(N * 100003 + Na * 7 + T)
@@ -62,9 +64,9 @@ def test_par_chain_equals_serial_and_oracle(pkg, gpu, N, Na, T, kind):
     z1, k1 = N - 1, float(a[Na // 2])
     ws = pkg.Workspace(N, Na)
     try:
-        Kp, sp, kp, zp = _run(pkg, ws, 1, pol, a, P, z1, k1, U)
+        Kp, sp, kp, zp = _run(pkg, ws, mode, pol, a, P, z1, k1, U)
         Ks, ss, ksr, zs = _run(pkg, ws, 0, pol, a, P, z1, k1, U)
-        Km, sm, _, _ = _run(pkg, ws, 1, pol, a, P, z1, k1, U, path=False)
+        Km, sm, _, _ = _run(pkg, ws, mode, pol, a, P, z1, k1, U, path=False)
     finally:
         ws.close()
     Ko, po = corc.sim_capital(pol, a, P, z1, k1, U, return_path=True)
@@ -80,7 +82,8 @@ def test_par_chain_equals_serial_and_oracle(pkg, gpu, N, Na, T, kind):
 
 @pytest.mark.parametrize("T,t_bad", [(10000, 2), (10000, 626), (10000, 9999), (300, 40),
                                      (20, 19)])
-def test_par_chain_find_empty(pkg, gpu, T, t_bad):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_par_chain_find_empty(pkg, gpu, T, t_bad, mode):
     """find() empty at step t_bad (first step, a segment boundary, the last step, short
     chains): the speculative chain stops there as the serial one does — status 1, and the path
     before t_bad and the z path agree."""
@@ -94,7 +97,7 @@ def test_par_chain_find_empty(pkg, gpu, T, t_bad):
     pol = np.sort(rng.uniform(0, a[-1], (N, Na)), axis=1)
     ws = pkg.Workspace(N, Na)
     try:
-        Kp, sp, kp, zp = _run(pkg, ws, 1, pol, a, P, 2, float(a[Na // 2]), U)
+        Kp, sp, kp, zp = _run(pkg, ws, mode, pol, a, P, 2, float(a[Na // 2]), U)
         Ks, ss, ksr, zs = _run(pkg, ws, 0, pol, a, P, 2, float(a[Na // 2]), U)
     finally:
         ws.close()
@@ -116,8 +119,9 @@ def test_par_chain_shape_rule_falls_back(pkg, gpu):
         ws = pkg.Workspace(N, Na)
         try:
             r1 = _run(pkg, ws, 1, pol, a, P, 0, float(a[3]), U)
+            r2 = _run(pkg, ws, 2, pol, a, P, 0, float(a[3]), U)
             r0 = _run(pkg, ws, 0, pol, a, P, 0, float(a[3]), U)
         finally:
             ws.close()
-        assert r1[0] == r0[0] and r1[1] == r0[1] == 0
-        assert np.array_equal(r1[2], r0[2])
+        assert r1[0] == r2[0] == r0[0] and r1[1] == r2[1] == r0[1] == 0
+        assert np.array_equal(r1[2], r0[2]) and np.array_equal(r2[2], r0[2])
