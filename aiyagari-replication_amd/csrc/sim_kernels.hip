@@ -611,7 +611,9 @@ __device__ __forceinline__ unsigned zmap_compose(unsigned A, unsigned B) {  // A
     return R;
 }
 
-// the chain's LDS tables (X0[SS] | H[SS] | Y[N][SS][2] = {y_i, y_{i+1} - y_i}), by nthr threads
+// the chain's LDS tables (X0[SS] | H[SS] | Y[N][SS][2] = {y_i, y_{i+1} - y_i}), by nthr threads;
+// eight elements' loads in flight per thread before their stores (a small workgroup would
+// otherwise pay one memory round trip per element)
 template <int SS>
 __device__ __forceinline__ void par_tables(const SimArgs& A, double* lds, int tid, int nthr) {
     double* X0 = lds;
@@ -623,13 +625,26 @@ __device__ __forceinline__ void par_tables(const SimArgs& A, double* lds, int ti
         X0[i] = x0;
         H[i] = x1 - x0;
     }
-    for (int q = tid; q < A.N * SS; q += nthr) {
-        const int zz = q / SS, i = q - zz * SS;
-        const double* row = A.pol + (size_t)zz * A.zs;
-        const double y0 = i < Na ? row[(size_t)i * A.as] : 0.0;
-        const double y1 = i + 1 < Na ? row[(size_t)(i + 1) * A.as] : 0.0;
-        Y[2 * (size_t)q] = y0;
-        Y[2 * (size_t)q + 1] = y1 - y0;
+    const int nq = A.N * SS;
+    for (int q0 = tid; q0 < nq; q0 += 8 * nthr) {
+        double y0[8], y1[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int q = q0 + u * nthr;
+            const int zz = q / SS, i = q - zz * SS;
+            const double* row = A.pol + (size_t)zz * A.zs;
+            const bool ok = q < nq;
+            y0[u] = ok && i < Na ? row[(size_t)i * A.as] : 0.0;
+            y1[u] = ok && i + 1 < Na ? row[(size_t)(i + 1) * A.as] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int q = q0 + u * nthr;
+            if (q < nq) {
+                Y[2 * (size_t)q] = y0[u];
+                Y[2 * (size_t)q + 1] = y1[u] - y0[u];
+            }
+        }
     }
 }
 
@@ -886,29 +901,33 @@ __global__ __launch_bounds__(1024) void sim_par_z_kernel(SimArgs A0) {
 }
 
 constexpr int kParSlice = kParMaxT / kParWaves + 2;  // a segment's states [Ts, Tn]
+// (256 threads: four waves stage the tables, then wave 0 alone runs the segment)
+constexpr int kParSegThreads = 256;
 template <int SS, bool FIX>
-__global__ __launch_bounds__(64) void sim_par_seg_kernel(SimArgs A0) {
-    const int c = blockIdx.x / kParWaves, s = blockIdx.x % kParWaves, lane = threadIdx.x;
+__global__ __launch_bounds__(kParSegThreads) void sim_par_seg_kernel(SimArgs A0) {
+    const int c = blockIdx.x / kParWaves, s = blockIdx.x % kParWaves;
+    const int tid = threadIdx.x, lane = tid & 63;
     double* kp;
     const SimArgs A = par_chain(A0, c, &kp);
     int* ig = par_ig(A0, c);
     if (FIX && s == 0) {
-        if (lane == 0) ig[1] = 0;
+        if (tid == 0) ig[1] = 0;
         return;
     }
     const int Te = ig[0];
     int Ts, Tn;
     par_seg_range(Te, s, Ts, Tn);
     if (Ts >= Tn) {
-        if (FIX && lane == 0) ig[1 + s] = 0;
+        if (FIX && tid == 0) ig[1 + s] = 0;
         return;
     }
     extern __shared__ double lds[];
     __shared__ unsigned char zs[kParSlice];
     const unsigned char* zg = par_zg(A0, c);
-    for (int t = Ts + lane; t <= Tn; t += 64) zs[t - Ts] = t < Te ? zg[t] : 0;
-    par_tables<SS>(A, lds, lane, 64);
+    for (int t = Ts + tid; t <= Tn; t += kParSegThreads) zs[t - Ts] = t < Te ? zg[t] : 0;
+    par_tables<SS>(A, lds, tid, kParSegThreads);
     __syncthreads();
+    if (tid >= 64) return;
     const int zrow = SS * 16;
     auto zo_of = [&](int t) __attribute__((always_inline)) { return t < Te ? (int)zs[t - Ts] * zrow : 0; };
     ParStepper<SS> ps{lds, lds + SS, lds + 2 * SS, A.Na, A.Na - 64, lane, 0, false, 0.0, 0.0, 0.0, 0.0};
@@ -988,8 +1007,8 @@ int launch_sim_chain_par(const SimArgs& A, hipStream_t st, bool spread) {
             AIY_LDS_ONCE((sim_par_seg_kernel<SS_, true>), SS_);                                    \
             AIY_LDS_ONCE((sim_par_sum_kernel<SS_>), SS_);                                          \
             sim_par_z_kernel<PA_><<<g, 1024, 0, st>>>(A);                                          \
-            sim_par_seg_kernel<SS_, false><<<g * kParWaves, 64, bytes, st>>>(A);                   \
-            sim_par_seg_kernel<SS_, true><<<g * kParWaves, 64, bytes, st>>>(A);                    \
+            sim_par_seg_kernel<SS_, false><<<g * kParWaves, kParSegThreads, bytes, st>>>(A);       \
+            sim_par_seg_kernel<SS_, true><<<g * kParWaves, kParSegThreads, bytes, st>>>(A);        \
             sim_par_sum_kernel<SS_><<<g, 1024, bytes, st>>>(A);                                    \
         } else {                                                                                   \
             AIY_LDS_ONCE((sim_chain_par_kernel<SS_, PA_>), SS_);                                   \

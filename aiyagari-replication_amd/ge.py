@@ -474,6 +474,7 @@ class _GESim:
         # the chain's workgroup reserves its CU so no speculative solve block shares it (a
         # co-resident block slows the serial wave; opt-in per workspace since ADVICE r5)
         self.ws.set_cu_exclusive(True)
+        self.ws.set_sim(_GE_SIM_MODE)
         self.k = torch.zeros(1, dtype=torch.float64, device=dev)
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)
         self.kh = torch.zeros(1, dtype=torch.float64).pin_memory()  # host copies (pinned)
@@ -486,6 +487,8 @@ class _GESim:
 # three alternating rounds; busy polling 23.6)
 import os as _os  # noqa: E402
 _CHAIN_NAP = float(_os.environ.get("AIY_GE_CHAIN_NAP", "2e-5"))  # profiles/r06_g15_ge_chain_nap.txt
+# the chains' variant (aiy_ws_set_sim; an A/B knob, results identical): -1 by size
+_GE_SIM_MODE = int(_os.environ.get("AIY_GE_SIM_MODE", "-1"))
 _GE_POOLS = {}  # (device, N, Na) -> (solve slots, chain resources) of aiyagari_vfi_overlapped
 _GE_STREAMS = {}  # device -> the driver's streams
 
