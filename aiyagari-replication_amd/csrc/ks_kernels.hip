@@ -54,13 +54,14 @@ __device__ __forceinline__ double ks_bellman_dev(const KsArgs& A, const KsView& 
     double kq = fmax(fmin(kp, W.kg[nk - 1]), W.kg[0]);
     int seg = hint >= 0 ? seg_hinted_dev(W.kg, nk, kq, hint) : seg_of_dev(W.kg, nk, kq);
     double expec = 0;
+    const double h = W.kg[seg + 1] - W.kg[seg], rh = 1.0 / h;  // the four queries' segment
 #pragma unroll
     for (int sn = 0; sn < 4; ++sn) {
         const int c = sn * A.nK + sl.kp_idx;  // (slice-uniform: scalar loads of the table)
         const size_t col = (size_t)c * nk;
         const double* Vc = A.colV ? A.colV[c] : W.V + col;
         const double* dVc = A.colV ? A.coldV[c] : W.dV + col;
-        expec = expec + A.P[si * 4 + sn] * pchip_at<SC1>(W.kg, Vc, dVc, seg, kq);
+        expec = expec + A.P[si * 4 + sn] * pchip_at<SC1>(W.kg, Vc, dVc, seg, kq, h, rh);
     }
     double c = (sl.a1 * k + sl.a2) - kp;
     c = fmax(c, 1e-10);

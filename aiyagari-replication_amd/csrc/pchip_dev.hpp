@@ -67,18 +67,34 @@ __device__ __forceinline__ double col_ld(const double* p) {
         return *p;
 }
 
-// pwch coefficients + ppval Horner on segment i
+// RN(a / b) for b > 0 from rb = RN(1 / b): q = RN(a·rb), then two residual corrections
+// q += fma(−q, b, a)·rb (Markstein: with rb correctly rounded and q faithful, the corrected
+// quotient is the correctly rounded one — no overflow or underflow here: grid spans and value
+// differences; tools/micro/fastdiv_check.c: 2·10⁸ random and adversarial pairs, one correction
+// misses 1, two miss 0).  A zero numerator keeps its sign, as IEEE a / b does for b > 0.  Five
+// dependent fp64 operations instead of the eleven of the IEEE division sequence.
+__device__ __forceinline__ double div_by_rcp(double a, double b, double rb) {
+    double q = a * rb;
+    double e = __builtin_fma(-q, b, a);
+    q = __builtin_fma(e, rb, q);
+    e = __builtin_fma(-q, b, a);
+    q = __builtin_fma(e, rb, q);
+    return a == 0.0 ? a : q;
+}
+
+// pwch coefficients + ppval Horner on segment i; rh = RN(1 / h) of the segment (the forecast
+// queries of one node share the segment: one IEEE division for all of them)
 template <bool SC1 = false>
 __device__ __forceinline__ double pchip_at(const double* __restrict__ x,
                                            const double* __restrict__ y,
-                                           const double* __restrict__ d, int i, double xq) {
+                                           const double* __restrict__ d, int i, double xq,
+                                           double h, double rh) {
     const double y0 = col_ld<SC1>(y + i), y1 = col_ld<SC1>(y + i + 1);
     const double d0 = col_ld<SC1>(d + i), d1 = col_ld<SC1>(d + i + 1);
-    double h = x[i + 1] - x[i];
-    double dl = (y1 - y0) / h;
-    double dzzdx = (dl - d0) / h;
-    double dzdxdx = (d1 - dl) / h;
-    double c3 = (dzdxdx - dzzdx) / h;
+    double dl = div_by_rcp(y1 - y0, h, rh);
+    double dzzdx = div_by_rcp(dl - d0, h, rh);
+    double dzdxdx = div_by_rcp(d1 - dl, h, rh);
+    double c3 = div_by_rcp(dzdxdx - dzzdx, h, rh);
     double c2 = 2 * dzzdx - dzdxdx;
     double sx = xq - x[i];
     double v = c3;
