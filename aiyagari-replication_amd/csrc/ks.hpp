@@ -17,6 +17,9 @@ struct KsArgs {
     int nk, nK;
     int node0, n_local;  // node range handled by this launch (sharding)
     const double* k_grid;
+    // nullable: the grid's slope tables (launch_ks_grid_tables: [nk] RN(1 / h_i), then [2·nk]
+    // the interior weights of each node) — the tiled slopes use them, same values
+    const double* kg_tab;
     const double* P;     // 4 x 4 row-major
     const KsSlice* slice;  // [s][K]
     double beta, k_min, k_max, tol;
@@ -77,6 +80,7 @@ bool ks_fused_fits(int nk, int nK);
 int launch_ks_fused(const KsArgs& A, double* V, double* kopt, int* nfev, KsOut* out,
                     hipStream_t st);
 int launch_ks_slopes(const KsArgs& A, const double* V, double* dV, hipStream_t st);
+int launch_ks_grid_tables(const double* kg, int nk, double* tab, hipStream_t st);
 int launch_ks_slopes_cols(const KsArgs& A, const int* cols, int ncols, const double* V,
                           double* dV, hipStream_t st);
 int launch_ks_improve(const KsArgs& A, const double* V, const double* dV, double* kopt,

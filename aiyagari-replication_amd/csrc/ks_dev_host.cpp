@@ -24,6 +24,7 @@ struct ks_dev {
     int s0 = 0, s1 = 4;  // owned s blocks [s0, s1): all four, or one z's pair ((K, Z) slices)
     double beta = 0, k_min = 0, k_max = 0;
     double* kg = nullptr;
+    double* kgt = nullptr;  // the grid's slope tables (launch_ks_grid_tables), 3·nk doubles
     double* P = nullptr;
     aiy::KsSlice* sl = nullptr;
     double* dV = nullptr;
@@ -61,6 +62,7 @@ static KsArgs shard_args(const ks_dev* h) {
     A.ns = h->s1 - h->s0;
     A.sstride = h->nK * h->nk;
     A.k_grid = h->kg;
+    A.kg_tab = h->kgt;
     A.P = h->P;
     A.slice = h->sl;
     A.beta = h->beta;
@@ -83,7 +85,7 @@ int ks_dev_destroy(ks_dev* h) {
         return fail(AIY_BAD_ARG, "ks_dev_destroy: %d handle(s) still share this handle's hints; "
                     "destroy them first", h->sharers);
     if (h->seg_owner) h->seg_owner->sharers--;
-    void* ps[] = {h->kg, h->P, h->sl, h->dV, h->cols, h->own_cols, h->slots,
+    void* ps[] = {h->kg, h->kgt, h->P, h->sl, h->dV, h->cols, h->own_cols, h->slots,
                   h->seg_owner ? nullptr : h->seg, h->cols_int, h->cols_bnd, h->copy_cnt};
     for (void* q : ps)
         if (q) (void)hipFree(q);
@@ -137,6 +139,7 @@ int ks_dev_create_slice(const double* k_grid, const double* K_grid, const double
     const size_t n = (size_t)nk * nK * 4;
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = hipMalloc((void**)&h->kg, nk * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc((void**)&h->kgt, 3 * nk * sizeof(double));
     if (e == hipSuccess) e = hipMalloc((void**)&h->P, sizeof Pr);
     if (e == hipSuccess) e = hipMalloc((void**)&h->sl, sl.size() * sizeof(KsSlice));
     if (e == hipSuccess) e = hipMalloc((void**)&h->dV, n * sizeof(double));
@@ -148,6 +151,8 @@ int ks_dev_create_slice(const double* k_grid, const double* K_grid, const double
     if (e == hipSuccess) e = hipMalloc((void**)&h->copy_cnt, 2 * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(h->copy_cnt, 0, 2 * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemcpy(h->kg, k_grid, nk * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_ks_grid_tables(h->kg, (int)nk, h->kgt, nullptr) == AIY_OK
+                                 ? hipStreamSynchronize(nullptr) : hipErrorLaunchFailure;
     if (e == hipSuccess) e = hipMemcpy(h->P, Pr, sizeof Pr, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->sl, sl.data(), sl.size() * sizeof(KsSlice), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->cols, cols.data(), cols.size() * sizeof(int), hipMemcpyHostToDevice);

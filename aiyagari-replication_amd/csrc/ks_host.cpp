@@ -55,7 +55,7 @@ void ks_slices(const KsParams& p, const double* B, const double* K_grid, int nK,
 }
 
 struct KsDev {
-    double *kg, *P, *V, *V2, *dV, *dV2, *Vold, *kopt;
+    double *kg, *kgt, *P, *V, *V2, *dV, *dV2, *Vold, *kopt;
     int* nfev;
     int* seg;  // Howard segment hints (verified before use, so never initialised)
     KsSlice* sl;
@@ -76,6 +76,7 @@ static int ks_stage(HostCtx* c, const double* value, const double* k_opt, const 
     ks_slices(p, B, K_grid, (int)nK, sl);
     size_t n = (size_t)nk * nK * 4, nb = n * sizeof(double);
     AIY_TRY(c->buf("ks_kg", nk * sizeof(double), (void**)&D.kg));
+    AIY_TRY(c->buf("ks_kgt", 3 * nk * sizeof(double), (void**)&D.kgt));
     AIY_TRY(c->buf("ks_P", 16 * sizeof(double), (void**)&D.P));
     AIY_TRY(c->buf("ks_V", nb, (void**)&D.V));
     AIY_TRY(c->buf("ks_V2", nb, (void**)&D.V2));
@@ -92,6 +93,7 @@ static int ks_stage(HostCtx* c, const double* value, const double* k_opt, const 
     for (int i = 0; i < 4; ++i)
         for (int m = 0; m < 4; ++m) Pr[i * 4 + m] = P[i + m * 4];
     AIY_HIP(hipMemcpyAsync(D.kg, k_grid, nk * sizeof(double), hipMemcpyHostToDevice, c->st));
+    AIY_TRY(launch_ks_grid_tables(D.kg, (int)nk, D.kgt, c->st));
     AIY_HIP(hipMemcpyAsync(D.P, Pr, sizeof Pr, hipMemcpyHostToDevice, c->st));
     AIY_HIP(hipMemcpyAsync(D.V, value, nb, hipMemcpyHostToDevice, c->st));
     if (k_opt) AIY_HIP(hipMemcpyAsync(D.kopt, k_opt, nb, hipMemcpyHostToDevice, c->st));
@@ -99,7 +101,7 @@ static int ks_stage(HostCtx* c, const double* value, const double* k_opt, const 
     AIY_HIP(hipStreamSynchronize(c->st));
     A = KsArgs{};
     A.nk = (int)nk; A.nK = (int)nK; A.node0 = 0; A.n_local = (int)n;
-    A.k_grid = D.kg; A.P = D.P; A.slice = D.sl;
+    A.k_grid = D.kg; A.kg_tab = D.kgt; A.P = D.P; A.slice = D.sl;
     A.beta = p.beta; A.k_min = p.k_min; A.k_max = p.k_max;
     A.seg_hint = D.seg;
     return AIY_OK;

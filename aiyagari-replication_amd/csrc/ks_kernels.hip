@@ -174,8 +174,14 @@ __global__ void ks_slopes_kernel(KsArgs A, const double* __restrict__ V, double*
     if (q >= A.nk) return;
     for (int c = blockIdx.y; c < 4 * A.nK; c += gridDim.y) {
         const size_t col = (size_t)c * A.nk;
-        dV[col + q] = pchip_slope(A.k_grid, V + col, A.nk, q);
+        dV[col + q] = A.kg_tab ? pchip_slope_tab(A.k_grid, V + col, A.nk, q, A.kg_tab)
+                               : pchip_slope(A.k_grid, V + col, A.nk, q);
     }
+}
+
+__global__ void ks_grid_tables_kernel(const double* __restrict__ kg, int nk, double* __restrict__ tab) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < nk) pchip_grid_tables(kg, nk, q, tab);
 }
 
 // slopes for a list of columns only (the columns a shard reads)
@@ -185,7 +191,8 @@ __global__ void ks_slopes_cols_kernel(KsArgs A, const int* __restrict__ cols, in
     if (q >= A.nk) return;
     for (int c = blockIdx.y; c < ncols; c += gridDim.y) {
         const size_t col = (size_t)cols[c] * A.nk;
-        dV[col + q] = pchip_slope(A.k_grid, V + col, A.nk, q);
+        dV[col + q] = A.kg_tab ? pchip_slope_tab(A.k_grid, V + col, A.nk, q, A.kg_tab)
+                               : pchip_slope(A.k_grid, V + col, A.nk, q);
     }
 }
 
@@ -287,7 +294,8 @@ __device__ __forceinline__ void howard_slopes_col(const KsArgs& A, const KsView&
     s_v[threadIdx.x] = v;
     __syncthreads();
     if (mine) {
-        const double d = pchip_slope_t(A.k_grid, yl, nk, q);
+        const double d = A.kg_tab ? pchip_slope_tab(A.k_grid, yl, nk, q, A.kg_tab)
+                                  : pchip_slope_t(A.k_grid, yl, nk, q);
         if (WT) {  // staged direct schedule: peers copy these columns once the next launch has
             // published — stored write-through (system-scope vector stores), so they are in
             // memory when this kernel ends
@@ -607,6 +615,11 @@ static dim3 ks_col_grid(int nk, long long ncols, int nz = 1) {
 }
 int launch_ks_slopes(const KsArgs& A, const double* V, double* dV, hipStream_t st) {
     ks_slopes_kernel<<<ks_col_grid(A.nk, 4ll * A.nK), ks_col_block(A.nk), 0, st>>>(A, V, dV);
+    AIY_HIP(hipGetLastError());
+    return AIY_OK;
+}
+int launch_ks_grid_tables(const double* kg, int nk, double* tab, hipStream_t st) {
+    ks_grid_tables_kernel<<<(nk + 255) / 256, 256, 0, st>>>(kg, nk, tab);
     AIY_HIP(hipGetLastError());
     return AIY_OK;
 }

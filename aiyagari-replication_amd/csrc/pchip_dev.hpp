@@ -8,6 +8,21 @@ namespace aiy {
 
 __device__ __forceinline__ int sgn_dev(double x) { return (x > 0) - (x < 0); }
 
+// RN(a / b) for b > 0 from rb = RN(1 / b): q = RN(a·rb), then two residual corrections
+// q += fma(−q, b, a)·rb (Markstein: with rb correctly rounded and q faithful, the corrected
+// quotient is the correctly rounded one — no overflow or underflow here: grid spans and value
+// differences; tools/micro/fastdiv_check.c: 2·10⁸ random and adversarial pairs, one correction
+// misses 1, two miss 0).  A zero numerator keeps its sign, as IEEE a / b does for b > 0.  Five
+// dependent fp64 operations instead of the eleven of the IEEE division sequence.
+__device__ __forceinline__ double div_by_rcp(double a, double b, double rb) {
+    double q = a * rb;
+    double e = __builtin_fma(-q, b, a);
+    q = __builtin_fma(e, rb, q);
+    e = __builtin_fma(-q, b, a);
+    q = __builtin_fma(e, rb, q);
+    return a == 0.0 ? a : q;
+}
+
 // pchip slope at point q of a column (x = k_grid), MATLAB pchipslopes.  y is anything
 // indexable by the column's node index: a column pointer, or a window staged in LDS (LdsCol).
 template <class Y>
@@ -47,6 +62,42 @@ __device__ inline double pchip_slope(const double* __restrict__ x, const double*
                                      int n, int q) {
     return pchip_slope_t(x, y, n, q);
 }
+
+// the grid's slope tables (ks_grid_tables): rcp[i] = RN(1 / (x[i+1] − x[i])), i < n − 1, then
+// w[2q], w[2q + 1] = the interior weights (h1 + hs) / (3·hs), (hs + h2) / (3·hs) of node q — the
+// values pchip_slope_t computes, computed once per grid
+__device__ __forceinline__ void pchip_grid_tables(const double* __restrict__ x, int n, int q,
+                                                  double* __restrict__ tab) {
+    if (q < n - 1) tab[q] = 1.0 / (x[q + 1] - x[q]);
+    if (q >= 1 && q < n - 1) {
+        const int k = q - 1;
+        double h1 = x[k + 1] - x[k], h2 = x[k + 2] - x[k + 1];
+        double hs = h1 + h2;
+        tab[n + 2 * q] = (h1 + hs) / (3 * hs);
+        tab[n + 2 * q + 1] = (hs + h2) / (3 * hs);
+    }
+}
+// pchip_slope_t with the grid tables: the two interval slopes divide by the tabled reciprocals
+// (div_by_rcp, correctly rounded), the weights are read, and of d1/dmax, d2/dmax the one whose
+// magnitude is dmax is ±1 exactly — three IEEE divisions instead of seven, the same values
+template <class Y>
+__device__ inline double pchip_slope_tab(const double* __restrict__ x, const Y& y, int n, int q,
+                                         const double* __restrict__ tab) {
+    if (q == 0 || q == n - 1) return pchip_slope_t(x, y, n, q);
+    int k = q - 1;
+    double h1 = x[k + 1] - x[k], h2 = x[k + 2] - x[k + 1];
+    double d1 = div_by_rcp(y[k + 1] - y[k], h1, tab[k]);
+    double d2 = div_by_rcp(y[k + 2] - y[k + 1], h2, tab[k + 1]);
+    if (sgn_dev(d1) * sgn_dev(d2) > 0) {
+        const double w1 = tab[n + 2 * q], w2 = tab[n + 2 * q + 1];
+        double dmax = fmax(fabs(d1), fabs(d2));
+        double dmin = fmin(fabs(d1), fabs(d2));
+        const double t1 = fabs(d1) == dmax ? copysign(1.0, d1) : d1 / dmax;
+        const double t2 = fabs(d2) == dmax ? copysign(1.0, d2) : d2 / dmax;
+        return dmin / (w1 * t1 + w2 * t2);
+    }
+    return 0.0;
+}
 // nodes [lo, lo + len) of a column staged in LDS, indexed by node
 struct LdsCol {
     const double* p;
@@ -65,21 +116,6 @@ __device__ __forceinline__ double col_ld(const double* p) {
             __HIP_MEMORY_SCOPE_AGENT));
     else
         return *p;
-}
-
-// RN(a / b) for b > 0 from rb = RN(1 / b): q = RN(a·rb), then two residual corrections
-// q += fma(−q, b, a)·rb (Markstein: with rb correctly rounded and q faithful, the corrected
-// quotient is the correctly rounded one — no overflow or underflow here: grid spans and value
-// differences; tools/micro/fastdiv_check.c: 2·10⁸ random and adversarial pairs, one correction
-// misses 1, two miss 0).  A zero numerator keeps its sign, as IEEE a / b does for b > 0.  Five
-// dependent fp64 operations instead of the eleven of the IEEE division sequence.
-__device__ __forceinline__ double div_by_rcp(double a, double b, double rb) {
-    double q = a * rb;
-    double e = __builtin_fma(-q, b, a);
-    q = __builtin_fma(e, rb, q);
-    e = __builtin_fma(-q, b, a);
-    q = __builtin_fma(e, rb, q);
-    return a == 0.0 ? a : q;
 }
 
 // pwch coefficients + ppval Horner on segment i; rh = RN(1 / h) of the segment (the forecast
