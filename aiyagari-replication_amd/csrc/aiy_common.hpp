@@ -117,6 +117,23 @@ __device__ __forceinline__ int seg_of_dev(const double* __restrict__ x, int n, d
     return i;
 }
 
+// seg_of_dev(x, n, q) searched inside segments [lo_s, hi_s] only, when q provably lies there
+// (x[lo_s] <= q unless lo_s == 0, q < x[hi_s + 1] unless hi_s == n - 2): the same answer in
+// log2(hi_s - lo_s) dependent loads; otherwise (or for NaN q) the full search
+__device__ __forceinline__ int seg_range_dev(const double* __restrict__ x, int n, double q,
+                                             int lo_s, int hi_s) {
+    const bool ok = (lo_s <= 0 || x[lo_s] <= q) && (hi_s >= n - 2 || q < x[hi_s + 1]) && q == q &&
+                    lo_s <= hi_s;
+    if (!ok) return seg_of_dev(x, n, q);
+    int lo = max(lo_s, 0) + 1, hi = min(hi_s, n - 2) + 1;
+    while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (x[mid] <= q) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo - 1;
+}
+
 // IEEE-ordered key for a non-negative double: uint64 compare == double compare
 __device__ __forceinline__ unsigned long long nonneg_key(double x) {
     return (unsigned long long)aiy_dbits(x);

@@ -46,13 +46,18 @@ __device__ __forceinline__ int seg_hinted_dev(const double* __restrict__ x, int 
     return seg_of_dev(x, n, q);
 }
 
+// hint: a guess of the segment (verified); [slo, shi]: segments the answer provably lies in
+// when the checks of seg_range_dev pass (fminbnd's bracket); seg_out: the segment used
 template <bool SC1 = false>
 __device__ __forceinline__ double ks_bellman_dev(const KsArgs& A, const KsView& W,
                                                  const KsSlice& sl, int si, double k, double kp,
-                                                 int hint = -1) {
+                                                 int hint = -1, int slo = -1, int shi = -1,
+                                                 int* seg_out = nullptr) {
     const int nk = A.nk;
     double kq = fmax(fmin(kp, W.kg[nk - 1]), W.kg[0]);
-    int seg = hint >= 0 ? seg_hinted_dev(W.kg, nk, kq, hint) : seg_of_dev(W.kg, nk, kq);
+    int seg = hint >= 0 ? seg_hinted_dev(W.kg, nk, kq, hint)
+                        : (slo >= 0 ? seg_range_dev(W.kg, nk, kq, slo, shi) : seg_of_dev(W.kg, nk, kq));
+    if (seg_out) *seg_out = seg;
     double expec = 0;
     const double h = W.kg[seg + 1] - W.kg[seg], rh = 1.0 / h;  // the four queries' segment
 #pragma unroll
@@ -69,14 +74,19 @@ __device__ __forceinline__ double ks_bellman_dev(const KsArgs& A, const KsView& 
 }
 
 // MATLAB fminbnd on −bellman over [ax, bx]
+// Every evaluation after the first lies in the bracket [a, b] whose ends are evaluated points
+// (or the interval's ends), so its segment is searched between theirs (sa, sb) — verified by
+// seg_range_dev, so the segments, hence the values, are the full search's.
 __device__ double ks_fminbnd_dev(const KsArgs& A, const KsView& W, const KsSlice& sl, int si,
                                  double k, double ax, double bx, int* nfev) {
-#define F(X) (-ks_bellman_dev(A, W, sl, si, k, (X)))
+    int sa = 0, sb = A.nk - 2, su = 0;
+#define F(X) (-ks_bellman_dev(A, W, sl, si, k, (X), -1, sa, sb, &su))
     const double seps = 1.4901161193847656e-08;  // sqrt(eps)
     const double tolx = 1e-4;
     const double cg = 0.5 * (3.0 - 2.23606797749978969641);  // 0.5*(3 - sqrt(5))
     double a = ax, b = bx, v = a + cg * (b - a), w = v, xf = v, d = 0, e = 0, x = xf;
     double fx = F(x);
+    int sxf = su;
     int num = 1, it = 0;
     double fv = fx, fw = fx, xm = 0.5 * (a + b);
     double tol1 = seps * fabs(xf) + tolx / 3.0, tol2 = 2.0 * tol1;
@@ -113,14 +123,14 @@ __device__ double ks_fminbnd_dev(const KsArgs& A, const KsView& W, const KsSlice
         ++num;
         ++it;
         if (fu <= fx) {
-            if (x >= xf) a = xf;
-            else b = xf;
+            if (x >= xf) a = xf, sa = sxf;
+            else b = xf, sb = sxf;
             v = w; fv = fw;
             w = xf; fw = fx;
-            xf = x; fx = fu;
+            xf = x; fx = fu; sxf = su;
         } else {
-            if (x < xf) a = x;
-            else b = x;
+            if (x < xf) a = x, sa = su;
+            else b = x, sb = su;
             if (fu <= fw || w == xf) {
                 v = w; fv = fw;
                 w = x; fw = fu;
