@@ -705,15 +705,23 @@ __device__ __forceinline__ int par_zpath(const SimArgs& A, unsigned char* zp, un
     return *s_stop;
 }
 
-// one wave: segment [Ts, Tn) of the k recurrence from k, stored (lane 0) into kp
+// one wave: segment [Ts, Tn) of the k recurrence from k into kp — each step's value parked in
+// lane (t − cb) of a register, 64 of them stored together (no per-step store or exec change)
 template <int SS, class ZO>
 __device__ __forceinline__ void par_segment(ParStepper<SS>& ps, double k, int Ts, int Tn,
                                             const ZO& zo_of, double* kp, int lane) {
     if (AIY_PAR_PROBE == 3) return;
+    double buf = 0.0;
+    int cb = Ts;
     for (int t = Ts; t < Tn; ++t) {
         k = ps.step(k, zo_of(t), zo_of(t + 1));
-        if (lane == 0) kp[t] = k;
+        buf = lane == t - cb ? k : buf;
+        if (t - cb == 63) {
+            kp[cb + lane] = buf;
+            cb += 64;
+        }
     }
+    if (cb < Tn && lane < Tn - cb) kp[cb + lane] = buf;
 }
 
 // one wave: repair segment [Ts, Tn) from k (its predecessor's end): step until the value equals
@@ -922,14 +930,14 @@ __global__ __launch_bounds__(kParSegThreads) void sim_par_seg_kernel(SimArgs A0)
         return;
     }
     extern __shared__ double lds[];
-    __shared__ unsigned char zs[kParSlice];
+    __shared__ int zs[kParSlice];  // the segment's row byte offsets (0 past Te)
     const unsigned char* zg = par_zg(A0, c);
-    for (int t = Ts + tid; t <= Tn; t += kParSegThreads) zs[t - Ts] = t < Te ? zg[t] : 0;
+    const int zrow = SS * 16;
+    for (int t = Ts + tid; t <= Tn; t += kParSegThreads) zs[t - Ts] = t < Te ? (int)zg[t] * zrow : 0;
     par_tables<SS>(A, lds, tid, kParSegThreads);
     __syncthreads();
     if (tid >= 64) return;
-    const int zrow = SS * 16;
-    auto zo_of = [&](int t) __attribute__((always_inline)) { return t < Te ? (int)zs[t - Ts] * zrow : 0; };
+    auto zo_of = [&](int t) __attribute__((always_inline)) { return zs[t - Ts]; };
     ParStepper<SS> ps{lds, lds + SS, lds + 2 * SS, A.Na, A.Na - 64, lane, 0, false, 0.0, 0.0, 0.0, 0.0};
     if (!FIX) {
         par_segment(ps, A.k1, Ts, Tn, zo_of, kp, lane);
