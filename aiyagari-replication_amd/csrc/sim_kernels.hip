@@ -733,11 +733,13 @@ template <int SS, class ZO>
 __device__ __forceinline__ int par_repair(ParStepper<SS>& ps, double k, int Ts, int Tn,
                                           const ZO& zo_of, double* kp, int lane) {
     ps.primed = false;
-    int cb = Ts, chg = 0;
+    int cb = Ts, chg = 0, t = Ts;
     double sv = Ts + lane < Tn ? kp[Ts + lane] : 0.0;
     double sn = Ts + 64 + lane < Tn ? kp[Ts + 64 + lane] : 0.0;
-    for (int t = Ts; t < Tn; ++t) {
+    double buf = 0.0;  // the rewritten values of chunk cb, one per lane, stored together
+    for (; t < Tn; ++t) {
         if (t - cb == 64) {
+            kp[cb + lane] = buf;  // the chunk before: every step of it was rewritten
             cb = t;
             sv = sn;
             sn = cb + 64 + lane < Tn ? kp[cb + 64 + lane] : 0.0;
@@ -747,9 +749,10 @@ __device__ __forceinline__ int par_repair(ParStepper<SS>& ps, double k, int Ts, 
         const unsigned long long sb =
             __builtin_bit_cast(unsigned long long, readlane_d(sv, t - cb));
         if (kb == sb) break;  // the stored path is the true one from here
-        if (lane == 0) kp[t] = k;
+        buf = lane == t - cb ? k : buf;
         if (t == Tn - 1) chg = 1;
     }
+    if (lane < t - cb) kp[cb + lane] = buf;  // the rewritten part of the last chunk
     return chg;
 }
 
