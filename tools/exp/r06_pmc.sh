@@ -28,7 +28,7 @@ run a1_400;   summ a1_400 bell_wide_kernel 0 0 a1_na400
 run ks;       summ ks ks_howard_slopes_xcd_kernel 0 0 ks_howard_slopes
 run egm;      summ egm egm_chain_kernel 0 200 egm_chain; summ egm egm_chain_kernel 200 200 labor_egm_chain
 run dist;     summ dist dist_push_kernel 0 0 dist_push
-run sim;      summ sim sim_chain_par_kernel 0 0 sim_chain_par
+run sim;      summ sim "sim_par_seg_kernel<512, false>" 0 0 sim_par_seg
 for f in $O/pmc_*.json; do python3 -c "import json; d=json.load(open('$f')); print('$f', d['launches'], json.dumps({k: round(v, 3) for k, v in d['derived'].items() if k in ('valu_busy','waves_per_simd','wait_frac','kernel_cycles')}))"; done
 for f in $O/traffic_*.json; do python3 -c "import json; d=json.load(open('$f')); print('$f', d.get('bytes_per_launch'))"; done
 echo "r06 pmc done"

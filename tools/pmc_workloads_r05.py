@@ -14,7 +14,7 @@ launches of the kernel it is about (VERDICT r4 "do this" 1):
   egm       egm_chain_kernel  — A4 then A5 solve loops at Na = 20,000, 200 chained steps each:
                                 take 200 / skip 200 take 200
   dist      dist_push_kernel  — 64 pushes on the r = 0.04 policy at Na = 20,000 (bench `dist`)
-  sim       sim_chain_par_kernel — (round 6) 20 capital-supply chains of T = 10,000 on the
+  sim       sim_par_seg_kernel — (round 6) 20 capital-supply chains of T = 10,000 on the
                                 Na = 400 policy at r = 0.04 (the GE loop's chain), K_s only
 (round 6: the same workloads, tools/exp/r06_pmc.sh; `ks` now times ks_howard_slopes_xcd_kernel)
 """
