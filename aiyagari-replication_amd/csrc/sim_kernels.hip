@@ -663,10 +663,14 @@ __device__ __forceinline__ int par_zpath(const SimArgs& A, unsigned char* zp, un
     if (tid == 0) *s_stop = T;
     __syncthreads();
     const int nst = T - 1;               // steps 1 .. T-1 use u[t - 1]
-    const int ch = (nst + 1023) / 1024;  // steps per thread
+    const int ch = (nst + 1023) / 1024;  // steps per thread (<= 16: T <= kParMaxT)
     const int t0 = 1 + tid * ch, t1 = min(T, t0 + ch);
+    constexpr int kCh = (kParMaxT + 1022) / 1024;
+    double ub[kCh];  // this thread's draws, all loads in flight together (both passes use them)
+#pragma unroll
+    for (int j = 0; j < kCh; ++j) ub[j] = t0 + j < t1 ? A.U[t0 + j - 1] : 0.0;
     auto zmap = [&](int t) __attribute__((always_inline)) -> unsigned {
-        const double u = A.U[t - 1];
+        const double u = ub[t - t0];
         unsigned M = 7u << 21;  // entry 7 -> 7 (absorbing "find() empty")
 #pragma unroll
         for (int z = 0; z < 7; ++z) {
@@ -682,7 +686,9 @@ __device__ __forceinline__ int par_zpath(const SimArgs& A, unsigned char* zp, un
 #pragma unroll
     for (int z = 0; z < 8; ++z) agg |= (unsigned)z << (3 * z);  // identity
     const unsigned ident = agg;
-    for (int t = t0; t < t1; ++t) agg = zmap_compose(agg, zmap(t));
+#pragma unroll
+    for (int j = 0; j < kCh; ++j)
+        if (t0 + j < t1) agg = zmap_compose(agg, zmap(t0 + j));
     s_map[tid] = agg;
     __syncthreads();
     for (int off = 1; off < 1024; off <<= 1) {  // inclusive scan of the compositions
@@ -694,10 +700,14 @@ __device__ __forceinline__ int par_zpath(const SimArgs& A, unsigned char* zp, un
     const unsigned pre = tid > 0 ? s_map[tid - 1] : ident;
     int z = (int)((pre >> (3 * A.z1)) & 7u);
     int first_bad = T;
-    for (int t = t0; t < t1; ++t) {
-        z = (int)((zmap(t) >> (3 * z)) & 7u);
-        zp[t] = (unsigned char)z;
-        if (z == 7 && first_bad == T) first_bad = t;
+#pragma unroll
+    for (int j = 0; j < kCh; ++j) {
+        const int t = t0 + j;
+        if (t < t1) {
+            z = (int)((zmap(t) >> (3 * z)) & 7u);
+            zp[t] = (unsigned char)z;
+            if (z == 7 && first_bad == T) first_bad = t;
+        }
     }
     if (first_bad < T) atomicMin(s_stop, first_bad);
     if (tid == 0) zp[0] = (unsigned char)A.z1;
