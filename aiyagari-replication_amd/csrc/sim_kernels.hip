@@ -821,8 +821,22 @@ __device__ __forceinline__ void par_passes_sum(const SimArgs& A, ParStepper<SS>&
             const double vn = c0 + 64 + lane < Te ? kp[c0 + 64 + lane] : 0.0;
             const int n = min(64, Te - c0);
             if (n == 64 && c0 > 0) {
+                // 16 values read back per group into distinct registers before their adds, the
+                // next group's while these add: the dependent adds wait only on each other
+                double x[16], y[16];
 #pragma unroll
-                for (int j = 0; j < 64; ++j) sum = sum + readlane_d(v, j);
+                for (int j = 0; j < 16; ++j) x[j] = readlane_d(v, j);
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    if (g < 3) {
+#pragma unroll
+                        for (int j = 0; j < 16; ++j) y[j] = readlane_d(v, 16 * (g + 1) + j);
+                    }
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) sum = sum + x[j];
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) x[j] = y[j];
+                }
             } else {
                 for (int j = c0 == 0 ? 1 : 0; j < n; ++j) sum = sum + readlane_d(v, j);
             }
